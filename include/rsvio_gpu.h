@@ -1,0 +1,195 @@
+/*
+ * rsvio_gpu.h -- C ABI of the MI355X (gfx950) implementation of RS-VIO's two hot paths.
+ *
+ * The reference (EthanD11/RS-VIO) is a pure-Rust crate with no FFI layer; its drop-in
+ * boundary is the Rust API the estimator calls.  Every entry point below names the
+ * reference item it replaces (file:line under the reference root).  INTEGRATION.md
+ * shows the `extern "C"` block and safe wrapper a Rust maintainer binds to it.
+ *
+ * Conventions
+ *  - Every function returns int: RSVIO_OK (0) or a negative RSVIO_ERR_* code;
+ *    rsvio_last_error() returns a thread-local message.  Nothing aborts or unwinds.
+ *  - Per-feature failure is valid = 0 (the reference's Option::None / false).
+ *  - Host buffers are borrowed for the duration of the call only.  Device memory is
+ *    owned by the handle and released by *_destroy.
+ *  - A handle is single-threaded (mirrors `&mut self`); distinct handles may run
+ *    concurrently on distinct HIP streams.
+ *  - Affine2<f32> state is float[6] = {m11, m12, m21, m22, m13, m23}.
+ *  - Pyramids are packed: level i is (w >> i) x (h >> i) u8, levels back to back.
+ *  - SE3 poses are 7-vectors {tx, ty, tz, qw, qx, qy, qz} of T_B_W
+ *    (src/estimator/sliding_window.rs:222-224).
+ */
+#ifndef RSVIO_GPU_H
+#define RSVIO_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    RSVIO_OK = 0,
+    RSVIO_ERR_INVALID_ARG = -1,
+    RSVIO_ERR_HIP = -2,
+    RSVIO_ERR_NOMEM = -3,
+    RSVIO_ERR_CAPACITY = -4,
+    RSVIO_ERR_NO_DEVICE = -5,
+    RSVIO_ERR_INTERNAL = -6,
+    RSVIO_ERR_RCCL = -7
+};
+
+/* Thread-local message for the last failing call on this thread. */
+const char* rsvio_last_error(void);
+/* Library / device identification; returns RSVIO_ERR_NO_DEVICE if no gfx950 is visible. */
+int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus);
+
+/* =============================== HP-T: patch tracker =============================== */
+
+typedef struct {
+    int32_t width, height;
+    int32_t levels;                 /* StereoPatchTracker<LEVELS> (estimator.rs:27 uses 6) */
+    int32_t grid_size;              /* config/euroc_vio.yaml:42 */
+    int32_t max_iterations;         /* optical_flow_max_iterations (:44) */
+    float convergence_threshold;    /* optical_flow_convergence_threshold (:45), f64->f32 (feature_tracker.rs:112) */
+    int32_t device;
+    int32_t max_features;           /* per-camera capacity of the track maps (0 -> 4096) */
+} rsvio_tracker_params;
+
+/* One tracked point: id + Affine2 state (pixel position = m13, m23). */
+typedef struct {
+    uint64_t id;
+    float x, y;       /* m13, m23 */
+    float r[4];       /* m11, m12, m21, m22 */
+} rsvio_feature;
+
+typedef struct rsvio_tracker rsvio_tracker;
+
+/* StereoPatchTracker::<N>::new(grid_size, max_iters, thresh)  (src/feature_tracker/feature_tracker.rs:103-114) */
+int rsvio_tracker_create(const rsvio_tracker_params* params, rsvio_tracker** out);
+void rsvio_tracker_destroy(rsvio_tracker* t);
+
+/* StereoPatchTracker::process_frame(&mut self, &GrayImage, &GrayImage, &mut Frame) (:116-187)
+ * followed by get_track_points (:188-200).  Images are u8, row stride `stride` bytes.
+ * Outputs are sorted by ascending id (canonical order; the reference iterates HashMaps).
+ * New ids are assigned in detection scan order (image_utilities.rs:141-142). */
+int rsvio_tracker_process_frame(rsvio_tracker* t, const uint8_t* left, const uint8_t* right,
+                                size_t stride, rsvio_feature* out_l, size_t cap_l, size_t* n_l,
+                                rsvio_feature* out_r, size_t cap_r, size_t* n_r);
+/* Same, with both images already in device memory (tightly packed w x h). */
+int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left,
+                                       const uint8_t* d_right, rsvio_feature* out_l,
+                                       size_t cap_l, size_t* n_l, rsvio_feature* out_r,
+                                       size_t cap_r, size_t* n_r);
+/* StereoPatchTracker::remove_id (:201-206) */
+int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n);
+/* HIP stream the tracker enqueues on (hipStream_t) */
+void* rsvio_tracker_stream(rsvio_tracker* t);
+
+/* ---- parity-level entry points (host buffers in/out) ---- */
+
+size_t rsvio_pyramid_bytes(int32_t w, int32_t h, int32_t levels);
+/* build_image_pyramid (feature_tracker.rs:209-220): imageops::resize Triangle per level */
+int rsvio_build_pyramid(const uint8_t* img, int32_t w, int32_t h, int32_t levels, uint8_t* out);
+/* track_points (feature_tracker.rs:252-291): forward, backward and ||dt||^2 < 0.4 per feature.
+ * aff_out receives the forward result for valid features (aff_in copied otherwise). */
+int rsvio_track_points(const uint8_t* pyr0, const uint8_t* pyr1, int32_t w, int32_t h,
+                       int32_t levels, const float* aff_in, int32_t n, int32_t max_iterations,
+                       float thresh, float* aff_out, uint8_t* valid_out);
+/* detect_key_points(img, grid, current, 1) (image_utilities.rs:108-175) with the existing
+ * tracks' positions (rounded as feature_tracker.rs:232-233).  out_xy: u32 (x, y) pairs. */
+int rsvio_detect_keypoints(const uint8_t* img, int32_t w, int32_t h, int32_t grid,
+                           const float* existing_xy, int32_t n_existing, uint32_t* out_xy,
+                           float* out_score, int32_t cap, int32_t* n_out);
+
+/* ---- device-pointer entry points (enqueue on `stream`, no synchronisation) ---- */
+typedef struct rsvio_track_ctx rsvio_track_ctx;
+/* Holds the per-(w,h,levels) resampling tables on device. */
+int rsvio_track_ctx_create(int32_t w, int32_t h, int32_t levels, int32_t device, rsvio_track_ctx** out);
+void rsvio_track_ctx_destroy(rsvio_track_ctx* c);
+/* n_img images (each w x h, packed) -> n_img pyramids (each rsvio_pyramid_bytes, packed) */
+int rsvio_build_pyramids_d(rsvio_track_ctx* c, const uint8_t* d_imgs, int32_t n_img,
+                           uint8_t* d_pyrs, void* stream);
+/* Up to 4 independent track_points batches in one launch. */
+typedef struct {
+    const uint8_t* d_pyr0;
+    const uint8_t* d_pyr1;
+    const float* d_aff_in;
+    float* d_aff_out;
+    uint8_t* d_valid;
+    int32_t n;
+} rsvio_track_batch;
+int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, int32_t n_batches,
+                         int32_t max_iterations, float thresh, void* stream);
+
+/* =========================== HP-B: sliding-window BA =========================== */
+
+enum {
+    RSVIO_LM_COST_TOLERANCE = 1,      /* OptimizationStatus::CostToleranceReached */
+    RSVIO_LM_PARAMETER_TOLERANCE = 2, /* ::ParameterToleranceReached */
+    RSVIO_LM_MAX_ITERATIONS = 3,      /* ::MaxIterationsReached (counts as success, sliding_window.rs:393) */
+    RSVIO_LM_TRUST_REGION = 4,        /* ::TrustRegionRadiusTooSmall */
+    RSVIO_LM_NUMERICAL_FAILURE = -1,  /* ::NumericalFailure -> caller reverts (:354-359) */
+    RSVIO_LM_SKIPPED = -2             /* too few residuals (:309-319) -> Ok(false) */
+};
+
+typedef struct {
+    int32_t max_iterations;       /* 20  (sliding_window.rs:131) */
+    double cost_tolerance;        /* 1e-6 (:132) */
+    double parameter_tolerance;   /* 1e-9 (:133) */
+    double huber_delta;           /* 2.0 (:295) */
+    double lambda_init;           /* 1e-4 (build's LM) */
+} rsvio_lm_cfg;
+
+typedef struct {
+    int32_t status;               /* RSVIO_LM_* ; success iff > 0 (is_optimization_successful :384-395) */
+    int32_t iterations;
+    double initial_cost;
+    double final_cost;
+    double solve_ms;              /* device time of the solve (HIP events) */
+} rsvio_ba_result;
+
+typedef struct {
+    int32_t max_keyframes;        /* window size (config/euroc_vio.yaml:35) */
+    int32_t max_landmarks;
+    int32_t max_observations;
+    int32_t device;
+} rsvio_ba_params;
+
+typedef struct rsvio_ba rsvio_ba;
+
+int rsvio_ba_create(const rsvio_ba_params* params, rsvio_ba** out);
+void rsvio_ba_destroy(rsvio_ba* ba);
+
+/* SlidingWindow::optimize's solver call (sliding_window.rs:325): LM with Schur elimination of
+ * the landmarks on BundleAdjustmentFactor residuals (factors.rs:350-447) + Huber.
+ * Observations: landmark index, keyframe index, camera (0 = left, 1 = right), normalised
+ * undistorted coordinates (frame.rs:118-119).  T_C_B2: two row-major 4x4 (T_Cl_B, T_Cr_B).
+ * pose7 and p_W are updated in place on success (status > 0). */
+int rsvio_ba_solve(rsvio_ba* ba, int32_t n_kf, double* pose7, const uint8_t* kf_fixed,
+                   int32_t n_lm, double* p_W, int32_t n_obs, const int32_t* obs_lm,
+                   const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
+                   const double* T_C_B2, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
+
+/* Split form for device-resident benchmarking: upload once, solve many times from the
+ * uploaded initial state (nothing crosses PCIe inside rsvio_ba_run except the status). */
+int rsvio_ba_set_problem(rsvio_ba* ba, int32_t n_kf, const double* pose7, const uint8_t* kf_fixed,
+                         int32_t n_lm, const double* p_W, int32_t n_obs, const int32_t* obs_lm,
+                         const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
+                         const double* T_C_B2);
+int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
+int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W);
+/* Reduced camera system at `lambda` for the uploaded state (parity tests):
+ * S is n x n row-major (n = 6 * free keyframes, ascending keyframe order), b is n. */
+int rsvio_ba_build_system(rsvio_ba* ba, double lambda, double huber_delta, double* S, double* b,
+                          double* cost);
+
+/* Landmark sharding over ranks: each rank uploads only its own
+ * landmarks/observations; the reduced system and costs are summed with RCCL over xGMI. */
+int rsvio_rccl_unique_id(uint8_t* out, size_t cap);   /* cap >= 128 */
+int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* unique_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

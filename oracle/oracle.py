@@ -1,0 +1,234 @@
+"""ctypes binding of the CPU oracle (oracle/librsvio_oracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module,
+and only as the checker / the timed CPU baseline -- never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "librsvio_oracle.so"
+
+P = C.c_void_p
+
+
+class LmCfg(C.Structure):
+    _fields_ = [("max_iterations", C.c_int), ("cost_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double), ("huber_delta", C.c_double),
+                ("lambda_init", C.c_double)]
+
+
+class BaResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("iterations", C.c_int), ("initial_cost", C.c_double),
+                ("final_cost", C.c_double)]
+
+
+class OrcFeature(C.Structure):
+    _fields_ = [("id", C.c_uint64), ("x", C.c_float), ("y", C.c_float), ("aff", C.c_float * 6)]
+
+
+_SIG = {
+    "orc_set_trig_mode": (None, [C.c_int]),
+    "orc_se2_exp": (None, [P, P]),
+    "orc_pyramid_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "orc_pyramid_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    "orc_build_pyramid": (None, [P, C.c_int, C.c_int, C.c_int, P]),
+    "orc_resize_triangle": (None, [P, C.c_int, C.c_int, P, C.c_int, C.c_int]),
+    "orc_pattern52_new": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
+    "orc_track_one_point": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_int, C.c_float, P]),
+    "orc_track_points": (None, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_int, C.c_int, C.c_float, P, P, C.c_int]),
+    "orc_fast9_scores": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P]),
+    "orc_detect_keypoints": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, C.c_int, P, P, C.c_int]),
+    "orc_tracker_create": (P, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float]),
+    "orc_tracker_destroy": (None, [P]),
+    "orc_tracker_process_frame": (C.c_int, [P, P, P, P, C.c_int, C.POINTER(C.c_int), P, C.c_int,
+                                            C.POINTER(C.c_int)]),
+    "orc_tracker_remove_ids": (None, [P, P, C.c_int]),
+    "orc_ba_factor_linearize": (None, [P, P, P, P, P, P, P]),
+    "orc_ba_build_system": (C.c_int, [C.c_int, P, P, C.c_int, P, C.c_int, P, P, P, P, P, C.c_double,
+                                      C.c_double, P, P, C.POINTER(C.c_double)]),
+    "orc_ba_solve": (C.c_int, [C.c_int, P, P, C.c_int, P, C.c_int, P, P, P, P, P, C.POINTER(LmCfg),
+                               C.POINTER(BaResult)]),
+    "orc_se3_plus": (None, [P, P, P]),
+    "orc_quat_from_rotation": (None, [P, P]),
+}
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        lib = C.CDLL(str(LIB))
+        for k, (r, a) in _SIG.items():
+            f = getattr(lib, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def set_trig_mode(mode: int):
+    load().orc_set_trig_mode(mode)
+
+
+def se2_exp(twist):
+    tw = np.ascontiguousarray(twist, np.float32)
+    out = np.zeros((3, 3), np.float32)
+    load().orc_se2_exp(_p(tw), _p(out))
+    return out
+
+
+def pyramid_bytes(w, h, levels):
+    return int(load().orc_pyramid_bytes(w, h, levels))
+
+
+def build_pyramid(img: np.ndarray, levels: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.empty(pyramid_bytes(w, h, levels), np.uint8)
+    load().orc_build_pyramid(_p(img), w, h, levels, _p(out))
+    return out
+
+
+def resize_triangle(img: np.ndarray, nw: int, nh: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.empty((nh, nw), np.uint8)
+    load().orc_resize_triangle(_p(img), w, h, _p(out), nw, nh)
+    return out
+
+
+def pattern52(img: np.ndarray, px: float, py: float):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    data = np.zeros(52, np.float32)
+    hj = np.zeros((3, 52), np.float32)
+    mean = C.c_float(0)
+    v = load().orc_pattern52_new(_p(img), w, h, px, py, _p(data), _p(hj), C.byref(mean))
+    return bool(v), data, hj, mean.value
+
+
+def track_points(pyr0, pyr1, w, h, levels, aff, max_iterations=20, thresh=0.01, n_threads=1):
+    aff = np.ascontiguousarray(aff, np.float32).reshape(-1, 6)
+    n = aff.shape[0]
+    out = np.empty_like(aff)
+    valid = np.zeros(n, np.uint8)
+    load().orc_track_points(_p(pyr0), _p(pyr1), w, h, levels, _p(aff), n, max_iterations, C.c_float(thresh),
+                            _p(out), _p(valid), n_threads)
+    return out, valid.astype(bool)
+
+
+def fast9_scores(img, threshold):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), np.uint8)
+    load().orc_fast9_scores(_p(img), w, h, threshold, _p(out))
+    return out
+
+
+def detect_key_points(img, grid, existing_xy=None, cap=4096):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    ex = np.zeros((0, 2), np.float32) if existing_xy is None else np.ascontiguousarray(existing_xy, np.float32)
+    out = np.zeros((cap, 2), np.uint32)
+    sc = np.zeros(cap, np.float32)
+    n = load().orc_detect_keypoints(_p(img), w, h, grid, _p(ex) if len(ex) else None, len(ex), _p(out), _p(sc), cap)
+    return out[:n].copy(), sc[:n].copy()
+
+
+class StereoTracker:
+    def __init__(self, w, h, levels=6, grid=50, max_iter=20, thresh=0.01, cap=4096):
+        self.h = load().orc_tracker_create(w, h, levels, grid, max_iter, C.c_float(thresh))
+        self.cap = cap
+        self.ol = (OrcFeature * cap)()
+        self.orr = (OrcFeature * cap)()
+
+    def process_frame(self, left, right):
+        nl, nr = C.c_int(0), C.c_int(0)
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        load().orc_tracker_process_frame(self.h, _p(left), _p(right), C.cast(self.ol, P), self.cap, C.byref(nl),
+                                         C.cast(self.orr, P), self.cap, C.byref(nr))
+
+        def conv(arr, n):
+            return [(int(f.id), float(f.x), float(f.y), tuple(float(v) for v in f.aff)) for f in arr[:n]]
+        return conv(self.ol, nl.value), conv(self.orr, nr.value)
+
+    def remove_ids(self, ids):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        load().orc_tracker_remove_ids(self.h, _p(ids), len(ids))
+
+    def __del__(self):
+        try:
+            load().orc_tracker_destroy(self.h)
+        except Exception:
+            pass
+
+
+def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):
+    return LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init)
+
+
+def ba_solve(prob, cfg=None):
+    """Returns (pose7, p_W, BaResult) after the oracle's LM; prob is a synthetic.BAProblem-like."""
+    cfg = cfg or lm_cfg()
+    pose = np.ascontiguousarray(prob.pose7, np.float64).copy()
+    pw = np.ascontiguousarray(prob.p_W, np.float64).copy()
+    res = BaResult()
+    load().orc_ba_solve(pose.shape[0], _p(pose), _p(np.ascontiguousarray(prob.kf_fixed, np.uint8)), pw.shape[0],
+                        _p(pw), len(prob.obs_lm), _p(prob.obs_lm), _p(prob.obs_kf), _p(prob.obs_cam),
+                        _p(prob.obs_uv), _p(np.ascontiguousarray(prob.T_C_B2, np.float64)), C.byref(cfg),
+                        C.byref(res))
+    return pose, pw, res
+
+
+def ba_build_system(prob, lam, huber_delta=2.0):
+    nfree = int((np.asarray(prob.kf_fixed) == 0).sum())
+    n = 6 * nfree
+    S = np.zeros((n, n))
+    b = np.zeros(n)
+    cost = C.c_double(0)
+    load().orc_ba_build_system(prob.pose7.shape[0], _p(np.ascontiguousarray(prob.pose7)),
+                               _p(np.ascontiguousarray(prob.kf_fixed, np.uint8)), prob.p_W.shape[0],
+                               _p(np.ascontiguousarray(prob.p_W)), len(prob.obs_lm), _p(prob.obs_lm), _p(prob.obs_kf),
+                               _p(prob.obs_cam), _p(prob.obs_uv), _p(np.ascontiguousarray(prob.T_C_B2)), huber_delta,
+                               lam, _p(S), _p(b), C.byref(cost))
+    return S, b, cost.value
+
+
+def factor_linearize(p_W, pose7, T_C_B, uv, T_B_W_fixed=None):
+    r = np.zeros(2)
+    J = np.zeros((2, 9))
+    load().orc_ba_factor_linearize(_p(np.ascontiguousarray(p_W, np.float64)),
+                                   _p(np.ascontiguousarray(pose7, np.float64)) if pose7 is not None else None,
+                                   _p(np.ascontiguousarray(T_B_W_fixed, np.float64)) if T_B_W_fixed is not None else None,
+                                   _p(np.ascontiguousarray(T_C_B, np.float64)),
+                                   _p(np.ascontiguousarray(uv, np.float64)), _p(r), _p(J))
+    return r, J
+
+
+def se3_plus(pose7, delta):
+    out = np.zeros(7)
+    load().orc_se3_plus(_p(np.ascontiguousarray(pose7, np.float64)), _p(np.ascontiguousarray(delta, np.float64)),
+                        _p(out))
+    return out

@@ -1,0 +1,142 @@
+/*
+ * rsvio_oracle.h -- TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+ *
+ * CPU restatement of the two RS-VIO hot paths (EthanD11/RS-VIO, snapshot 2026-03-20),
+ * used only as the parity checker by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py.  The product library (rs-vio_amd/lib/librsvio_gpu.so)
+ * never links or loads it.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - Reference is pure Rust; no cargo/rustc here => the reference cannot be built.
+ *     No golden vectors exist upstream for either path.
+ *   - The oracle is pinned only by the reference's own known-answer tests that apply
+ *     (exp_se2 KATs, feature_tracker/src/feature_tracker/feature_tracking.rs:264-291;
+ *     pyramid dimensions, feature_tracker/src/image_operations.rs:84-94; the
+ *     translation-only BA convergence property, src/optimization/tests.rs:135-380).
+ *     Third-party arithmetic (image::imageops::resize Triangle, imageproc corners_fast9,
+ *     apex-solver LM) is restated from the crates' published algorithms and is
+ *     "parity unpinned".
+ *
+ * Conventions
+ *   Affine2 (nalgebra Affine2<f32>) is passed as float[6] = {m11, m12, m21, m22, m13, m23}.
+ *   Pyramid levels are packed back to back: level i (width w>>i... see orc_pyramid_offset)
+ *   starts at orc_pyramid_offset(w, h, i).
+ *   Poses are 7-vectors [tx, ty, tz, qw, qx, qy, qz] of T_B_W (sliding_window.rs:222-224).
+ */
+#ifndef RSVIO_ORACLE_H
+#define RSVIO_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- tracker (src/feature_tracker/) ---------------- */
+
+/* 0 = glibc sinf/cosf (what Rust f32::sin_cos calls on linux-gnu; default),
+ * 1 = (float)sin((double)x) -- the correctly-rounded form the GPU kernel uses. */
+void orc_set_trig_mode(int mode);
+
+/* se2_exp_matrix (image_utilities.rs:82-106), twist [vx, vy, theta] -> row-major 3x3 */
+void orc_se2_exp(const float* twist, float* out9);
+
+size_t orc_pyramid_offset(int w, int h, int level);
+size_t orc_pyramid_bytes(int w, int h, int levels);
+
+/* feature_tracker.rs:209-220 (imageops::resize Triangle from full resolution per level) */
+void orc_build_pyramid(const uint8_t* img, int w, int h, int levels, uint8_t* out);
+
+/* image 0.25 imageops::resize(.., FilterType::Triangle), u8 luma */
+void orc_resize_triangle(const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh);
+
+/* patch.rs:124-162 -- exposes the template for white-box parity tests.
+ * out_data[52], out_hinvjt[3*52] (row-major 3x52); returns valid flag. */
+int orc_pattern52_new(const uint8_t* img, int w, int h, float px, float py,
+                      float* out_data, float* out_hinvjt, float* out_mean);
+
+/* feature_tracker.rs:344-395; aff in/out float[6]; returns success flag */
+int orc_track_point_at_level(const uint8_t* img, int w, int h, const uint8_t* tmpl_img,
+                             float px, float py, float* aff, int max_iter, float thresh);
+
+/* feature_tracker.rs:292-342; returns 1 and writes aff_out on success */
+int orc_track_one_point(const uint8_t* pyr0, const uint8_t* pyr1, int w, int h, int levels,
+                        const float* aff_in, int max_iter, float thresh, float* aff_out);
+
+/* feature_tracker.rs:252-291 (forward + backward + ||dt||^2 < 0.4 check), per feature */
+void orc_track_points(const uint8_t* pyr0, const uint8_t* pyr1, int w, int h, int levels,
+                      const float* aff_in, int n, int max_iter, float thresh,
+                      float* aff_out, uint8_t* valid_out, int n_threads);
+
+/* imageproc corners_fast9 restatement on a full image: writes score per pixel
+ * (0 = not a corner at `threshold`), returns corner count. */
+int orc_fast9_scores(const uint8_t* img, int w, int h, int threshold, uint8_t* score_out);
+
+/* image_utilities.rs:108-175 with num_points_in_cell = 1.
+ * existing_xy: n_existing x 2 float tracked positions (rounded like feature_tracker.rs:232-233).
+ * out_xy: corner positions (u32 pairs), returns count (<= cap). */
+int orc_detect_keypoints(const uint8_t* img, int w, int h, int grid, const float* existing_xy,
+                         int n_existing, uint32_t* out_xy, float* out_score, int cap);
+
+/* StereoPatchTracker (feature_tracker.rs:91-207) with canonical (ascending id) ordering */
+typedef struct orc_tracker orc_tracker;
+typedef struct {
+    uint64_t id;
+    float x, y;
+    float aff[6];
+} orc_feature;
+orc_tracker* orc_tracker_create(int w, int h, int levels, int grid, int max_iter, float thresh);
+void orc_tracker_destroy(orc_tracker* t);
+/* returns 0; fills up to cap features per camera, counts in n_l/n_r */
+int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t* right,
+                              orc_feature* out_l, int cap_l, int* n_l,
+                              orc_feature* out_r, int cap_r, int* n_r);
+void orc_tracker_remove_ids(orc_tracker* t, const uint64_t* ids, int n);
+
+/* ---------------- bundle adjustment (src/optimization/factors.rs, sliding_window.rs) ---------------- */
+
+typedef struct {
+    int max_iterations;        /* sliding_window.rs:131 -> 20 */
+    double cost_tolerance;     /* :132 -> 1e-6 */
+    double parameter_tolerance;/* :133 -> 1e-9 */
+    double huber_delta;        /* :295 -> 2.0 */
+    double lambda_init;        /* build's own LM -> 1e-4 */
+} orc_lm_cfg;
+
+typedef struct {
+    int status;      /* RSVIO_LM_* codes, shared with include/rsvio_gpu.h */
+    int iterations;
+    double initial_cost;
+    double final_cost;
+} orc_ba_result;
+
+/* factors.rs:350-447 -- one observation; J is 2x9 row-major [dp_W | dt | dw];
+ * pose7 == NULL means "fixed pose" given by T_B_W_fixed (3x4 row-major). */
+void orc_ba_factor_linearize(const double* p_W, const double* pose7, const double* T_B_W_fixed,
+                             const double* T_C_B, const double* uv, double* r, double* J);
+
+/* Reduced camera system at a given lambda for the current parameters.
+ * S is n x n (n = 6 * free KFs, free KFs in ascending KF order), b is n. */
+int orc_ba_build_system(int n_kf, const double* pose7, const uint8_t* kf_fixed,
+                        int n_lm, const double* p_W,
+                        int n_obs, const int32_t* obs_lm, const int32_t* obs_kf,
+                        const uint8_t* obs_cam, const double* obs_uv, const double* T_C_B2,
+                        double huber_delta, double lambda, double* S, double* b, double* cost);
+
+/* Full LM solve (build's restatement of apex-solver LM with Schur elimination). */
+int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed,
+                 int n_lm, double* p_W,
+                 int n_obs, const int32_t* obs_lm, const int32_t* obs_kf,
+                 const uint8_t* obs_cam, const double* obs_uv, const double* T_C_B2,
+                 const orc_lm_cfg* cfg, orc_ba_result* res);
+
+/* SE3 right-plus used by the LM update: pose7 <- pose7 (+) delta ([rho; theta]) */
+void orc_se3_plus(const double* pose7, const double* delta, double* out7);
+
+/* nalgebra UnitQuaternion::from_matrix restatement (sliding_window.rs:221) */
+void orc_quat_from_rotation(const double* R, double* qwxyz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,94 @@
+// common.hpp -- shared helpers for the rsvio_gpu C-ABI library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "rsvio_gpu.h"
+
+namespace rsvio {
+
+void set_last_error(const std::string& msg);
+
+struct HipError {
+    hipError_t err;
+    std::string where;
+};
+
+#define RSVIO_HIP(expr)                                                                    \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            throw ::rsvio::HipError{_e, std::string(#expr) + " @ " + __FILE__ + ":" +      \
+                                            std::to_string(__LINE__)};                     \
+    } while (0)
+
+// Run a C-ABI body, translating exceptions into status codes (never unwinds across the ABI).
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const HipError& e) {
+        set_last_error(std::string("HIP error ") + hipGetErrorString(e.err) + " in " + e.where);
+        return RSVIO_ERR_HIP;
+    } catch (const std::bad_alloc&) {
+        set_last_error("host allocation failed");
+        return RSVIO_ERR_NOMEM;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return RSVIO_ERR_INTERNAL;
+    }
+}
+
+// Pyramid level geometry: level i = (w / 2^i) x (h / 2^i), packed back to back
+// (feature_tracker.rs:215-216).
+__host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }
+__host__ __device__ inline uint32_t level_h(uint32_t h, int i) { return h / (1u << i); }
+__host__ __device__ inline size_t level_offset(uint32_t w, uint32_t h, int level) {
+    size_t off = 0;
+    for (int i = 0; i < level; ++i) off += (size_t)level_w(w, i) * level_h(h, i);
+    return off;
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    void alloc(size_t count) {
+        release();
+        if (count) RSVIO_HIP(hipMalloc(&p, count * sizeof(T)));
+        n = count;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DevBuf() { release(); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+};
+
+// Pinned host staging buffer
+template <class T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void alloc(size_t count) {
+        release();
+        if (count) RSVIO_HIP(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+        n = count;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~HostBuf() { release(); }
+};
+
+}  // namespace rsvio

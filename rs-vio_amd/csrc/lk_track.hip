@@ -1,0 +1,357 @@
+// lk_track.hip -- K2: coarse-to-fine inverse-compositional SE(2) LK with the 52-point pattern,
+// forward + backward + consistency check, one wavefront per feature (gfx950, wave64).
+//
+// Replaces track_points / track_one_point / track_point_at_level
+// (src/feature_tracker/feature_tracker.rs:252-395) and Pattern52::{new, set_data_jac_se2,
+// residual} (src/feature_tracker/patch.rs:75-232).
+//
+// Mapping: lane i < 52 owns pattern point i (its offset, template intensity, its column of
+// H^-1 J^T, its bilinear sample).  Everything the reference sums over the 52 points is summed
+// in the reference's order -- a sequential chain over lanes 0..51 through v_readlane -- so
+// the result is bit-identical to the scalar Rust/oracle arithmetic (no FMA contraction,
+// correctly rounded f32 divide/sqrt).  The only deviation: sin/cos of the SE(2) increment
+// are evaluated in f64 and rounded to f32 (glibc sinf differs from that on < 1e-4 of the
+// |theta| < 2^-6 inputs the tracker produces; DESIGN.md "Tracker parity").
+#include "lk_track.hpp"
+
+namespace rsvio {
+
+namespace {
+
+constexpr int NP = 52;
+
+// patch.rs:19-72 -- the 52-point pattern (pixel offsets before the 1/2 scale of :126)
+__constant__ int8_t kPattern[64][2] = {
+    {-3, 7},  {-1, 7},  {1, 7},   {3, 7},   {-5, 5},  {-3, 5},  {-1, 5},  {1, 5},   {3, 5},
+    {5, 5},   {-7, 3},  {-5, 3},  {-3, 3},  {-1, 3},  {1, 3},   {3, 3},   {5, 3},   {7, 3},
+    {-7, 1},  {-5, 1},  {-3, 1},  {-1, 1},  {1, 1},   {3, 1},   {5, 1},   {7, 1},   {-7, -1},
+    {-5, -1}, {-3, -1}, {-1, -1}, {1, -1},  {3, -1},  {5, -1},  {7, -1},  {-7, -3}, {-5, -3},
+    {-3, -3}, {-1, -3}, {1, -3},  {3, -3},  {5, -3},  {7, -3},  {-5, -5}, {-3, -5}, {-1, -5},
+    {1, -5},  {3, -5},  {5, -5},  {-3, -7}, {-1, -7}, {1, -7},  {3, -7}};
+
+__device__ __forceinline__ float rl(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// acc = 0; acc += v_k, k = 0..51 (Rust `sum += x` loops)
+__device__ __forceinline__ float chain_from_zero(float v) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) acc = acc + rl(v, k);
+    return acc;
+}
+// acc = v_0; acc = v_k + acc, k = 1..51 (nalgebra gemv / gemm column accumulation)
+__device__ __forceinline__ float chain_first(float v) {
+    float acc = rl(v, 0);
+#pragma unroll
+    for (int k = 1; k < NP; ++k) acc = rl(v, k) + acc;
+    return acc;
+}
+
+__device__ __forceinline__ uint32_t sat_u32(float v) {
+    if (!(v > 0.0f)) return 0u;
+    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)v;
+}
+
+struct LevelImg {
+    const uint8_t* __restrict__ p;
+    uint32_t w, h;
+};
+
+// image_utilities.rs:75-80
+__device__ __forceinline__ bool inbound(const LevelImg& im, float x, float y, uint32_t r) {
+    uint32_t xi = sat_u32(roundf(x)), yi = sat_u32(roundf(y));
+    return xi >= r && yi >= r && xi < im.w - r && yi < im.h - r;
+}
+
+__device__ __forceinline__ float px(const LevelImg& im, uint32_t x, uint32_t y) {
+    return (float)im.p[(size_t)y * im.w + x];
+}
+
+// image_utilities.rs:5-66
+__device__ __forceinline__ void image_grad(const LevelImg& im, float x, float y, float out[3]) {
+    uint32_t ix = (uint32_t)floorf(x), iy = (uint32_t)floorf(y);
+    float dx = x - (float)ix, dy = y - (float)iy;
+    float ddx = 1.0f - dx, ddy = 1.0f - dy;
+    float p00 = px(im, ix, iy), p10 = px(im, ix + 1, iy), p01 = px(im, ix, iy + 1), p11 = px(im, ix + 1, iy + 1);
+    float pm0 = px(im, ix - 1, iy), pm1 = px(im, ix - 1, iy + 1);
+    float p20 = px(im, ix + 2, iy), p21 = px(im, ix + 2, iy + 1);
+    float p0m = px(im, ix, iy - 1), p1m = px(im, ix + 1, iy - 1);
+    float p02 = px(im, ix, iy + 2), p12 = px(im, ix + 1, iy + 2);
+    float res0 = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
+    float res_mx = ddx * ddy * pm0 + ddx * dy * pm1 + dx * ddy * p00 + dx * dy * p01;
+    float res_px = ddx * ddy * p10 + ddx * dy * p11 + dx * ddy * p20 + dx * dy * p21;
+    float res_my = ddx * ddy * p0m + ddx * dy * p00 + dx * ddy * p1m + dx * dy * p10;
+    float res_py = ddx * ddy * p01 + ddx * dy * p02 + dx * ddy * p11 + dx * dy * p12;
+    out[0] = res0;
+    out[1] = 0.5f * (res_px - res_mx);
+    out[2] = 0.5f * (res_py - res_my);
+}
+
+// Affine2 as a 3x3 with implicit last row [0 0 1] kept explicitly for exact product order.
+struct Aff {
+    float m00, m01, m02, m10, m11, m12, m20, m21, m22;
+};
+
+// nalgebra 3x3 gemm: C[i][j] = (A[i][0] B[0][j] + A[i][1] B[1][j]) + A[i][2] B[2][j]
+__device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
+    Aff C;
+#define RSV_EL(i, j) ((A.m##i##2 * B.m2##j) + ((A.m##i##1 * B.m1##j) + (A.m##i##0 * B.m0##j)))
+    C.m00 = RSV_EL(0, 0); C.m01 = RSV_EL(0, 1); C.m02 = RSV_EL(0, 2);
+    C.m10 = RSV_EL(1, 0); C.m11 = RSV_EL(1, 1); C.m12 = RSV_EL(1, 2);
+    C.m20 = RSV_EL(2, 0); C.m21 = RSV_EL(2, 1); C.m22 = RSV_EL(2, 2);
+#undef RSV_EL
+    return C;
+}
+
+// image_utilities.rs:82-106, twist [vx, vy, theta]
+__device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
+    float s = (float)sin((double)theta);
+    float c = (float)cos((double)theta);
+    float sin_by, omc_by;
+    if (fabsf(theta) < __FLT_EPSILON__) {
+        float th2 = theta * theta;
+        sin_by = 1.0f - (1.0f / 6.0f) * th2;
+        omc_by = 0.5f * theta - (1.0f / 24.0f) * theta * th2;
+    } else {
+        sin_by = s / theta;
+        omc_by = (1.0f - c) / theta;
+    }
+    Aff E;
+    E.m00 = c; E.m01 = -s; E.m10 = s; E.m11 = c;
+    E.m02 = sin_by * a0 - omc_by * a1;
+    E.m12 = omc_by * a0 + sin_by * a1;
+    E.m20 = 0.0f; E.m21 = 0.0f; E.m22 = 1.0f;
+    return E;
+}
+
+// nalgebra Cholesky (3x3, lower) + solve_mut(identity); uniform across lanes.
+__device__ __forceinline__ bool chol_inv3(float A[3][3], float X[3][3]) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < j; ++k) {
+            float factor = -A[j][k];
+#pragma unroll
+            for (int r = j; r < 3; ++r) A[r][j] = factor * A[r][k] + A[r][j];
+        }
+        float diag = A[j][j];
+        if (!(diag != 0.0f && diag >= 0.0f)) return false;
+        float den = sqrtf(diag);
+        A[j][j] = den;
+#pragma unroll
+        for (int r = j + 1; r < 3; ++r) A[r][j] = A[r][j] / den;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float b[3] = {0.0f, 0.0f, 0.0f};
+        b[c] = 1.0f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            float coeff = b[i] / A[i][i];
+            b[i] = coeff;
+#pragma unroll
+            for (int r = i + 1; r < 3; ++r) b[r] = (-coeff) * A[r][i] + b[r];
+        }
+#pragma unroll
+        for (int i = 2; i >= 0; --i) {
+            float dot = 0.0f;
+#pragma unroll
+            for (int r = i + 1; r < 3; ++r) dot = dot + A[r][i] * b[r];
+            b[i] = (b[i] - dot) / A[i][i];
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) X[r][c] = b[r];
+    }
+    return true;
+}
+
+struct Template {
+    float data;   // normalised intensity of this lane's point (-1 invalid)
+    float h0, h1, h2;  // this lane's column of H^-1 J^T
+};
+
+// Pattern52::new (patch.rs:124-162) + set_data_jac_se2 (:75-123)
+__device__ bool make_template(const LevelImg& im, float posx, float posy, int lane, float patx,
+                              float paty, Template& T) {
+    const bool act = lane < NP;
+    const float ox = act ? (float)kPattern[lane][0] : 0.0f;
+    const float oy = act ? (float)kPattern[lane][1] : 0.0f;
+    const float qx = posx + ox / 2.0f, qy = posy + oy / 2.0f;
+    const float jw02 = -oy / 2.0f, jw12 = ox / 2.0f;
+    const bool in = act && inbound(im, qx, qy, 2);
+    float v = 0.0f, J0 = 0.0f, J1 = 0.0f, J2 = 0.0f;
+    if (in) {
+        float vg[3];
+        image_grad(im, qx, qy, vg);
+        v = vg[0];
+        J0 = vg[1] * 1.0f + vg[2] * 0.0f;
+        J1 = vg[1] * 0.0f + vg[2] * 1.0f;
+        J2 = vg[1] * jw02 + vg[2] * jw12;
+    }
+    float data = in ? v : -1.0f;
+    const float sum = chain_from_zero(in ? v : 0.0f);
+    const float gs0 = chain_from_zero(in ? J0 : 0.0f);
+    const float gs1 = chain_from_zero(in ? J1 : 0.0f);
+    const float gs2 = chain_from_zero(in ? J2 : 0.0f);
+    const int nvalid = __popcll(__ballot(in));
+    const float mean = sum / (float)nvalid;
+    const float mean_inv = (float)nvalid / sum;
+    if (data >= 0.0f) {
+        J0 = J0 + (-(gs0 * data / sum));
+        J1 = J1 + (-(gs1 * data / sum));
+        J2 = J2 + (-(gs2 * data / sum));
+        data *= mean_inv;
+    } else {
+        J0 = J1 = J2 = 0.0f;
+    }
+    J0 *= mean_inv;
+    J1 *= mean_inv;
+    J2 *= mean_inv;
+    float H[3][3];
+    H[0][0] = chain_first(J0 * J0);
+    H[0][1] = chain_first(J0 * J1);
+    H[0][2] = chain_first(J0 * J2);
+    H[1][1] = chain_first(J1 * J1);
+    H[1][2] = chain_first(J1 * J2);
+    H[2][2] = chain_first(J2 * J2);
+    H[1][0] = H[0][1];
+    H[2][0] = H[0][2];
+    H[2][1] = H[1][2];
+    float Hi[3][3];
+    T.data = data;
+    if (!chol_inv3(H, Hi)) return false;
+    T.h0 = Hi[0][2] * J2 + (Hi[0][1] * J1 + Hi[0][0] * J0);
+    T.h1 = Hi[1][2] * J2 + (Hi[1][1] * J1 + Hi[1][0] * J0);
+    T.h2 = Hi[2][2] * J2 + (Hi[2][1] * J1 + Hi[2][0] * J0);
+    const bool fin = !act || (isfinite(T.h0) && isfinite(T.h1) && isfinite(T.h2) && isfinite(data));
+    const bool all_fin = __ballot(!fin) == 0ull;
+    return (mean > __FLT_EPSILON__) && all_fin;
+}
+
+// track_point_at_level (feature_tracker.rs:344-395) with Pattern52::residual (patch.rs:163-232)
+__device__ bool track_at_level(const LevelImg& im, const Template& T, float patx, float paty, int lane,
+                               Aff& A, int max_iter, float thresh) {
+    const bool act = lane < NP;
+    const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
+    for (int it = 0; it < max_iter; ++it) {
+        float x = A.m00 * patx;
+        x = A.m01 * paty + x;
+        float y = A.m10 * patx;
+        y = A.m11 * paty + y;
+        x = x + A.m02;
+        y = y + A.m12;
+        const bool inb = act && x >= 2.0f && y >= 2.0f && x < wlim && y < hlim;
+        float v = -1.0f;
+        if (inb) {
+            uint32_t ix = (uint32_t)floorf(x), iy = (uint32_t)floorf(y);
+            float dx = x - (float)ix, dy = y - (float)iy;
+            float ddx = 1.0f - dx, ddy = 1.0f - dy;
+            const uint8_t* r0 = im.p + (size_t)iy * im.w + ix;
+            const uint8_t* r1 = r0 + im.w;
+            float p00 = (float)r0[0], p10 = (float)r0[1], p01 = (float)r1[0], p11 = (float)r1[1];
+            v = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
+        }
+        const float sum = chain_from_zero(inb ? v : 0.0f);
+        const int nv = __popcll(__ballot(inb));
+        if (sum < __FLT_EPSILON__) return false;
+        const bool use = inb && v >= 0.0f && T.data >= 0.0f;
+        const float r = use ? ((float)nv * v / sum - T.data) : 0.0f;
+        const int nres = __popcll(__ballot(use));
+        if (!(nres > NP / 2)) return false;
+        const float i0 = chain_first((-T.h0) * r);
+        const float i1 = chain_first((-T.h1) * r);
+        const float i2 = chain_first((-T.h2) * r);
+        if (!(isfinite(i0) && isfinite(i1) && isfinite(i2))) return false;
+        const float nrm = sqrtf(i0 * i0 + i1 * i1 + i2 * i2);
+        if (nrm > 1e6f) return false;
+        if (nrm < thresh) break;
+        A = mul3(A, se2_exp(i0, i1, i2));
+        if (!inbound(im, A.m02, A.m12, 2)) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ LevelImg level_of(const uint8_t* pyr, uint32_t w, uint32_t h, int i) {
+    LevelImg L;
+    L.p = pyr + level_offset(w, h, i);
+    L.w = level_w(w, i);
+    L.h = level_h(h, i);
+    return L;
+}
+
+// track_one_point (feature_tracker.rs:292-342)
+__device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, uint32_t h, int levels,
+                          const Aff& T0, int lane, float patx, float paty, int max_iter, float thresh,
+                          Aff& out) {
+    Aff T1;
+    T1.m00 = 1.0f; T1.m01 = 0.0f; T1.m10 = 0.0f; T1.m11 = 1.0f;
+    T1.m20 = 0.0f; T1.m21 = 0.0f; T1.m22 = 1.0f;
+    T1.m02 = T0.m02;
+    T1.m12 = T0.m12;
+    for (int i = levels - 1; i >= 0; --i) {
+        const float sdn = (float)(1 << i);
+        T1.m02 /= sdn;
+        T1.m12 /= sdn;
+        Template tp;
+        if (!make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp))
+            return false;
+        if (!track_at_level(level_of(pyr1, w, h, i), tp, patx, paty, lane, T1, max_iter, thresh))
+            return false;
+        T1.m02 *= sdn;
+        T1.m12 *= sdn;
+    }
+    Aff R = mul3(T0, T1);
+    T1.m00 = R.m00;
+    T1.m01 = R.m01;
+    T1.m10 = R.m10;
+    T1.m11 = R.m11;
+    out = T1;
+    return true;
+}
+
+__global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
+    const int job = blockIdx.x;
+    int b = 0;
+    while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
+    const int idx = job - L.start[b];
+    if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
+    const int lane = threadIdx.x;
+    const float patx = lane < NP ? (float)kPattern[lane][0] / 2.0f : 0.0f;
+    const float paty = lane < NP ? (float)kPattern[lane][1] / 2.0f : 0.0f;
+    const float* a = L.ain[b] + 6 * (size_t)idx;
+    Aff T0;
+    T0.m00 = a[0]; T0.m01 = a[1]; T0.m10 = a[2]; T0.m11 = a[3]; T0.m02 = a[4]; T0.m12 = a[5];
+    T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
+    Aff fwd, bwd;
+    bool ok = track_one(L.pyr0[b], L.pyr1[b], L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
+                        L.thresh, fwd);
+    if (ok)
+        ok = track_one(L.pyr1[b], L.pyr0[b], L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
+                       L.thresh, bwd);
+    if (ok) {
+        // feature_tracker.rs:277-281: squared translation distance < 0.4
+        float dx = T0.m02 - bwd.m02, dy = T0.m12 - bwd.m12;
+        ok = (dx * dx + dy * dy) < 0.4f;
+    }
+    if (lane == 0) {
+        float* o = L.aout[b] + 6 * (size_t)idx;
+        if (ok) {
+            o[0] = fwd.m00; o[1] = fwd.m01; o[2] = fwd.m10; o[3] = fwd.m11; o[4] = fwd.m02; o[5] = fwd.m12;
+        } else {
+            for (int k = 0; k < 6; ++k) o[k] = a[k];
+        }
+        L.valid[b][idx] = ok ? 1 : 0;
+    }
+}
+
+}  // namespace
+
+void enqueue_track(const TrackLaunch& L, hipStream_t s) {
+    const int total = L.start[L.nb];
+    if (total <= 0) return;
+    hipLaunchKernelGGL(lk_track_kernel, dim3(total), dim3(64), 0, s, L);
+    RSVIO_HIP(hipGetLastError());
+}
+
+}  // namespace rsvio

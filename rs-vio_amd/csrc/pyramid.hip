@@ -1,0 +1,201 @@
+// pyramid.hip -- K1: image pyramid (gfx950).
+//
+// Replaces build_image_pyramid (src/feature_tracker/feature_tracker.rs:209-220): level i is
+// imageops::resize(full_res, W>>i, H>>i, Triangle) -- every level is resampled from the full
+// resolution image, separable, vertical pass (f32) then horizontal pass (clamp, round to u8),
+// image 0.25 semantics.  Bit-exact with the oracle: the tap weights and the sequential tap
+// sums use the same f32 operations in the same order (-ffp-contract=off).
+//
+// One launch covers every level of every image: a workgroup owns a 64 x 8 output tile of
+// one level; the vertical pass for the tile's rows over the tile's input-column span is
+// staged in LDS (coalesced u8 reads along x), the horizontal pass reads it back.
+#include "pyramid.hpp"
+
+namespace rsvio {
+
+namespace {
+
+constexpr int TW = 64;
+constexpr int TH = 8;
+constexpr int LDS_COLS = 1024;  // >= 64 * ratio + 2 * ratio + 4 for every level of a <= 2048-wide image
+
+__device__ __forceinline__ float triangle_kernel(float x) {
+    float ax = fabsf(x);
+    return ax < 1.0f ? 1.0f - ax : 0.0f;
+}
+
+// image 0.25 sample.rs: taps of one output index (same f32 ops as oracle make_taps)
+__global__ void make_taps_kernel(TapTable tab, int n_entries) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_entries) return;
+    int in_len = tab.ent_in_len[e];
+    int out_len = tab.ent_out_len[e];
+    int o = tab.ent_out_idx[e];
+    float ratio = (float)in_len / (float)out_len;
+    float sratio = ratio < 1.0f ? 1.0f : ratio;
+    float support = 1.0f * sratio;
+    float inputc = ((float)o + 0.5f) * ratio;
+    long long left = (long long)floorf(inputc - support);
+    if (left < 0) left = 0;
+    if (left > (long long)in_len - 1) left = in_len - 1;
+    long long right = (long long)ceilf(inputc + support);
+    if (right < left + 1) right = left + 1;
+    if (right > (long long)in_len) right = in_len;
+    inputc = inputc - 0.5f;
+    int cnt = (int)(right - left);
+    float* w = tab.weights + (size_t)e * tab.max_taps;
+    float sum = 0.0f;
+    for (int k = 0; k < cnt; ++k) {
+        float wv = triangle_kernel(((float)(left + k) - inputc) / sratio);
+        w[k] = wv;
+        sum += wv;
+    }
+    for (int k = 0; k < cnt; ++k) w[k] = w[k] / sum;
+    tab.left[e] = (int)left;
+    tab.count[e] = cnt;
+}
+
+__global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
+    __shared__ float tmp[TH * LDS_COLS];
+    const int img = blockIdx.y;
+    const uint8_t* __restrict__ src = io.src[img];
+    uint8_t* __restrict__ dst_base = io.dst[img];
+    int b = blockIdx.x;
+    // level-0 copy blocks first (16 B per lane)
+    if (b < L.copy_blocks) {
+        const size_t tot = (size_t)L.w * L.h;
+        if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst_base)) & 15) {
+            for (size_t i = (size_t)b * blockDim.x + threadIdx.x; i < tot; i += (size_t)L.copy_blocks * blockDim.x)
+                dst_base[i] = src[i];
+            return;
+        }
+        const size_t n16 = tot / 16;
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst_base);
+        for (size_t i = (size_t)b * blockDim.x + threadIdx.x; i < n16; i += (size_t)L.copy_blocks * blockDim.x)
+            d4[i] = s4[i];
+        size_t tail0 = n16 * 16;
+        if (b == 0)
+            for (size_t i = tail0 + threadIdx.x; i < tot; i += blockDim.x) dst_base[i] = src[i];
+        return;
+    }
+    b -= L.copy_blocks;
+    int lev = 1;
+    while (lev < L.levels - 1 && b >= L.tile_start[lev + 1]) ++lev;
+    b -= L.tile_start[lev];
+    const int nw = (int)level_w(L.w, lev), nh = (int)level_h(L.h, lev);
+    const int tw = L.tile_w[lev];
+    const int tiles_x = (nw + tw - 1) / tw;
+    const int tx = b % tiles_x, ty = b / tiles_x;
+    const int ox0 = tx * tw, ox1 = min(ox0 + tw, nw);
+    const int oy0 = ty * TH, oy1 = min(oy0 + TH, nh);
+    const int rows = oy1 - oy0, cols_out = ox1 - ox0;
+    const int hx = L.hx_ent[lev], vy = L.vy_ent[lev];
+    const TapTable& T = L.tab;
+    const int xl = T.left[hx + ox0];
+    const int xr = T.left[hx + ox1 - 1] + T.count[hx + ox1 - 1];
+    const int ncols = xr - xl;
+    // vertical pass: tmp[r][c] = sum_k src[(vleft + k) * w + xl + c] * vw[k]
+    for (int idx = threadIdx.x; idx < rows * ncols; idx += blockDim.x) {
+        const int r = idx / ncols, c = idx - r * ncols;
+        const int e = vy + oy0 + r;
+        const int vl = T.left[e], vc = T.count[e];
+        const float* __restrict__ vw = T.weights + (size_t)e * T.max_taps;
+        const uint8_t* __restrict__ col = src + (size_t)vl * L.w + xl + c;
+        float acc = 0.0f;
+        for (int k = 0; k < vc; ++k) acc += (float)col[(size_t)k * L.w] * vw[k];
+        tmp[r * LDS_COLS + c] = acc;
+    }
+    __syncthreads();
+    uint8_t* __restrict__ dst = dst_base + level_offset(L.w, L.h, lev);
+    for (int idx = threadIdx.x; idx < rows * cols_out; idx += blockDim.x) {
+        const int r = idx / cols_out, c = idx - r * cols_out;
+        const int e = hx + ox0 + c;
+        const int hl = T.left[e] - xl, hc = T.count[e];
+        const float* __restrict__ hw = T.weights + (size_t)e * T.max_taps;
+        const float* __restrict__ row = tmp + r * LDS_COLS + hl;
+        float acc = 0.0f;
+        for (int k = 0; k < hc; ++k) acc += row[k] * hw[k];
+        float cl = acc < 0.0f ? 0.0f : (acc > 255.0f ? 255.0f : acc);
+        dst[(size_t)(oy0 + r) * nw + ox0 + c] = (uint8_t)roundf(cl);
+    }
+}
+
+}  // namespace
+
+void PyramidPlan::init(int w_, int h_, int levels_) {
+    w = w_;
+    h = h_;
+    levels = levels_;
+    if (levels < 1 || levels > kMaxLevels) throw std::invalid_argument("levels must be in [1, 8]");
+    if (w < 16 || h < 16) throw std::invalid_argument("image too small");
+    // entries: for each level >= 1: nw horizontal + nh vertical
+    std::vector<int> in_len, out_len, out_idx;
+    float max_ratio = 1.0f;
+    memset(&launch, 0, sizeof(launch));
+    for (int i = 1; i < levels; ++i) {
+        int nw = (int)level_w(w, i), nh = (int)level_h(h, i);
+        if (nw < 1 || nh < 1) throw std::invalid_argument("too many levels for image size");
+        launch.hx_ent[i] = (int)in_len.size();
+        for (int o = 0; o < nw; ++o) { in_len.push_back(w); out_len.push_back(nw); out_idx.push_back(o); }
+        launch.vy_ent[i] = (int)in_len.size();
+        for (int o = 0; o < nh; ++o) { in_len.push_back(h); out_len.push_back(nh); out_idx.push_back(o); }
+        float rx = (float)w / nw;
+        max_ratio = std::max(max_ratio, std::max(rx, (float)h / nh));
+        // widest input span of a tile of tw outputs: tw * rx + 2 * rx + 3 columns
+        int tw = std::min(TW, (int)std::floor((LDS_COLS - 2.0f * rx - 4.0f) / rx));
+        if (tw < 1) throw std::invalid_argument("image too wide for the pyramid tile");
+        launch.tile_w[i] = tw;
+    }
+    n_entries = (int)in_len.size();
+    max_taps = (int)std::ceil(2.0f * max_ratio) + 4;
+    int tiles = 0;
+    for (int i = 1; i < levels; ++i) {
+        launch.tile_start[i] = tiles;
+        int nw = (int)level_w(w, i), nh = (int)level_h(h, i);
+        tiles += ((nw + launch.tile_w[i] - 1) / launch.tile_w[i]) * ((nh + TH - 1) / TH);
+    }
+    launch.tile_start[levels] = tiles;
+    launch.copy_blocks = std::max(1, (int)(((size_t)w * h / 16 + 255) / 256 / 4));
+    total_blocks = launch.copy_blocks + tiles;
+    launch.w = (uint32_t)w;
+    launch.h = (uint32_t)h;
+    launch.levels = levels;
+    launch.pyr_bytes = level_offset(w, h, levels);
+    if (n_entries > 0) {
+        i_in.alloc(n_entries); i_out.alloc(n_entries); i_idx.alloc(n_entries);
+        d_left.alloc(n_entries); d_count.alloc(n_entries);
+        d_w.alloc((size_t)n_entries * max_taps);
+        RSVIO_HIP(hipMemcpy(i_in.p, in_len.data(), sizeof(int) * n_entries, hipMemcpyHostToDevice));
+        RSVIO_HIP(hipMemcpy(i_out.p, out_len.data(), sizeof(int) * n_entries, hipMemcpyHostToDevice));
+        RSVIO_HIP(hipMemcpy(i_idx.p, out_idx.data(), sizeof(int) * n_entries, hipMemcpyHostToDevice));
+        TapTable t;
+        t.left = d_left.p; t.count = d_count.p; t.weights = d_w.p; t.max_taps = max_taps;
+        t.ent_in_len = i_in.p; t.ent_out_len = i_out.p; t.ent_out_idx = i_idx.p;
+        hipLaunchKernelGGL(make_taps_kernel, dim3((n_entries + 255) / 256), dim3(256), 0, 0, t, n_entries);
+        RSVIO_HIP(hipGetLastError());
+        RSVIO_HIP(hipDeviceSynchronize());
+        launch.tab = t;
+    }
+}
+
+void PyramidPlan::enqueue(const PyrIO& io, int n_img, hipStream_t s) const {
+    if (n_img <= 0) return;
+    if (n_img > kMaxPyrIO) throw std::invalid_argument("too many images per pyramid launch");
+    hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks, n_img), dim3(256), 0, s, launch, io);
+    RSVIO_HIP(hipGetLastError());
+}
+
+void PyramidPlan::enqueue(const uint8_t* d_imgs, int n_img, uint8_t* d_pyrs, hipStream_t s) const {
+    for (int i0 = 0; i0 < n_img; i0 += kMaxPyrIO) {
+        PyrIO io;
+        int n = std::min(kMaxPyrIO, n_img - i0);
+        for (int k = 0; k < n; ++k) {
+            io.src[k] = d_imgs + (size_t)(i0 + k) * w * h;
+            io.dst[k] = d_pyrs + (size_t)(i0 + k) * pyr_bytes();
+        }
+        enqueue(io, n, s);
+    }
+}
+
+}  // namespace rsvio

@@ -1,0 +1,725 @@
+// tracker.hip -- device-resident StereoPatchTracker and the HP-T C ABI.
+//
+// Replaces StereoPatchTracker::{new, process_frame, get_track_points, remove_id}
+// (src/feature_tracker/feature_tracker.rs:91-207), add_points (:222-251) and
+// detect_key_points (src/feature_tracker/image_utilities.rs:108-175).
+//
+// Per stereo frame, all on one HIP stream, nothing leaves HBM except the final feature list:
+//   K1 pyramid (both images, all levels, one launch)            pyramid.hip
+//   K2 temporal track cam0 + cam1 (one launch)                   lk_track.hip
+//   Kc compact surviving tracks + bin cam0 tracks into the grid  (1 workgroup)
+//   K3 FAST-9 threshold ladder, one workgroup per empty cell     (integer, exact)
+//   Kg gather new corners in the reference's cell scan order     (1 workgroup)
+//   K2 stereo track of the new corners cam0 -> cam1              lk_track.hip
+//   Ka append survivors with consecutive ids, pack the output    (1 workgroup)
+// Canonical order: track maps are kept sorted by id; new ids are assigned in detection scan
+// order (the reference's HashMap iteration order is random, feature_tracker.rs:162-170).
+#include <cmath>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lk_track.hpp"
+#include "pyramid.hpp"
+
+namespace rsvio {
+
+namespace {
+
+thread_local std::string g_last_error;
+
+constexpr int kEdge = 19;  // EDGE_THRESHOLD, image_utilities.rs:114
+
+struct GridGeom {
+    int w, h, g;
+    int xs, ys, xe, ye;   // x_start, y_start, x_stop, y_stop (image_utilities.rs:121-125)
+    int bin_rows, bin_cols;  // (h / g + 1) x (w / g + 1) counters
+    int cells_x, cells_y;    // cells actually scanned
+};
+
+GridGeom make_grid(int w, int h, int g) {
+    GridGeom G;
+    G.w = w; G.h = h; G.g = g;
+    G.xs = (w % g) / 2;
+    G.xe = G.xs + g * (w / g - 1) + 1;
+    G.ys = (h % g) / 2;
+    G.ye = G.ys + g * (h / g - 1) + 1;
+    G.bin_rows = h / g + 1;
+    G.bin_cols = w / g + 1;
+    G.cells_x = (G.xe - G.xs + g - 1) / g;
+    G.cells_y = (G.ye - G.ys + g - 1) / g;
+    return G;
+}
+
+__device__ __forceinline__ uint32_t sat_u32(float v) {
+    if (!(v > 0.0f)) return 0u;
+    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)v;
+}
+
+// Block-wide exclusive scan of one int per thread (blockDim.x <= 1024).
+__device__ int block_exclusive_scan(int v, int* sh, int* total) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+        int t = tid >= off ? sh[tid - off] : 0;
+        __syncthreads();
+        sh[tid] += t;
+        __syncthreads();
+    }
+    int incl = sh[tid];
+    *total = sh[blockDim.x - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+// Stable compaction of track map c (keep valid), then bin cam0 positions into grid counters
+// (image_utilities.rs:128-139 with feature_tracker.rs:228-237's rounding).
+__global__ __launch_bounds__(1024) void compact_bin_kernel(
+    int n0, int n1, const float* __restrict__ aff_t0, const float* __restrict__ aff_t1,
+    const uint8_t* __restrict__ v0, const uint8_t* __restrict__ v1, float* __restrict__ map_aff0,
+    float* __restrict__ map_aff1, uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
+    uint64_t* __restrict__ ids_tmp, int* __restrict__ counts, int* __restrict__ bins, GridGeom G,
+    int tracked) {
+    __shared__ int sh[1024];
+    const int tid = threadIdx.x;
+    for (int c = 0; c < 2; ++c) {
+        const int n = c == 0 ? n0 : n1;
+        const float* at = c == 0 ? aff_t0 : aff_t1;
+        const uint8_t* vv = c == 0 ? v0 : v1;
+        float* ma = c == 0 ? map_aff0 : map_aff1;
+        uint64_t* ids = c == 0 ? ids0 : ids1;
+        if (!tracked) {
+            if (tid == 0) counts[c] = n;
+            continue;
+        }
+        const int per = (n + blockDim.x - 1) / blockDim.x;
+        const int b = tid * per, e = min(n, b + per);
+        int local = 0;
+        for (int i = b; i < e; ++i) local += vv[i] ? 1 : 0;
+        int total;
+        int pos = block_exclusive_scan(local, sh, &total);
+        // ids: copy through a temporary so that in-place compaction is race free
+        for (int i = b; i < e; ++i) ids_tmp[i] = ids[i];
+        __syncthreads();
+        for (int i = b; i < e; ++i) {
+            if (!vv[i]) continue;
+            for (int k = 0; k < 6; ++k) ma[6 * pos + k] = at[6 * i + k];
+            ids[pos] = ids_tmp[i];
+            ++pos;
+        }
+        if (tid == 0) counts[c] = total;
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int i = tid; i < G.bin_rows * G.bin_cols; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    const int n = counts[0];
+    for (int i = tid; i < n; i += blockDim.x) {
+        uint32_t x = sat_u32(roundf(map_aff0[6 * i + 4]));
+        uint32_t y = sat_u32(roundf(map_aff0[6 * i + 5]));
+        if (x >= (uint32_t)G.xs && y >= (uint32_t)G.ys && x < (uint32_t)(G.xe + G.g) && y < (uint32_t)(G.ye + G.g)) {
+            uint32_t cx = (x - G.xs) / G.g, cy = (y - G.ys) / G.g;
+            atomicAdd(&bins[cy * G.bin_cols + cx], 1);
+        }
+    }
+}
+
+// FAST-9 score of a candidate (largest t with a contiguous 9-arc all brighter than c + t or all
+// darker than c - t); equals imageproc's binary-searched fast_corner_score whenever the pixel is
+// a corner at the starting threshold.
+__device__ __forceinline__ int fast9_score(const uint8_t* crop, int g, int x, int y) {
+    const int8_t ox[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    const int8_t oy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+    const int c = crop[y * g + x];
+    int d[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] = (int)crop[(y + oy[i]) * g + x + ox[i]] - c;
+    int sb = -1000, sd = -1000;
+#pragma unroll
+    for (int a = 0; a < 16; ++a) {
+        int mb = 1000, md = 1000;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            int v = d[(a + k) & 15];
+            mb = min(mb, v);
+            md = min(md, -v);
+        }
+        sb = max(sb, mb);
+        sd = max(sd, md);
+    }
+    return max(sb, sd) - 1;
+}
+
+// detect_key_points per cell (image_utilities.rs:141-172): skip occupied cells; otherwise
+// thresholds 40, 35, ..., 10 on the cell's grid x grid crop; keep the lowest-score corner
+// (ties: crop scan order) that lies in [19, w-19] x [19, h-19].
+__global__ __launch_bounds__(256) void fast_cells_kernel(const uint8_t* __restrict__ img, GridGeom G,
+                                                         const int* __restrict__ bins,
+                                                         int4* __restrict__ cell_pt) {
+    extern __shared__ uint8_t crop[];
+    __shared__ int s_max, s_key;
+    const int s = blockIdx.x;            // scan order: x outer, y inner
+    const int cx = s / G.cells_y, cy = s % G.cells_y;
+    const int x0 = G.xs + cx * G.g, y0 = G.ys + cy * G.g;
+    if (bins[cy * G.bin_cols + cx] > 0) {
+        if (threadIdx.x == 0) cell_pt[s] = make_int4(0, 0, 0, 0);
+        return;
+    }
+    const int g = G.g;
+    for (int i = threadIdx.x; i < g * g; i += blockDim.x) crop[i] = img[(size_t)(y0 + i / g) * G.w + x0 + i % g];
+    if (threadIdx.x == 0) {
+        s_max = -1;
+        s_key = 0x7FFFFFFF;
+    }
+    __syncthreads();
+    const int span = g - 6;  // crop-local candidates [3, g - 3)
+    int my_best = -1;
+    for (int i = threadIdx.x; i < span * span; i += blockDim.x) {
+        const int x = 3 + i % span, y = 3 + i / span;
+        const int X = x0 + x, Y = y0 + y;
+        if (X < kEdge || X > G.w - kEdge || Y < kEdge || Y > G.h - kEdge) continue;
+        int sc = fast9_score(crop, g, x, y);
+        if (sc >= 10) my_best = max(my_best, sc);
+    }
+    if (my_best >= 0) atomicMax(&s_max, my_best);
+    __syncthreads();
+    const int smax = s_max;
+    int tstar = -1;
+    for (int t = 40; t >= 10; t -= 5)
+        if (smax >= t) {
+            tstar = t;
+            break;
+        }
+    if (tstar < 0) {
+        if (threadIdx.x == 0) cell_pt[s] = make_int4(0, 0, 0, 0);
+        return;
+    }
+    int my_key = 0x7FFFFFFF;
+    for (int i = threadIdx.x; i < span * span; i += blockDim.x) {
+        const int x = 3 + i % span, y = 3 + i / span;
+        const int X = x0 + x, Y = y0 + y;
+        if (X < kEdge || X > G.w - kEdge || Y < kEdge || Y > G.h - kEdge) continue;
+        int sc = fast9_score(crop, g, x, y);
+        if (sc >= tstar) my_key = min(my_key, (sc << 16) | (y * g + x));
+    }
+    atomicMin(&s_key, my_key);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int key = s_key;
+        const int idx = key & 0xFFFF;
+        cell_pt[s] = make_int4(x0 + idx % g, y0 + idx / g, key >> 16, 1);
+    }
+}
+
+// New corners in scan order -> identity Affine2 at the corner (feature_tracker.rs:143-152)
+__global__ __launch_bounds__(1024) void gather_new_kernel(const int4* __restrict__ cell_pt, int n_cells,
+                                                          float* __restrict__ new_aff, int* __restrict__ new_count,
+                                                          float* __restrict__ new_score) {
+    __shared__ int sh[1024];
+    const int per = (n_cells + blockDim.x - 1) / blockDim.x;
+    const int b = threadIdx.x * per, e = min(n_cells, b + per);
+    int local = 0;
+    for (int i = b; i < e; ++i) local += cell_pt[i].w;
+    int total;
+    int pos = block_exclusive_scan(local, sh, &total);
+    for (int i = b; i < e; ++i) {
+        int4 c = cell_pt[i];
+        if (!c.w) continue;
+        float* a = new_aff + 6 * pos;
+        a[0] = 1.0f; a[1] = 0.0f; a[2] = 0.0f; a[3] = 1.0f;
+        a[4] = (float)c.x;
+        a[5] = (float)c.y;
+        if (new_score) new_score[pos] = (float)c.z;
+        ++pos;
+    }
+    if (threadIdx.x == 0) *new_count = total;
+}
+
+// feature_tracker.rs:162-170 in canonical order, then get_track_points packing.
+__global__ __launch_bounds__(1024) void append_pack_kernel(
+    const float* __restrict__ new_aff0, const float* __restrict__ new_aff1,
+    const uint8_t* __restrict__ new_valid, const int* __restrict__ new_count, float* __restrict__ map_aff0,
+    float* __restrict__ map_aff1, uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
+    int* __restrict__ counts, unsigned long long* __restrict__ last_id, int capacity,
+    rsvio_feature* __restrict__ out0, rsvio_feature* __restrict__ out1, int* __restrict__ overflow) {
+    __shared__ int sh[1024];
+    const int m = *new_count;
+    const int per = (m + blockDim.x - 1) / blockDim.x;
+    const int b = threadIdx.x * per, e = min(m, b + per);
+    int local = 0;
+    for (int i = b; i < e; ++i) local += new_valid[i] ? 1 : 0;
+    int total;
+    int pos = block_exclusive_scan(local, sh, &total);
+    const int c0 = counts[0], c1 = counts[1];
+    const unsigned long long base = *last_id;
+    for (int i = b; i < e; ++i) {
+        if (!new_valid[i]) continue;
+        const int d0 = c0 + pos, d1 = c1 + pos;
+        if (d0 < capacity && d1 < capacity) {
+            for (int k = 0; k < 6; ++k) {
+                map_aff0[6 * d0 + k] = new_aff0[6 * i + k];
+                map_aff1[6 * d1 + k] = new_aff1[6 * i + k];
+            }
+            ids0[d0] = base + pos;
+            ids1[d1] = base + pos;
+        }
+        ++pos;
+    }
+    __syncthreads();
+    int n0 = c0 + total, n1 = c1 + total;
+    if (n0 > capacity || n1 > capacity) {
+        n0 = min(n0, capacity);
+        n1 = min(n1, capacity);
+        if (threadIdx.x == 0) *overflow = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        counts[0] = n0;
+        counts[1] = n1;
+        *last_id = base + (unsigned long long)total;
+    }
+    for (int i = threadIdx.x; i < n0; i += blockDim.x) {
+        const float* a = map_aff0 + 6 * i;
+        rsvio_feature f;
+        f.id = ids0[i]; f.x = a[4]; f.y = a[5]; f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
+        out0[i] = f;
+    }
+    for (int i = threadIdx.x; i < n1; i += blockDim.x) {
+        const float* a = map_aff1 + 6 * i;
+        rsvio_feature f;
+        f.id = ids1[i]; f.x = a[4]; f.y = a[5]; f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
+        out1[i] = f;
+    }
+}
+
+// StereoPatchTracker::remove_id (feature_tracker.rs:201-206)
+__global__ __launch_bounds__(1024) void remove_ids_kernel(const uint64_t* __restrict__ rm, int n_rm,
+                                                          float* __restrict__ map_aff0, float* __restrict__ map_aff1,
+                                                          uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
+                                                          float* __restrict__ tmp_aff, uint64_t* __restrict__ tmp_ids,
+                                                          int* __restrict__ counts, rsvio_feature* out0,
+                                                          rsvio_feature* out1) {
+    __shared__ int sh[1024];
+    for (int c = 0; c < 2; ++c) {
+        float* ma = c == 0 ? map_aff0 : map_aff1;
+        uint64_t* ids = c == 0 ? ids0 : ids1;
+        rsvio_feature* out = c == 0 ? out0 : out1;
+        const int n = counts[c];
+        const int per = (n + blockDim.x - 1) / blockDim.x;
+        const int b = threadIdx.x * per, e = min(n, b + per);
+        int local = 0;
+        for (int i = b; i < e; ++i) {
+            bool drop = false;
+            for (int k = 0; k < n_rm; ++k) drop |= (rm[k] == ids[i]);
+            local += drop ? 0 : 1;
+            tmp_ids[i] = drop ? ~0ull : ids[i];
+            for (int k = 0; k < 6; ++k) tmp_aff[6 * i + k] = ma[6 * i + k];
+        }
+        int total;
+        int pos = block_exclusive_scan(local, sh, &total);
+        for (int i = b; i < e; ++i) {
+            if (tmp_ids[i] == ~0ull) continue;
+            for (int k = 0; k < 6; ++k) ma[6 * pos + k] = tmp_aff[6 * i + k];
+            ids[pos] = tmp_ids[i];
+            ++pos;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) counts[c] = total;
+        for (int i = threadIdx.x; i < total; i += blockDim.x) {
+            const float* a = ma + 6 * i;
+            rsvio_feature f;
+            f.id = ids[i]; f.x = a[4]; f.y = a[5]; f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
+            out[i] = f;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+// ------------------------------------------------------------------------------------------
+struct Tracker {
+    rsvio_tracker_params P;
+    GridGeom G;
+    PyramidPlan plan;
+    hipStream_t stream = nullptr;
+    size_t pyr_bytes = 0;
+    int cap = 0;
+    int n_cells = 0;
+    int cur = 0;            // pyramid ping-pong index
+    bool has_prev = false;
+    int host_count[2] = {0, 0};
+    DevBuf<uint8_t> d_img, d_pyr;   // 2 images; 2 slots x 2 cams pyramids
+    DevBuf<float> map_aff, tmp_aff, new_aff, new_aff1, new_score;
+    DevBuf<uint64_t> ids, ids_tmp, rm_ids;
+    DevBuf<uint8_t> valid, new_valid;
+    DevBuf<int> counts, bins, new_count, overflow;
+    DevBuf<int4> cell_pt;
+    DevBuf<unsigned long long> last_id;
+    DevBuf<rsvio_feature> out;
+    HostBuf<int> h_counts;
+
+    uint8_t* pyr(int slot, int cam) { return d_pyr.p + (size_t)(2 * slot + cam) * pyr_bytes; }
+
+    void init(const rsvio_tracker_params& p) {
+        P = p;
+        if (P.width < 32 || P.height < 32 || P.levels < 1 || P.levels > kMaxLevels || P.grid_size < 8 ||
+            P.grid_size > 128 || P.max_iterations < 0)
+            throw std::invalid_argument("invalid tracker parameters");
+        if (P.grid_size > P.width || P.grid_size > P.height) throw std::invalid_argument("grid larger than image");
+        cap = P.max_features > 0 ? P.max_features : 4096;
+        RSVIO_HIP(hipSetDevice(P.device));
+        RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        plan.init(P.width, P.height, P.levels);
+        pyr_bytes = plan.pyr_bytes();
+        G = make_grid(P.width, P.height, P.grid_size);
+        n_cells = G.cells_x * G.cells_y;
+        const size_t img = (size_t)P.width * P.height;
+        d_img.alloc(2 * img);
+        d_pyr.alloc(4 * pyr_bytes);
+        map_aff.alloc((size_t)2 * cap * 6);
+        tmp_aff.alloc((size_t)2 * cap * 6);
+        ids.alloc((size_t)2 * cap);
+        ids_tmp.alloc((size_t)2 * cap);
+        valid.alloc((size_t)2 * cap);
+        new_aff.alloc((size_t)n_cells * 6);
+        new_aff1.alloc((size_t)n_cells * 6);
+        new_score.alloc(n_cells);
+        new_valid.alloc(n_cells);
+        counts.alloc(2);
+        bins.alloc((size_t)G.bin_rows * G.bin_cols);
+        new_count.alloc(1);
+        overflow.alloc(1);
+        cell_pt.alloc(n_cells);
+        last_id.alloc(1);
+        out.alloc((size_t)2 * cap);
+        h_counts.alloc(4);
+        RSVIO_HIP(hipMemsetAsync(counts.p, 0, sizeof(int) * 2, stream));
+        RSVIO_HIP(hipMemsetAsync(last_id.p, 0, sizeof(unsigned long long), stream));
+        RSVIO_HIP(hipMemsetAsync(overflow.p, 0, sizeof(int), stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+    }
+    ~Tracker() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    float* maff(int c) { return map_aff.p + (size_t)c * cap * 6; }
+    float* taff(int c) { return tmp_aff.p + (size_t)c * cap * 6; }
+    uint64_t* mid(int c) { return ids.p + (size_t)c * cap; }
+
+    // Enqueue one frame; images already in device memory.
+    void enqueue_frame(const uint8_t* d_left, const uint8_t* d_right) {
+        const int nxt = has_prev ? 1 - cur : cur;
+        PyrIO io;
+        io.src[0] = d_left; io.dst[0] = pyr(nxt, 0);
+        io.src[1] = d_right; io.dst[1] = pyr(nxt, 1);
+        plan.enqueue(io, 2, stream);
+        if (has_prev) {
+            TrackLaunch L{};
+            L.w = P.width; L.h = P.height; L.levels = P.levels; L.max_iter = P.max_iterations;
+            L.thresh = P.convergence_threshold;
+            L.nb = 2;
+            L.start[0] = 0; L.start[1] = host_count[0]; L.start[2] = host_count[0] + host_count[1];
+            for (int c = 0; c < 2; ++c) {
+                L.pyr0[c] = pyr(cur, c); L.pyr1[c] = pyr(nxt, c);
+                L.ain[c] = maff(c); L.aout[c] = taff(c); L.valid[c] = valid.p + (size_t)c * cap;
+                L.dcount[c] = nullptr;
+            }
+            enqueue_track(L, stream);
+        }
+        hipLaunchKernelGGL(compact_bin_kernel, dim3(1), dim3(1024), 0, stream, host_count[0], host_count[1],
+                           taff(0), taff(1), valid.p, valid.p + cap, maff(0), maff(1), mid(0), mid(1),
+                           ids_tmp.p, counts.p, bins.p, G, has_prev ? 1 : 0);
+        RSVIO_HIP(hipGetLastError());
+        const uint8_t* cur0 = pyr(nxt, 0);  // level 0 == the left image
+        hipLaunchKernelGGL(fast_cells_kernel, dim3(n_cells), dim3(256), (size_t)P.grid_size * P.grid_size, stream,
+                           cur0, G, bins.p, cell_pt.p);
+        RSVIO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(gather_new_kernel, dim3(1), dim3(1024), 0, stream, cell_pt.p, n_cells, new_aff.p,
+                           new_count.p, new_score.p);
+        RSVIO_HIP(hipGetLastError());
+        {
+            TrackLaunch L{};
+            L.w = P.width; L.h = P.height; L.levels = P.levels; L.max_iter = P.max_iterations;
+            L.thresh = P.convergence_threshold;
+            L.nb = 1;
+            L.start[0] = 0; L.start[1] = n_cells;
+            L.pyr0[0] = pyr(nxt, 0); L.pyr1[0] = pyr(nxt, 1);
+            L.ain[0] = new_aff.p; L.aout[0] = new_aff1.p; L.valid[0] = new_valid.p;
+            L.dcount[0] = new_count.p;
+            enqueue_track(L, stream);
+        }
+        hipLaunchKernelGGL(append_pack_kernel, dim3(1), dim3(1024), 0, stream, new_aff.p, new_aff1.p, new_valid.p,
+                           new_count.p, maff(0), maff(1), mid(0), mid(1), counts.p, last_id.p, cap, out.p,
+                           out.p + cap, overflow.p);
+        RSVIO_HIP(hipGetLastError());
+        cur = nxt;
+        has_prev = true;
+    }
+
+    void fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
+        RSVIO_HIP(hipMemcpyAsync(h_counts.p, counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipMemcpyAsync(h_counts.p + 2, overflow.p, sizeof(int), hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+        host_count[0] = h_counts.p[0];
+        host_count[1] = h_counts.p[1];
+        const size_t nl = std::min((size_t)host_count[0], cap_l), nr = std::min((size_t)host_count[1], cap_r);
+        if (nl) RSVIO_HIP(hipMemcpyAsync(out_l, out.p, nl * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
+        if (nr) RSVIO_HIP(hipMemcpyAsync(out_r, out.p + cap, nr * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+        *n_l = nl;
+        *n_r = nr;
+    }
+};
+
+// Parity-level context: taps + scratch for the stateless entry points
+struct TrackCtx {
+    PyramidPlan plan;
+    int device = 0;
+};
+
+}  // namespace rsvio
+
+struct rsvio_tracker {
+    rsvio::Tracker t;
+};
+struct rsvio_track_ctx {
+    rsvio::TrackCtx c;
+};
+
+using rsvio::guarded;
+
+extern "C" {
+
+const char* rsvio_last_error(void) { return rsvio::g_last_error.c_str(); }
+
+int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus) {
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+            rsvio::set_last_error("no HIP device visible");
+            return (int)RSVIO_ERR_NO_DEVICE;
+        }
+        hipDeviceProp_t prop;
+        RSVIO_HIP(hipGetDeviceProperties(&prop, device));
+        if (name_out && cap) snprintf(name_out, cap, "%s", prop.gcnArchName);
+        if (n_cus) *n_cus = prop.multiProcessorCount;
+        if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+            rsvio::set_last_error(std::string("device is ") + prop.gcnArchName + ", library built for gfx950");
+            return (int)RSVIO_ERR_NO_DEVICE;
+        }
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_create(const rsvio_tracker_params* params, rsvio_tracker** out) {
+    if (!params || !out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto* h = new rsvio_tracker();
+        try {
+            h->t.init(*params);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+        return (int)RSVIO_OK;
+    });
+}
+
+void rsvio_tracker_destroy(rsvio_tracker* t) { delete t; }
+
+void* rsvio_tracker_stream(rsvio_tracker* t) { return t ? (void*)t->t.stream : nullptr; }
+
+int rsvio_tracker_process_frame(rsvio_tracker* t, const uint8_t* left, const uint8_t* right, size_t stride,
+                                rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r,
+                                size_t cap_r, size_t* n_r) {
+    if (!t || !left || !right || !n_l || !n_r) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto& T = t->t;
+        const size_t w = (size_t)T.P.width, h = (size_t)T.P.height;
+        if (stride == 0) stride = w;
+        if (stride < w) throw std::invalid_argument("stride < width");
+        RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p, w, left, stride, w, h, hipMemcpyHostToDevice, T.stream));
+        RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p + w * h, w, right, stride, w, h, hipMemcpyHostToDevice, T.stream));
+        T.enqueue_frame(T.d_img.p, T.d_img.p + w * h);
+        T.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left, const uint8_t* d_right,
+                                       rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r,
+                                       size_t cap_r, size_t* n_r) {
+    if (!t || !d_left || !d_right || !n_l || !n_r) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        t->t.enqueue_frame(d_left, d_right);
+        t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n) {
+    if (!t || (!ids && n)) return RSVIO_ERR_INVALID_ARG;
+    if (n == 0) return RSVIO_OK;
+    return guarded([&] {
+        auto& T = t->t;
+        if (T.rm_ids.n < n) T.rm_ids.alloc(n);
+        RSVIO_HIP(hipMemcpyAsync(T.rm_ids.p, ids, n * sizeof(uint64_t), hipMemcpyHostToDevice, T.stream));
+        hipLaunchKernelGGL(rsvio::remove_ids_kernel, dim3(1), dim3(1024), 0, T.stream, T.rm_ids.p, (int)n, T.maff(0),
+                           T.maff(1), T.mid(0), T.mid(1), T.tmp_aff.p, T.ids_tmp.p, T.counts.p, T.out.p,
+                           T.out.p + T.cap);
+        RSVIO_HIP(hipGetLastError());
+        RSVIO_HIP(hipMemcpyAsync(T.h_counts.p, T.counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, T.stream));
+        RSVIO_HIP(hipStreamSynchronize(T.stream));
+        T.host_count[0] = T.h_counts.p[0];
+        T.host_count[1] = T.h_counts.p[1];
+        return (int)RSVIO_OK;
+    });
+}
+
+size_t rsvio_pyramid_bytes(int32_t w, int32_t h, int32_t levels) {
+    if (w <= 0 || h <= 0 || levels <= 0) return 0;
+    return rsvio::level_offset((uint32_t)w, (uint32_t)h, levels);
+}
+
+int rsvio_track_ctx_create(int32_t w, int32_t h, int32_t levels, int32_t device, rsvio_track_ctx** out) {
+    if (!out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        RSVIO_HIP(hipSetDevice(device));
+        auto* c = new rsvio_track_ctx();
+        try {
+            c->c.device = device;
+            c->c.plan.init(w, h, levels);
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+        return (int)RSVIO_OK;
+    });
+}
+
+void rsvio_track_ctx_destroy(rsvio_track_ctx* c) { delete c; }
+
+int rsvio_build_pyramids_d(rsvio_track_ctx* c, const uint8_t* d_imgs, int32_t n_img, uint8_t* d_pyrs, void* stream) {
+    if (!c || !d_imgs || !d_pyrs || n_img < 0) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        c->c.plan.enqueue(d_imgs, n_img, d_pyrs, (hipStream_t)stream);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, int32_t n_batches,
+                         int32_t max_iterations, float thresh, void* stream) {
+    if (!c || !batches || n_batches < 0 || n_batches > rsvio::kMaxTrackBatches) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        rsvio::TrackLaunch L{};
+        L.w = c->c.plan.w; L.h = c->c.plan.h; L.levels = c->c.plan.levels;
+        L.max_iter = max_iterations; L.thresh = thresh; L.nb = n_batches;
+        L.start[0] = 0;
+        for (int b = 0; b < n_batches; ++b) {
+            if (batches[b].n < 0) throw std::invalid_argument("negative batch size");
+            L.start[b + 1] = L.start[b] + batches[b].n;
+            L.pyr0[b] = batches[b].d_pyr0; L.pyr1[b] = batches[b].d_pyr1;
+            L.ain[b] = batches[b].d_aff_in; L.aout[b] = batches[b].d_aff_out; L.valid[b] = batches[b].d_valid;
+            L.dcount[b] = nullptr;
+        }
+        rsvio::enqueue_track(L, (hipStream_t)stream);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_build_pyramid(const uint8_t* img, int32_t w, int32_t h, int32_t levels, uint8_t* out) {
+    if (!img || !out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        rsvio::PyramidPlan plan;
+        plan.init(w, h, levels);
+        rsvio::DevBuf<uint8_t> di((size_t)w * h), dp(plan.pyr_bytes());
+        RSVIO_HIP(hipMemcpy(di.p, img, (size_t)w * h, hipMemcpyHostToDevice));
+        plan.enqueue(di.p, 1, dp.p, nullptr);
+        RSVIO_HIP(hipMemcpy(out, dp.p, plan.pyr_bytes(), hipMemcpyDeviceToHost));
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_track_points(const uint8_t* pyr0, const uint8_t* pyr1, int32_t w, int32_t h, int32_t levels,
+                       const float* aff_in, int32_t n, int32_t max_iterations, float thresh, float* aff_out,
+                       uint8_t* valid_out) {
+    if (!pyr0 || !pyr1 || n < 0 || (n > 0 && (!aff_in || !aff_out || !valid_out))) return RSVIO_ERR_INVALID_ARG;
+    if (levels < 1 || levels > rsvio::kMaxLevels || w < 1 || h < 1) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        const size_t pb = rsvio::level_offset(w, h, levels);
+        rsvio::DevBuf<uint8_t> d0(pb), d1(pb), dv(std::max(n, 1));
+        rsvio::DevBuf<float> ai((size_t)std::max(n, 1) * 6), ao((size_t)std::max(n, 1) * 6);
+        RSVIO_HIP(hipMemcpy(d0.p, pyr0, pb, hipMemcpyHostToDevice));
+        RSVIO_HIP(hipMemcpy(d1.p, pyr1, pb, hipMemcpyHostToDevice));
+        if (n) RSVIO_HIP(hipMemcpy(ai.p, aff_in, sizeof(float) * 6 * n, hipMemcpyHostToDevice));
+        rsvio::TrackLaunch L{};
+        L.w = w; L.h = h; L.levels = levels; L.max_iter = max_iterations; L.thresh = thresh; L.nb = 1;
+        L.start[0] = 0; L.start[1] = n;
+        L.pyr0[0] = d0.p; L.pyr1[0] = d1.p; L.ain[0] = ai.p; L.aout[0] = ao.p; L.valid[0] = dv.p;
+        L.dcount[0] = nullptr;
+        rsvio::enqueue_track(L, nullptr);
+        if (n) {
+            RSVIO_HIP(hipMemcpy(aff_out, ao.p, sizeof(float) * 6 * n, hipMemcpyDeviceToHost));
+            RSVIO_HIP(hipMemcpy(valid_out, dv.p, n, hipMemcpyDeviceToHost));
+        }
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_detect_keypoints(const uint8_t* img, int32_t w, int32_t h, int32_t grid, const float* existing_xy,
+                           int32_t n_existing, uint32_t* out_xy, float* out_score, int32_t cap, int32_t* n_out) {
+    if (!img || !out_xy || !n_out || n_existing < 0 || (n_existing && !existing_xy) || grid < 8 || grid > 128 ||
+        grid > w || grid > h)
+        return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        rsvio::GridGeom G = rsvio::make_grid(w, h, grid);
+        const int n_cells = G.cells_x * G.cells_y;
+        const int ne = std::max(n_existing, 1);
+        rsvio::DevBuf<uint8_t> di((size_t)w * h), dv(ne);
+        rsvio::DevBuf<float> ea((size_t)ne * 6), na((size_t)n_cells * 6), ns(n_cells);
+        rsvio::DevBuf<uint64_t> ids(ne), idt(ne);
+        rsvio::DevBuf<int> counts(2), bins((size_t)G.bin_rows * G.bin_cols), nc(1);
+        rsvio::DevBuf<int4> cp(n_cells);
+        RSVIO_HIP(hipMemcpy(di.p, img, (size_t)w * h, hipMemcpyHostToDevice));
+        std::vector<float> aff((size_t)ne * 6, 0.0f);
+        for (int i = 0; i < n_existing; ++i) {
+            aff[6 * i + 4] = existing_xy[2 * i];
+            aff[6 * i + 5] = existing_xy[2 * i + 1];
+        }
+        RSVIO_HIP(hipMemcpy(ea.p, aff.data(), sizeof(float) * aff.size(), hipMemcpyHostToDevice));
+        // counts[0] = n_existing, map already "compacted": run the kernel in not-tracked mode
+        hipLaunchKernelGGL(rsvio::compact_bin_kernel, dim3(1), dim3(1024), 0, nullptr, n_existing, 0, ea.p, ea.p,
+                           dv.p, dv.p, ea.p, ea.p, ids.p, ids.p, idt.p, counts.p, bins.p, G, 0);
+        RSVIO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(rsvio::fast_cells_kernel, dim3(n_cells), dim3(256), (size_t)grid * grid, nullptr, di.p, G,
+                           bins.p, cp.p);
+        RSVIO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(rsvio::gather_new_kernel, dim3(1), dim3(1024), 0, nullptr, cp.p, n_cells, na.p, nc.p, ns.p);
+        RSVIO_HIP(hipGetLastError());
+        int m = 0;
+        RSVIO_HIP(hipMemcpy(&m, nc.p, sizeof(int), hipMemcpyDeviceToHost));
+        std::vector<float> a((size_t)std::max(m, 1) * 6), sc(std::max(m, 1));
+        if (m) {
+            RSVIO_HIP(hipMemcpy(a.data(), na.p, sizeof(float) * 6 * m, hipMemcpyDeviceToHost));
+            RSVIO_HIP(hipMemcpy(sc.data(), ns.p, sizeof(float) * m, hipMemcpyDeviceToHost));
+        }
+        const int k = std::min(m, cap);
+        for (int i = 0; i < k; ++i) {
+            out_xy[2 * i] = (uint32_t)a[6 * i + 4];
+            out_xy[2 * i + 1] = (uint32_t)a[6 * i + 5];
+            if (out_score) out_score[i] = sc[i];
+        }
+        *n_out = k;
+        return m > cap ? (int)RSVIO_ERR_CAPACITY : (int)RSVIO_OK;
+    });
+}
+
+}  // extern "C"

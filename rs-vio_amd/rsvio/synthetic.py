@@ -1,0 +1,290 @@
+"""Seeded synthetic inputs shaped like BASELINE.json's configurations.
+
+No EuRoC / TUM-VI data exists offline, so every workload is procedural:
+
+* ``stereo_sequence`` -- config 2: 752x480 u8 stereo frames.  A continuous texture of 6000
+  Gaussian blobs (amplitude U(-60, 60), sigma U(1.5, 8)) around 128 plus 2*N(0,1) pixel noise;
+  the right image sees the texture shifted by the disparity d(y) = 4 + 8*y/480; frame t+1
+  is frame t moved by (1.7, -0.9) px and rotated by 0.2 degrees.  (SURVEY.md 8d sketched 400
+  blobs / sigma 2-12 / noise 8 / d = 8..32 px: with that texture the reference algorithm keeps
+  < 50 % of its tracks and a 3-level pyramid cannot reach 32 px of disparity, so most of the
+  measured work would be early exits.  The denser texture keeps ~98 % of temporal tracks.)
+* ``track_features`` -- 300 feature positions (FAST-9 corners at t=20, >= 20 px apart, inside
+  [20, 732) x [20, 460), topped up with seeded uniform points) for config 2.
+* ``ba_problem`` -- config 3: 10 keyframes (KF_0 fixed), EuRoC extrinsics, 2000 landmarks,
+  each seen by both cameras in 6 consecutive keyframes (24,000 observations), noisy
+  observations and perturbed initial values.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+# config/euroc_vio.yaml:21-30 (T_B_Cl, T_B_Cr) and :10-16 (intrinsics)
+T_B_CL = np.array([
+    [0.0148655429818, -0.999880929698, 0.00414029679422, -0.0216401454975],
+    [0.999557249008, 0.0149672133247, 0.025715529948, -0.064676986768],
+    [-0.0257744366974, 0.00375618835797, 0.999660727178, 0.00981073058949],
+    [0.0, 0.0, 0.0, 1.0]])
+T_B_CR = np.array([
+    [0.0125552670891, -0.999755099723, 0.0182237714554, -0.0198435579556],
+    [0.999598781151, 0.0130119051815, 0.0251588363115, 0.0453689425024],
+    [-0.0253898008918, 0.0179005838253, 0.999517347078, 0.00786212447038],
+    [0.0, 0.0, 0.0, 1.0]])
+FX_LEFT = 458.654
+
+
+# ----------------------------------------------------------------------------------------
+# Tracker workload (config 2)
+# ----------------------------------------------------------------------------------------
+@dataclass
+class Texture:
+    mu: np.ndarray      # (K, 2) blob centres in texture coordinates
+    amp: np.ndarray     # (K,)
+    sigma: np.ndarray   # (K,)
+
+
+def make_texture(w: int, h: int, n_blobs: int = 6000, seed: int = 20260320) -> Texture:
+    rng = np.random.default_rng(seed)
+    margin = 80.0
+    mu = np.stack([rng.uniform(-margin, w + margin, n_blobs), rng.uniform(-margin, h + margin, n_blobs)], 1)
+    return Texture(mu=mu, amp=rng.uniform(-60, 60, n_blobs), sigma=rng.uniform(1.5, 8, n_blobs))
+
+
+def _render(tex: Texture, w: int, h: int, t: int, right: bool, noise: np.ndarray) -> np.ndarray:
+    """I(x) = 128 + sum_k A_k exp(-|warp(x) - mu_k|^2 / 2 sigma_k^2) + noise, clamped to u8.
+
+    warp(x) maps pixel x of frame t (left or right camera) to texture coordinates; each blob is
+    evaluated only in a pixel window around its forward-mapped centre.
+    """
+    ang = math.radians(0.2) * t
+    ca, sa = math.cos(ang), math.sin(ang)
+    sx, sy = 1.7 * t, -0.9 * t
+    cx, cy = w / 2.0, h / 2.0
+    acc = np.full((h, w), 128.0)
+    for (mx, my), a, sg in zip(tex.mu, tex.amp, tex.sigma):
+        # forward map of the blob centre: p = R(ang) (mu - c) + c + s  (then - d(y) on the right)
+        px_ = ca * (mx - cx) - sa * (my - cy) + cx + sx
+        py_ = sa * (mx - cx) + ca * (my - cy) + cy + sy
+        if right:
+            px_ -= disparity(py_)
+        r = 4.0 * sg + 3.0
+        x0, x1 = max(0, int(px_ - r)), min(w, int(px_ + r) + 2)
+        y0, y1 = max(0, int(py_ - r)), min(h, int(py_ + r) + 2)
+        if x0 >= x1 or y0 >= y1:
+            continue
+        ys, xs = np.mgrid[y0:y1, x0:x1].astype(np.float64)
+        x = xs - cx - sx
+        y = ys - cy - sy
+        if right:
+            x = x + disparity(ys)
+        u = ca * x + sa * y + cx
+        v = -sa * x + ca * y + cy
+        du = u - mx
+        dv = v - my
+        acc[y0:y1, x0:x1] += a * np.exp(-(du * du + dv * dv) / (2.0 * sg * sg))
+    acc += noise
+    return np.clip(np.rint(acc), 0, 255).astype(np.uint8)
+
+
+def stereo_sequence(n_frames: int, w: int = 752, h: int = 480, seed: int = 20260320):
+    """Yield (left, right) u8 frames of config 2."""
+    tex = make_texture(w, h, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    for t in range(n_frames):
+        left = _render(tex, w, h, t, False, 2.0 * rng.standard_normal((h, w)))
+        right = _render(tex, w, h, t, True, 2.0 * rng.standard_normal((h, w)))
+        yield left, right
+
+
+def fast9_mask(img: np.ndarray, t: int) -> np.ndarray:
+    """Vectorised FAST-9 corner test (contiguous arc of >= 9 of 16 brighter/darker by > t)."""
+    im = img.astype(np.int16)
+    h, w = im.shape
+    off = [(0, -3), (1, -3), (2, -2), (3, -1), (3, 0), (3, 1), (2, 2), (1, 3), (0, 3), (-1, 3),
+           (-2, 2), (-3, 1), (-3, 0), (-3, -1), (-2, -2), (-1, -3)]
+    c = im[3:h - 3, 3:w - 3]
+    ring = np.stack([im[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in off])
+    out = np.zeros((h, w), bool)
+    for sign in (1, -1):
+        ok = (sign * (ring - c[None])) > t
+        ok2 = np.concatenate([ok, ok[:8]], 0)
+        run = np.zeros_like(c, dtype=np.int16)
+        best = np.zeros_like(c, dtype=np.int16)
+        for k in range(ok2.shape[0]):
+            run = np.where(ok2[k], run + 1, 0)
+            best = np.maximum(best, run)
+        out[3:h - 3, 3:w - 3] |= best >= 9
+    return out
+
+
+def track_features(img: np.ndarray, n: int = 300, seed: int = 20260320, spacing: float = 20.0) -> np.ndarray:
+    """Config-2 feature positions as an (n, 6) Affine2 array {1, 0, 0, 1, x, y}."""
+    h, w = img.shape
+    mask = fast9_mask(img, 20)
+    ys, xs = np.nonzero(mask)
+    pts: list[tuple[float, float]] = []
+    for x, y in zip(xs, ys):
+        if not (20 <= x < w - 20 and 20 <= y < h - 20):
+            continue
+        if all((x - px) ** 2 + (y - py) ** 2 >= spacing ** 2 for px, py in pts[-64:]) and \
+                all((x - px) ** 2 + (y - py) ** 2 >= spacing ** 2 for px, py in pts):
+            pts.append((float(x), float(y)))
+            if len(pts) == n:
+                break
+    rng = np.random.default_rng(seed + 7)
+    while len(pts) < n:
+        pts.append((float(rng.uniform(20, w - 20)), float(rng.uniform(20, h - 20))))
+    aff = np.zeros((n, 6), np.float32)
+    aff[:, 0] = 1.0
+    aff[:, 3] = 1.0
+    aff[:, 4:6] = np.asarray(pts, np.float32)
+    return aff
+
+
+def disparity(y):
+    return 4.0 + 8.0 * y / 480.0
+
+
+def stereo_shift(aff: np.ndarray) -> np.ndarray:
+    """Where a left-image feature appears in the right image (x - d(y))."""
+    out = aff.copy()
+    out[:, 4] = aff[:, 4] - disparity(aff[:, 5])
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# Bundle-adjustment workload (config 3)
+# ----------------------------------------------------------------------------------------
+def rot_z(a: float) -> np.ndarray:
+    c, s = math.cos(a), math.sin(a)
+    return np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
+
+
+def quat_from_rot(R: np.ndarray) -> np.ndarray:
+    """nalgebra UnitQuaternion::from_rotation_matrix branch structure; returns (w, x, y, z)."""
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0.0:
+        d = math.sqrt(tr + 1.0) * 2.0
+        return np.array([0.25 * d, (R[2, 1] - R[1, 2]) / d, (R[0, 2] - R[2, 0]) / d, (R[1, 0] - R[0, 1]) / d])
+    if R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        d = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2.0
+        return np.array([(R[2, 1] - R[1, 2]) / d, 0.25 * d, (R[0, 1] + R[1, 0]) / d, (R[0, 2] + R[2, 0]) / d])
+    if R[1, 1] > R[2, 2]:
+        d = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2.0
+        return np.array([(R[0, 2] - R[2, 0]) / d, (R[0, 1] + R[1, 0]) / d, 0.25 * d, (R[1, 2] + R[2, 1]) / d])
+    d = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2.0
+    return np.array([(R[1, 0] - R[0, 1]) / d, (R[0, 2] + R[2, 0]) / d, (R[1, 2] + R[2, 1]) / d, 0.25 * d])
+
+
+def rot_from_quat(q: np.ndarray) -> np.ndarray:
+    w, x, y, z = q / np.linalg.norm(q)
+    return np.array([
+        [w * w + x * x - y * y - z * z, 2 * (x * y - w * z), 2 * (w * y + x * z)],
+        [2 * (w * z + x * y), w * w - x * x + y * y - z * z, 2 * (y * z - w * x)],
+        [2 * (x * z - w * y), 2 * (w * x + y * z), w * w - x * x - y * y + z * z]])
+
+
+def pose7_from_T_W_B(T_W_B: np.ndarray) -> np.ndarray:
+    """sliding_window.rs:218-224: T_B_W = inv(T_W_B) -> [t_B_W, q_B_W (w, x, y, z)]."""
+    R = T_W_B[:3, :3].T
+    t = -R @ T_W_B[:3, 3]
+    return np.concatenate([t, quat_from_rot(R)])
+
+
+def small_rot(rng, sigma_rad: float) -> np.ndarray:
+    v = rng.normal(0.0, sigma_rad, 3)
+    th = np.linalg.norm(v)
+    if th < 1e-15:
+        return np.eye(3)
+    k = v / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+@dataclass
+class BAProblem:
+    pose7: np.ndarray       # (n_kf, 7) initial T_B_W
+    kf_fixed: np.ndarray    # (n_kf,) u8
+    p_W: np.ndarray         # (n_lm, 3) initial
+    obs_lm: np.ndarray      # (n_obs,) i32
+    obs_kf: np.ndarray      # (n_obs,) i32
+    obs_cam: np.ndarray     # (n_obs,) u8
+    obs_uv: np.ndarray      # (n_obs, 2) f64 normalised coordinates
+    T_C_B2: np.ndarray      # (2, 16) row-major T_Cl_B, T_Cr_B
+    true_pose7: np.ndarray
+    true_p_W: np.ndarray
+
+    @property
+    def n_kf(self):
+        return self.pose7.shape[0]
+
+    @property
+    def n_lm(self):
+        return self.p_W.shape[0]
+
+    @property
+    def n_obs(self):
+        return self.obs_lm.shape[0]
+
+    def shard(self, rank: int, world: int) -> "BAProblem":
+        """Contiguous landmark range of this rank (observations follow their landmark)."""
+        lo = self.n_lm * rank // world
+        hi = self.n_lm * (rank + 1) // world
+        sel = (self.obs_lm >= lo) & (self.obs_lm < hi)
+        return BAProblem(self.pose7.copy(), self.kf_fixed.copy(), self.p_W[lo:hi].copy(),
+                         (self.obs_lm[sel] - lo).astype(np.int32), self.obs_kf[sel].copy(),
+                         self.obs_cam[sel].copy(), self.obs_uv[sel].copy(), self.T_C_B2.copy(),
+                         self.true_pose7.copy(), self.true_p_W[lo:hi].copy())
+
+
+def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int = 7,
+               noise_px: float = 0.5, init_seed: int = 11, pose_noise=(0.02, math.radians(0.5)),
+               depth_noise: float = 0.05) -> BAProblem:
+    """Config 3 (and, with other arguments, config 5's shape)."""
+    rng = np.random.default_rng(seed)
+    T_W_B = []
+    for k in range(n_kf):
+        T = np.eye(4)
+        T[:3, :3] = rot_z(0.01 * k)
+        T[:3, 3] = [0.08 * k, 0.01 * math.sin(k), 0.0]
+        T_W_B.append(T)
+    T_C_B = [np.linalg.inv(T_B_CL), np.linalg.inv(T_B_CR)]
+    # landmarks in cam0 of KF_0: U([-3,3] x [-2,2] x [2,8])
+    p_c0 = np.stack([rng.uniform(-3, 3, n_lm), rng.uniform(-2, 2, n_lm), rng.uniform(2, 8, n_lm)], 1)
+    T_W_C0 = T_W_B[0] @ T_B_CL
+    p_W = (T_W_C0[:3, :3] @ p_c0.T).T + T_W_C0[:3, 3]
+    start = rng.integers(0, n_kf - kf_per_lm + 1, n_lm)
+    obs_lm, obs_kf, obs_cam, obs_uv = [], [], [], []
+    sig = noise_px / FX_LEFT
+    for l in range(n_lm):
+        for k in range(start[l], start[l] + kf_per_lm):
+            T_B_W = np.linalg.inv(T_W_B[k])
+            for c in range(2):
+                T = T_C_B[c] @ T_B_W
+                pc = T[:3, :3] @ p_W[l] + T[:3, 3]
+                uv = pc[:2] / pc[2] + rng.normal(0.0, sig, 2)
+                obs_lm.append(l)
+                obs_kf.append(k)
+                obs_cam.append(c)
+                obs_uv.append(uv)
+    true_pose7 = np.stack([pose7_from_T_W_B(T) for T in T_W_B])
+    rng2 = np.random.default_rng(init_seed)
+    pose7 = true_pose7.copy()
+    for k in range(1, n_kf):
+        T = T_W_B[k].copy()
+        T[:3, :3] = small_rot(rng2, pose_noise[1]) @ T[:3, :3]
+        T[:3, 3] += rng2.normal(0.0, pose_noise[0] / math.sqrt(3.0), 3)
+        pose7[k] = pose7_from_T_W_B(T)
+    # 5 % depth error along the KF_0 cam0 ray
+    scale = 1.0 + rng2.uniform(-depth_noise, depth_noise, n_lm)
+    p_init = (T_W_C0[:3, :3] @ (p_c0 * scale[:, None]).T).T + T_W_C0[:3, 3]
+    kf_fixed = np.zeros(n_kf, np.uint8)
+    kf_fixed[0] = 1
+    return BAProblem(pose7=pose7, kf_fixed=kf_fixed, p_W=p_init,
+                     obs_lm=np.asarray(obs_lm, np.int32), obs_kf=np.asarray(obs_kf, np.int32),
+                     obs_cam=np.asarray(obs_cam, np.uint8), obs_uv=np.asarray(obs_uv, np.float64),
+                     T_C_B2=np.stack([T_C_B[0].reshape(16), T_C_B[1].reshape(16)]),
+                     true_pose7=true_pose7, true_p_W=p_W)

@@ -1,0 +1,208 @@
+"""GPU parity of the patch tracker (HP-T) against the CPU oracle, through the C ABI.
+
+Bars (DESIGN.md "Tracker parity"):
+  * pyramid: bit-exact (u8 output of f32 arithmetic in the reference's order);
+  * FAST grid detection: bit-exact (integer);
+  * track_points: bit-exact against the oracle in trig mode 1 (sin/cos of the SE(2) increment
+    rounded from f64, as the kernel does); against the libm-sinf oracle (trig mode 0) the valid
+    masks must agree on >= 99 % of features and positions within 1e-3 px;
+  * StereoPatchTracker: identical ids, counts and (bitwise) positions frame by frame.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _gold(name):
+    return np.load(GOLD / name, allow_pickle=False)
+
+
+@pytest.mark.parametrize("shape,levels", [((480, 752), 3), ((480, 752), 6), ((61, 97), 3), ((120, 160), 5),
+                                          ((512, 512), 6), ((33, 40), 2)])
+def test_pyramid_bitexact(gpu, oracle, shape, levels):
+    rng = np.random.default_rng(shape[0] * 1000 + levels)
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    ref = oracle.build_pyramid(img, levels)
+    out = gpu.build_image_pyramid(img, levels)
+    assert out.shape == ref.shape
+    assert np.array_equal(out, ref)
+
+
+def test_pyramid_dimensions(gpu):
+    # reference KAT (feature_tracker/src/image_operations.rs:84-94): 120x60 -> 60x30 -> 30x15
+    img = np.zeros((60, 120), np.uint8)
+    pyr = gpu.build_image_pyramid(img, 3)
+    lv = gpu.pyramid_levels(pyr, 120, 60, 3)
+    assert [x.shape for x in lv] == [(60, 120), (30, 60), (15, 30)]
+
+
+def test_pyramid_golden(gpu):
+    g = _gold("tracker_small.npz")
+    assert np.array_equal(gpu.build_image_pyramid(g["left"][0], 3), g["pyr_l0"])
+    assert np.array_equal(gpu.build_image_pyramid(g["noise_img"], 5), g["pyr_noise5"])
+
+
+def test_pyramid_synthetic_frame(gpu, oracle, stereo_frames):
+    left, _ = stereo_frames[0]
+    for levels in (3, 6):
+        assert np.array_equal(gpu.build_image_pyramid(left, levels), oracle.build_pyramid(left, levels))
+
+
+def test_track_points_golden(gpu):
+    g = _gold("tracker_small.npz")
+    w, h, L = int(g["w"]), int(g["h"]), int(g["levels"])
+    aff, valid = gpu.track_points(g["pyr_l0"], g["pyr_l1"], w, h, L, g["aff"])
+    assert np.array_equal(valid, g["t_valid_cr"].astype(bool))
+    assert np.array_equal(aff[valid], g["t_aff_cr"][valid])
+
+
+@pytest.mark.parametrize("levels", [3, 6])
+def test_track_points_bitexact(gpu, oracle, stereo_frames, levels):
+    from rsvio import synthetic as S
+    (l0, r0), (l1, r1) = stereo_frames[0], stereo_frames[1]
+    w, h = 752, 480
+    p0 = oracle.build_pyramid(l0, levels)
+    p1 = oracle.build_pyramid(l1, levels)
+    pr = oracle.build_pyramid(r0, levels)
+    aff = S.track_features(l0, 300)
+    oracle.set_trig_mode(1)
+    try:
+        for a_pyr, b_pyr in ((p0, p1), (p0, pr)):
+            ref_aff, ref_valid = oracle.track_points(a_pyr, b_pyr, w, h, levels, aff)
+            out_aff, out_valid = gpu.track_points(a_pyr, b_pyr, w, h, levels, aff)
+            assert np.array_equal(out_valid, ref_valid)
+            assert np.array_equal(out_aff[out_valid].view(np.uint32), ref_aff[ref_valid].view(np.uint32))
+            # L=6 loses tracks whose template leaves the 23x15 top level (reference behaviour)
+            assert ref_valid.mean() > (0.8 if levels == 3 else 0.3)
+    finally:
+        oracle.set_trig_mode(0)
+
+
+def test_track_points_vs_libm_oracle(gpu, oracle, stereo_frames):
+    from rsvio import synthetic as S
+    (l0, _), (l1, _) = stereo_frames[0], stereo_frames[1]
+    p0, p1 = oracle.build_pyramid(l0, 3), oracle.build_pyramid(l1, 3)
+    aff = S.track_features(l0, 300)
+    oracle.set_trig_mode(0)
+    ref_aff, ref_valid = oracle.track_points(p0, p1, 752, 480, 3, aff)
+    out_aff, out_valid = gpu.track_points(p0, p1, 752, 480, 3, aff)
+    assert (out_valid == ref_valid).mean() >= 0.99
+    both = out_valid & ref_valid
+    assert np.abs(out_aff[both] - ref_aff[both]).max() < 1e-3
+
+
+def test_track_points_edge_cases(gpu, oracle):
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (64, 80), dtype=np.uint8)
+    black = np.zeros((64, 80), np.uint8)
+    p = oracle.build_pyramid(img, 2)
+    pb = oracle.build_pyramid(black, 2)
+    aff = np.zeros((7, 6), np.float32)
+    aff[:, 0] = aff[:, 3] = 1.0
+    aff[:, 4:6] = [[1.0, 1.0], [40.0, 30.0], [79.5, 63.5], [-5.0, 10.0], [40.0, 30.0], [2.6, 2.6], [1e9, 5.0]]
+    aff[4, 0:4] = [0.0, -1.0, 1.0, 0.0]  # rotated state (rotation is carried, not used)
+    oracle.set_trig_mode(1)
+    try:
+        for a, b in ((p, p), (p, pb), (pb, p)):
+            ra, rv = oracle.track_points(a, b, 80, 64, 2, aff)
+            ga, gv = gpu.track_points(a, b, 80, 64, 2, aff)
+            assert np.array_equal(gv, rv)
+            assert np.array_equal(ga.view(np.uint32), ra.view(np.uint32))
+    finally:
+        oracle.set_trig_mode(0)
+    # empty batch
+    ga, gv = gpu.track_points(p, p, 80, 64, 2, np.zeros((0, 6), np.float32))
+    assert ga.shape == (0, 6) and gv.shape == (0,)
+
+
+def test_detect_golden(gpu):
+    g = _gold("tracker_small.npz")
+    xy, sc = gpu.detect_key_points(g["left"][0], 30, None)
+    assert np.array_equal(xy, g["det_xy"]) and np.array_equal(sc, g["det_score"])
+    ex = g["det_xy"][: len(g["det_xy"]) // 2].astype(np.float32)
+    xy, sc = gpu.detect_key_points(g["left"][0], 30, ex)
+    assert np.array_equal(xy, g["det2_xy"]) and np.array_equal(sc, g["det2_score"])
+
+
+@pytest.mark.parametrize("grid", [30, 50])
+def test_detect_bitexact(gpu, oracle, stereo_frames, grid):
+    left, _ = stereo_frames[0]
+    rng = np.random.default_rng(grid)
+    for existing in (None, rng.uniform(-10, 760, (200, 2)).astype(np.float32)):
+        ref = oracle.detect_key_points(left, grid, existing)
+        out = gpu.detect_key_points(left, grid, existing)
+        assert np.array_equal(out[0], ref[0])
+        assert np.array_equal(out[1], ref[1])
+    noise = rng.integers(0, 256, (480, 752), dtype=np.uint8)
+    assert all(np.array_equal(a, b) for a, b in zip(gpu.detect_key_points(noise, grid),
+                                                     oracle.detect_key_points(noise, grid)))
+    flat = np.full((480, 752), 77, np.uint8)
+    assert len(gpu.detect_key_points(flat, grid)[0]) == 0
+
+
+def _pipeline_compare(gpu, oracle, frames, w, h, levels, grid):
+    oracle.set_trig_mode(1)
+    try:
+        ref = oracle.StereoTracker(w, h, levels, grid, 20, 0.01)
+        trk = gpu.StereoPatchTracker(w, h, levels=levels, grid_size=grid)
+        for k, (l, r) in enumerate(frames):
+            rl, rr = ref.process_frame(l, r)
+            gl, gr = trk.process_frame(l, r)
+            for refl, gpul in ((rl, gl), (rr, gr)):
+                assert len(refl) == len(gpul), f"frame {k}"
+                assert [f[0] for f in refl] == gpul["id"].tolist()
+                assert np.array_equal(np.array([f[1] for f in refl], np.float32).view(np.uint32),
+                                      gpul["x"].view(np.uint32))
+                assert np.array_equal(np.array([f[2] for f in refl], np.float32).view(np.uint32),
+                                      gpul["y"].view(np.uint32))
+                assert np.array_equal(np.array([f[3][:4] for f in refl], np.float32).reshape(-1, 4),
+                                      gpul["r"].reshape(-1, 4))
+        trk.close()
+    finally:
+        oracle.set_trig_mode(0)
+
+
+def test_stereo_tracker_golden(gpu):
+    g = _gold("tracker_small.npz")
+    w, h = int(g["w"]), int(g["h"])
+    trk = gpu.StereoPatchTracker(w, h, levels=3, grid_size=30)
+    rows_l, rows_r = [], []
+    for k in range(4):
+        fl, fr = trk.process_frame(g["left"][k], g["right"][k])
+        rows_l += [(k, float(f["id"]), float(f["x"]), float(f["y"])) for f in fl]
+        rows_r += [(k, float(f["id"]), float(f["x"]), float(f["y"])) for f in fr]
+    assert np.array_equal(np.array(rows_l), g["pipe_l"])
+    assert np.array_equal(np.array(rows_r), g["pipe_r"])
+
+
+def test_stereo_tracker_pipeline(gpu, oracle, stereo_frames):
+    _pipeline_compare(gpu, oracle, stereo_frames, 752, 480, 6, 50)
+
+
+def test_stereo_tracker_pipeline_l3(gpu, oracle, stereo_frames):
+    _pipeline_compare(gpu, oracle, stereo_frames[:3], 752, 480, 3, 30)
+
+
+def test_stereo_tracker_remove_ids(gpu, stereo_frames):
+    trk = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50)
+    l0, r0 = stereo_frames[0]
+    fl, fr = trk.process_frame(l0, r0)
+    drop = fl["id"][::3]
+    trk.remove_id(drop)
+    l1, r1 = stereo_frames[1]
+    gl, gr = trk.process_frame(l1, r1)
+    assert not set(drop.tolist()) & set(gl["id"].tolist())
+    assert not set(drop.tolist()) & set(gr["id"].tolist())
+    assert np.all(np.diff(gl["id"].astype(np.int64)) > 0)
+
+
+def test_stereo_tracker_bad_input(gpu):
+    trk = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50)
+    with pytest.raises(ValueError):
+        trk.process_frame(np.zeros((10, 10), np.uint8), np.zeros((10, 10), np.uint8))
+    with pytest.raises(gpu.RsvioError):
+        gpu.StereoPatchTracker(8, 8, levels=3)
