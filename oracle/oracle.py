@@ -192,13 +192,12 @@ def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, hub
 def ba_solve(prob, cfg=None):
     """Returns (pose7, p_W, BaResult) after the oracle's LM; prob is a synthetic.BAProblem-like."""
     cfg = cfg or lm_cfg()
-    pose = np.ascontiguousarray(prob.pose7, np.float64).copy()
-    pw = np.ascontiguousarray(prob.p_W, np.float64).copy()
+    a = _problem_arrays(prob)
+    pose = a[0].copy()
+    pw = a[2].copy()
     res = BaResult()
-    load().orc_ba_solve(pose.shape[0], _p(pose), _p(np.ascontiguousarray(prob.kf_fixed, np.uint8)), pw.shape[0],
-                        _p(pw), len(prob.obs_lm), _p(prob.obs_lm), _p(prob.obs_kf), _p(prob.obs_cam),
-                        _p(prob.obs_uv), _p(np.ascontiguousarray(prob.T_C_B2, np.float64)), C.byref(cfg),
-                        C.byref(res))
+    load().orc_ba_solve(pose.shape[0], _p(pose), _p(a[1]), pw.shape[0], _p(pw), len(a[3]), _p(a[3]), _p(a[4]),
+                        _p(a[5]), _p(a[6]), _p(a[7]), C.byref(cfg), C.byref(res))
     return pose, pw, res
 
 
@@ -208,27 +207,29 @@ def ba_build_system(prob, lam, huber_delta=2.0):
     S = np.zeros((n, n))
     b = np.zeros(n)
     cost = C.c_double(0)
-    load().orc_ba_build_system(prob.pose7.shape[0], _p(np.ascontiguousarray(prob.pose7)),
-                               _p(np.ascontiguousarray(prob.kf_fixed, np.uint8)), prob.p_W.shape[0],
-                               _p(np.ascontiguousarray(prob.p_W)), len(prob.obs_lm), _p(prob.obs_lm), _p(prob.obs_kf),
-                               _p(prob.obs_cam), _p(prob.obs_uv), _p(np.ascontiguousarray(prob.T_C_B2)), huber_delta,
-                               lam, _p(S), _p(b), C.byref(cost))
+    a = _problem_arrays(prob)  # keep the contiguous copies alive across the call
+    load().orc_ba_build_system(a[0].shape[0], _p(a[0]), _p(a[1]), a[2].shape[0], _p(a[2]), len(a[3]), _p(a[3]),
+                               _p(a[4]), _p(a[5]), _p(a[6]), _p(a[7]), huber_delta, lam, _p(S), _p(b), C.byref(cost))
     return S, b, cost.value
+
+
+def _problem_arrays(prob):
+    return (np.ascontiguousarray(prob.pose7, np.float64), np.ascontiguousarray(prob.kf_fixed, np.uint8),
+            np.ascontiguousarray(prob.p_W, np.float64), np.ascontiguousarray(prob.obs_lm, np.int32),
+            np.ascontiguousarray(prob.obs_kf, np.int32), np.ascontiguousarray(prob.obs_cam, np.uint8),
+            np.ascontiguousarray(prob.obs_uv, np.float64), np.ascontiguousarray(prob.T_C_B2, np.float64))
 
 
 def factor_linearize(p_W, pose7, T_C_B, uv, T_B_W_fixed=None):
     r = np.zeros(2)
     J = np.zeros((2, 9))
-    load().orc_ba_factor_linearize(_p(np.ascontiguousarray(p_W, np.float64)),
-                                   _p(np.ascontiguousarray(pose7, np.float64)) if pose7 is not None else None,
-                                   _p(np.ascontiguousarray(T_B_W_fixed, np.float64)) if T_B_W_fixed is not None else None,
-                                   _p(np.ascontiguousarray(T_C_B, np.float64)),
-                                   _p(np.ascontiguousarray(uv, np.float64)), _p(r), _p(J))
+    keep = [None if v is None else np.ascontiguousarray(v, np.float64) for v in (p_W, pose7, T_B_W_fixed, T_C_B, uv)]
+    load().orc_ba_factor_linearize(*[_p(v) for v in keep], _p(r), _p(J))
     return r, J
 
 
 def se3_plus(pose7, delta):
     out = np.zeros(7)
-    load().orc_se3_plus(_p(np.ascontiguousarray(pose7, np.float64)), _p(np.ascontiguousarray(delta, np.float64)),
-                        _p(out))
+    a, d = np.ascontiguousarray(pose7, np.float64), np.ascontiguousarray(delta, np.float64)
+    load().orc_se3_plus(_p(a), _p(d), _p(out))
     return out

@@ -1,0 +1,229 @@
+"""Host-side mirror of the reference's bundle-adjustment API over the C ABI.
+
+* ``BundleAdjuster`` -- the solver handle (rsvio_ba_*): replaces the apex-solver
+  ``LevenbergMarquardt::optimize`` call of ``SlidingWindow::optimize``
+  (src/estimator/sliding_window.rs:325) with the HIP Schur-complement LM; optional landmark
+  sharding over ranks with an RCCL all-reduce (``attach_comm``).
+* ``SlidingWindow`` -- mirrors ``SlidingWindow`` (sliding_window.rs:21-486): keyframe FIFO,
+  problem assembly (stereo-landmark rule, depth-2 initialisation, KF_0 fixed), guards,
+  rollback on failure, map points kept as f32.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import deque
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):
+    """sliding_window.rs:126-135 (max 20 iterations, cost tol 1e-6, parameter tol 1e-9) + Huber(2.0)."""
+    return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class BundleAdjuster:
+    """One device-resident BA solver (one HIP stream)."""
+
+    def __init__(self, max_keyframes=21, max_landmarks=1 << 16, max_observations=1 << 20, device=0):
+        lib = _lib.load()
+        p = _lib.BaParams(max_keyframes, max_landmarks, max_observations, device)
+        h = C.c_void_p()
+        check(lib.rsvio_ba_create(C.byref(p), C.byref(h)))
+        self._h = h
+        self.n_kf = self.n_lm = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().rsvio_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def attach_comm(self, nranks: int, rank: int, unique_id: bytes):
+        if nranks > 1:
+            buf = (C.c_uint8 * len(unique_id)).from_buffer_copy(unique_id)
+            check(_lib.load().rsvio_ba_attach_comm(self._h, nranks, rank, buf))
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(_lib.load().rsvio_rccl_unique_id(buf, 128))
+        return bytes(buf)
+
+    def set_problem(self, pose7, kf_fixed, p_W, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2):
+        self._keep = [_c(pose7, np.float64), _c(kf_fixed, np.uint8), _c(p_W, np.float64).reshape(-1, 3),
+                      _c(obs_lm, np.int32), _c(obs_kf, np.int32), _c(obs_cam, np.uint8),
+                      _c(obs_uv, np.float64).reshape(-1, 2), _c(T_C_B2, np.float64).reshape(2, 16)]
+        pose, fixed, pw, lm, kf, cam, uv, tcb = self._keep
+        self.n_kf, self.n_lm = pose.shape[0], pw.shape[0]
+        check(_lib.load().rsvio_ba_set_problem(self._h, self.n_kf, ptr(pose), ptr(fixed), self.n_lm, ptr(pw),
+                                               len(lm), ptr(lm), ptr(kf), ptr(cam), ptr(uv), ptr(tcb)))
+
+    def set_problem_from(self, prob):
+        self.set_problem(prob.pose7, prob.kf_fixed, prob.p_W, prob.obs_lm, prob.obs_kf, prob.obs_cam, prob.obs_uv,
+                         prob.T_C_B2)
+
+    def run(self, cfg=None) -> _lib.BaResult:
+        res = _lib.BaResult()
+        check(_lib.load().rsvio_ba_run(self._h, C.byref(cfg or lm_cfg()), C.byref(res)))
+        return res
+
+    def state(self):
+        pose = np.zeros((self.n_kf, 7))
+        pw = np.zeros((self.n_lm, 3))
+        check(_lib.load().rsvio_ba_get_state(self._h, ptr(pose), ptr(pw)))
+        return pose, pw
+
+    def build_system(self, lam, huber_delta=2.0):
+        nfree = int((self._keep[1] == 0).sum())
+        S = np.zeros((6 * nfree, 6 * nfree))
+        b = np.zeros(6 * nfree)
+        cost = C.c_double()
+        check(_lib.load().rsvio_ba_build_system(self._h, lam, huber_delta, ptr(S), ptr(b), C.byref(cost)))
+        return S, b, cost.value
+
+    def solve(self, pose7, kf_fixed, p_W, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2, cfg=None):
+        """rsvio_ba_solve: returns (pose7, p_W, result); inputs are not modified."""
+        pose = _c(pose7, np.float64).copy()
+        pw = _c(p_W, np.float64).reshape(-1, 3).copy()
+        lm, kf, cam = _c(obs_lm, np.int32), _c(obs_kf, np.int32), _c(obs_cam, np.uint8)
+        uv, tcb, fixed = _c(obs_uv, np.float64).reshape(-1, 2), _c(T_C_B2, np.float64), _c(kf_fixed, np.uint8)
+        res = _lib.BaResult()
+        check(_lib.load().rsvio_ba_solve(self._h, pose.shape[0], ptr(pose), ptr(fixed), pw.shape[0], ptr(pw), len(lm),
+                                         ptr(lm), ptr(kf), ptr(cam), ptr(uv), ptr(tcb), C.byref(cfg or lm_cfg()),
+                                         C.byref(res)))
+        self.n_kf, self.n_lm = pose.shape[0], pw.shape[0]
+        return pose, pw, res
+
+
+# --------------------------------------------------------------------------------------------
+# SlidingWindow mirror
+# --------------------------------------------------------------------------------------------
+@dataclass
+class Frame:
+    """The fields of estimator::Frame (src/estimator/frame.rs:20-47) that the BA reads."""
+    frame_id: int
+    T_W_B: np.ndarray = field(default_factory=lambda: np.eye(4))
+    T_B_Cl: np.ndarray = field(default_factory=lambda: np.eye(4))
+    T_B_Cr: np.ndarray = field(default_factory=lambda: np.eye(4))
+    is_keyframe: bool = True
+    # (feature_id, undistorted (x, y)) per camera, in feature order
+    left_features: list = field(default_factory=list)
+    right_features: list = field(default_factory=list)
+
+
+def _quat_from_rot(R):
+    from .synthetic import quat_from_rot
+    return quat_from_rot(R)
+
+
+def _T_from_pose7(p7):
+    from .synthetic import rot_from_quat
+    T = np.eye(4)
+    T[:3, :3] = rot_from_quat(np.asarray(p7[3:7]))
+    T[:3, 3] = p7[:3]
+    return T
+
+
+class SlidingWindow:
+    """Keyframe FIFO + BA problem assembly (sliding_window.rs:21-486) over the GPU solver."""
+
+    def __init__(self, max_frames: int, device: int = 0, solver: BundleAdjuster | None = None):
+        self.max_frames = max_frames
+        self.keyframes: deque[Frame] = deque()
+        self.map_points: dict[int, np.ndarray] = {}  # feature id -> [f32; 3]
+        self.solver = solver or BundleAdjuster(max_keyframes=max(max_frames, 2), device=device)
+        self.last_result = None
+
+    def add_frame(self, frame: Frame) -> bool:
+        if not frame.is_keyframe:
+            return False
+        if len(self.keyframes) >= self.max_frames:
+            self.keyframes.popleft()
+        self.keyframes.append(frame)
+        return True
+
+    def __len__(self):
+        return len(self.keyframes)
+
+    def is_full(self) -> bool:
+        return len(self.keyframes) >= self.max_frames
+
+    def get_keyframe_poses(self):
+        return [f.T_W_B.copy() for f in self.keyframes]
+
+    def build_problem(self):
+        """sliding_window.rs:174-300 in canonical order (frames, left then right, feature order)."""
+        kfs = list(self.keyframes)
+        T_Cl_B = np.linalg.inv(kfs[0].T_B_Cl)
+        T_Cr_B = np.linalg.inv(kfs[0].T_B_Cr)
+        cnt_l, cnt_r = {}, {}
+        for f in kfs:
+            for fid, _ in f.left_features:
+                cnt_l[fid] = cnt_l.get(fid, 0) + 1
+            for fid, _ in f.right_features:
+                cnt_r[fid] = cnt_r.get(fid, 0) + 1
+        pose7 = np.zeros((len(kfs), 7))
+        kf_fixed = np.zeros(len(kfs), np.uint8)
+        kf_fixed[0] = 1
+        lm_index: dict[int, int] = {}
+        p_init, obs_lm, obs_kf, obs_cam, obs_uv = [], [], [], [], []
+        for i, f in enumerate(kfs):
+            T_B_W = np.linalg.inv(f.T_W_B)
+            pose7[i, :3] = T_B_W[:3, 3]
+            pose7[i, 3:] = _quat_from_rot(T_B_W[:3, :3])
+            for cam, (feats, T_C_B) in enumerate(((f.left_features, T_Cl_B), (f.right_features, T_Cr_B))):
+                for fid, uv in feats:
+                    if cnt_l.get(fid, 0) == 0 or cnt_r.get(fid, 0) == 0:
+                        continue
+                    if fid not in lm_index:
+                        lm_index[fid] = len(p_init)
+                        if fid in self.map_points:
+                            p_init.append(np.asarray(self.map_points[fid], np.float32).astype(np.float64))
+                        else:
+                            # depth-2.0 ray (sliding_window.rs:256-269)
+                            p_C = np.array([float(np.float32(uv[0])), float(np.float32(uv[1])), 2.0])
+                            T_B_C = np.linalg.inv(T_C_B)
+                            p_W = f.T_W_B[:3, :3] @ (T_B_C[:3, :3] @ p_C + T_B_C[:3, 3]) + f.T_W_B[:3, 3]
+                            p_init.append(p_W)
+                    obs_lm.append(lm_index[fid])
+                    obs_kf.append(i)
+                    obs_cam.append(cam)
+                    obs_uv.append([float(np.float32(uv[0])), float(np.float32(uv[1]))])
+        p_init = np.array(p_init, np.float64).reshape(-1, 3)
+        T_C_B2 = np.stack([T_Cl_B.reshape(16), T_Cr_B.reshape(16)])
+        ids = sorted(lm_index, key=lm_index.get)
+        return (pose7, kf_fixed, p_init, np.array(obs_lm, np.int32), np.array(obs_kf, np.int32),
+                np.array(obs_cam, np.uint8), np.array(obs_uv, np.float64).reshape(-1, 2), T_C_B2, ids)
+
+    def optimize(self, cfg=None) -> bool:
+        """Returns Ok(true)/Ok(false) as a bool; raises RuntimeError for a non-full window (:137-149)."""
+        if not self.keyframes:
+            raise RuntimeError("Window is empty")
+        if len(self.keyframes) < self.max_frames:
+            raise RuntimeError("Need more keyframes")
+        pose7, fixed, p_init, lm, kf, cam, uv, tcb, ids = self.build_problem()
+        num_vars = len(self.keyframes) + len(p_init)  # KF_0 is in initial_values too (:217-226)
+        if len(lm) < 6 or len(lm) < num_vars:
+            self.last_result = None
+            return False
+        pose, pw, res = self.solver.solve(pose7, fixed, p_init, lm, kf, cam, uv, tcb, cfg)
+        self.last_result = res
+        if res.status <= 0:
+            return False  # revert: nothing was modified
+        self.map_points = {fid: pw[j].astype(np.float32) for j, fid in enumerate(ids)}
+        for i, f in enumerate(self.keyframes):
+            f.T_W_B = np.linalg.inv(_T_from_pose7(pose[i]))
+        return True

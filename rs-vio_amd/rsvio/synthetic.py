@@ -283,6 +283,8 @@ def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int =
     p_init = (T_W_C0[:3, :3] @ (p_c0 * scale[:, None]).T).T + T_W_C0[:3, 3]
     kf_fixed = np.zeros(n_kf, np.uint8)
     kf_fixed[0] = 1
+    p_init = np.ascontiguousarray(p_init)
+    p_W = np.ascontiguousarray(p_W)
     return BAProblem(pose7=pose7, kf_fixed=kf_fixed, p_W=p_init,
                      obs_lm=np.asarray(obs_lm, np.int32), obs_kf=np.asarray(obs_kf, np.int32),
                      obs_cam=np.asarray(obs_cam, np.uint8), obs_uv=np.asarray(obs_uv, np.float64),
