@@ -1,0 +1,339 @@
+#!/usr/bin/env python3
+"""bench.py -- stereo frames/sec (tracker + BA) on the synthetic EuRoC-shaped stream.
+
+One step = one stereo frame of BASELINE.json config 2 through the patch tracker (2 pyramids,
+L=3, + track_points x 3: cam0 temporal, cam1 temporal, cam0->cam1 stereo, 300 features each,
+forward + backward) followed by one full sliding-window BA solve of config 3 (10 keyframes,
+KF_0 fixed, 2000 landmarks per GPU, 24,000 observations per GPU, LM to convergence, <= 20
+iterations) -- i.e. every frame is treated as a keyframe (worst case of estimator.rs:243-246).
+Inputs are resident in HBM before the timed region; nothing crosses PCIe inside a step except
+the LM status word the host loop reads once per iteration.
+
+Multi-GPU (torchrun, one process per GPU): the tracker runs as independent replicas (each rank
+its own stream); the BA is ONE problem whose landmarks are sharded 2000 per rank (weak scaling)
+with an RCCL all-reduce of the reduced camera system per LM iteration.  value = frames of all
+ranks / max-over-ranks time.
+
+Also reported: BA ms per LM iteration, tracker ms per frame, the dominant kernel's roofline
+(HIP events on the stream it runs on) and the CPU oracle baseline on the host cores (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT), str(ROOT / "rs-vio_amd")]
+
+import numpy as np  # noqa: E402
+
+METRIC = "stereo frames/sec (tracker+BA) on 752×480 EuRoC stream; BA ms/iter at window=10"
+W, H, LEVELS, NFEAT = 752, 480, 3, 300
+MAX_IT, THRESH = 20, 0.01
+N_FRAMES = 4                       # palindromic cycle 0,1,2,3,2,1,0,... (one frame of motion per step)
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: 8 TB/s spec
+FP64_PEAK_TFLOPS = 78.6            # MI355X FP64 vector (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------------------
+# Algorithmic work per unit, frozen here and in DESIGN.md
+# ---------------------------------------------------------------------------------------
+def tracker_bytes_per_frame(calls: int) -> int:
+    """2 pyramids (source reads + level writes) + 11x11 patch footprint per (call, level) in
+    template and target image + 48 B feature state per call."""
+    pyr = 2 * ((LEVELS - 1) * W * H + sum((W >> i) * (H >> i) for i in range(1, LEVELS)))
+    return pyr + calls * LEVELS * 2 * 121 + calls * 48
+
+
+def lk_bytes_per_launch(calls: int) -> int:
+    return calls * LEVELS * 2 * 121 + calls * 48
+
+
+def ba_flops_per_iter(n_obs: int, n_lm: int, k_per_lm: int, n_free: int) -> float:
+    """F = N_obs (470 + 50) + sum_l [30 + K 108 + K(K+1)/2 216 + K 36 + (K 36 + 18)] + n^3/3 + 2 n^2."""
+    K = k_per_lm
+    per_lm = 30 + K * 108 + K * (K + 1) / 2 * 216 + K * 36 + (K * 36 + 18)
+    n = 6 * n_free
+    return n_obs * 520 + n_lm * per_lm + n ** 3 / 3 + 2 * n * n
+
+
+# ---------------------------------------------------------------------------------------
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class TrackerWorkload:
+    """Config 2 on device: per-frame pyramids (left, right) + 3 track_points batches."""
+
+    def __init__(self, device: int):
+        import ctypes as C
+
+        import torch
+
+        from rsvio import _lib
+        from rsvio import synthetic as S
+        self.C, self.torch, self.L = C, torch, _lib
+        lib = _lib.load()
+        t0 = time.time()
+        frames = list(S.stereo_sequence(N_FRAMES, W, H))
+        log(f"[bench] rendered {N_FRAMES} stereo frames in {time.time() - t0:.1f}s")
+        # true feature positions per frame: cam0 = FAST corners of frame 0 moved by the synthetic motion
+        aff0 = S.track_features(frames[0][0], NFEAT)
+        ang = math.radians(0.2)
+        c = np.array([W / 2.0, H / 2.0])
+        affs0, affs1 = [], []
+        for t in range(N_FRAMES):
+            R = np.array([[math.cos(ang * t), -math.sin(ang * t)], [math.sin(ang * t), math.cos(ang * t)]])
+            a = aff0.copy()
+            a[:, 4:6] = ((R @ (aff0[:, 4:6] - c).T).T + c + np.array([1.7, -0.9]) * t).astype(np.float32)
+            affs0.append(a)
+            affs1.append(S.stereo_shift(a))
+        dev = torch.device("cuda", device)
+        self.imgs = torch.from_numpy(np.stack([np.stack(f) for f in frames])).to(dev)       # F x 2 x H x W
+        self.aff0 = torch.from_numpy(np.stack(affs0)).to(dev)                               # F x N x 6
+        self.aff1 = torch.from_numpy(np.stack(affs1)).to(dev)
+        self.pyr_bytes = int(lib.rsvio_pyramid_bytes(W, H, LEVELS))
+        self.pyr = torch.empty((2, 2, self.pyr_bytes), dtype=torch.uint8, device=dev)      # slot x cam
+        self.out = torch.empty((3, NFEAT, 6), dtype=torch.float32, device=dev)
+        self.valid = torch.empty((3, NFEAT), dtype=torch.uint8, device=dev)
+        ctx = C.c_void_p()
+        _lib.check(lib.rsvio_track_ctx_create(W, H, LEVELS, device, C.byref(ctx)))
+        self.ctx = ctx
+        self.lib = lib
+        self.seq = [0, 1, 2, 3, 2, 1]
+        self.k = 0
+        self.slot = 0
+        self.stream = torch.cuda.current_stream(dev)
+        self.ev = []
+        # prime: pyramids of the first frame
+        self._pyramids(self.seq[0], self.slot)
+
+    def _pyramids(self, t, slot):
+        s = self.stream.cuda_stream
+        self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, self.imgs[t].data_ptr(), 2,
+                                                     self.pyr[slot].data_ptr(), s))
+
+    def step(self, timed: bool):
+        """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches."""
+        C = self.C
+        t = self.seq[self.k % len(self.seq)]
+        t2 = self.seq[(self.k + 1) % len(self.seq)]
+        prev, cur = self.slot, 1 - self.slot
+        self._pyramids(t2, cur)
+        b = (self.L.TrackBatch * 3)()
+        spec = [(self.pyr[prev, 0], self.pyr[cur, 0], self.aff0[t]),
+                (self.pyr[prev, 1], self.pyr[cur, 1], self.aff1[t]),
+                (self.pyr[cur, 0], self.pyr[cur, 1], self.aff0[t2])]
+        for i, (p0, p1, a) in enumerate(spec):
+            b[i] = self.L.TrackBatch(p0.data_ptr(), p1.data_ptr(), a.data_ptr(), self.out[i].data_ptr(),
+                                     self.valid[i].data_ptr(), NFEAT)
+        if timed:
+            e0 = self.torch.cuda.Event(enable_timing=True)
+            e1 = self.torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+        self.L.check(self.lib.rsvio_track_points_d(self.ctx, b, 3, MAX_IT, C.c_float(THRESH), self.stream.cuda_stream))
+        if timed:
+            e1.record(self.stream)
+            self.ev.append((e0, e1))
+        self.slot = cur
+        self.k += 1
+
+    def lk_ms(self):
+        if not self.ev:
+            return float("nan")
+        return float(np.mean([a.elapsed_time(b) for a, b in self.ev]))
+
+
+class BAWorkload:
+    def __init__(self, device: int, world: int, rank: int):
+        from rsvio import synthetic as S
+        from rsvio.ba import BundleAdjuster
+        t0 = time.time()
+        full = S.ba_problem(n_lm=2000 * world)
+        self.full = full
+        self.prob = full.shard(rank, world) if world > 1 else full
+        log(f"[bench] rank {rank}: BA shard {self.prob.n_lm} landmarks / {self.prob.n_obs} obs "
+            f"(global {full.n_lm}/{full.n_obs}) built in {time.time() - t0:.1f}s")
+        self.ba = BundleAdjuster(max_keyframes=full.n_kf, max_landmarks=self.prob.n_lm,
+                                 max_observations=self.prob.n_obs, device=device)
+        if world > 1:
+            import torch.distributed as dist
+            obj = [BundleAdjuster.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            self.ba.attach_comm(world, rank, obj[0])
+        self.ba.set_problem_from(self.prob)
+        self.iters = []
+        self.solve_ms = []
+
+    def step(self, timed: bool):
+        r = self.ba.run()
+        if r.status <= 0:
+            raise RuntimeError(f"BA solve failed with status {r.status}")
+        if timed:
+            self.iters.append(r.iterations)
+            self.solve_ms.append(r.solve_ms)
+        return r
+
+
+def cpu_baseline(frames_budget_s: float):
+    """The oracle (C++ restatement of the reference) on the host: same tracker frame + BA solve."""
+    from oracle import oracle as O
+    from rsvio import synthetic as S
+    frames = list(S.stereo_sequence(2, W, H))
+    aff0 = S.track_features(frames[0][0], NFEAT)
+    aff1 = S.stereo_shift(aff0)
+    affn = aff0.copy()
+    affn[:, 4:6] += np.array([1.7, -0.9], np.float32)
+    prob = S.ba_problem()
+    pyr_prev = [O.build_pyramid(frames[0][c], LEVELS) for c in range(2)]
+    n, t_track, t_ba = 0, 0.0, 0.0
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < frames_budget_s or n < 2:
+        t0 = time.perf_counter()
+        pc = [O.build_pyramid(frames[1][c], LEVELS) for c in range(2)]
+        O.track_points(pyr_prev[0], pc[0], W, H, LEVELS, aff0, MAX_IT, THRESH)
+        O.track_points(pyr_prev[1], pc[1], W, H, LEVELS, aff1, MAX_IT, THRESH)
+        O.track_points(pc[0], pc[1], W, H, LEVELS, affn, MAX_IT, THRESH)
+        t1 = time.perf_counter()
+        _, _, r = O.ba_solve(prob)
+        t2 = time.perf_counter()
+        t_track += t1 - t0
+        t_ba += t2 - t1
+        n += 1
+    fps = n / (t_track + t_ba)
+    return {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames of config 2 (2 pyramids + 3x300 track_points) each followed by one config-3 "
+                      f"BA solve ({r.iterations} LM iterations), oracle/ C++ restatement, 1 thread",
+            "tracker_ms_per_frame": round(1e3 * t_track / n, 3), "ba_ms_per_solve": round(1e3 * t_ba / n, 3),
+            "ba_ms_per_iter": round(1e3 * t_ba / n / max(r.iterations, 1), 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = setup_dist()
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    import torch
+
+    import rsvio
+    arch = rsvio.require_device(local)
+    log(f"[bench] rank {rank}/{world} on cuda:{local} ({arch})")
+    trk = TrackerWorkload(local)
+    ba = BAWorkload(local, world, rank)
+
+    for _ in range(args.warmup):
+        trk.step(False)
+        ba.step(False)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trk.step(True)
+        ba.step(True)
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, world)
+
+    frames = world * args.steps
+    value = frames / elapsed
+    lk_ms = trk.lk_ms()
+    ba_iters = float(np.mean(ba.iters))
+    ba_solve_ms = float(np.mean(ba.solve_ms))
+    ba_ms_iter = ba_solve_ms / ba_iters
+    calls = 3 * NFEAT * 2
+    lk_bytes = lk_bytes_per_launch(calls)
+    achieved = lk_bytes / (lk_ms * 1e-3) / 1e9
+    prob = ba.prob
+    flops = ba_flops_per_iter(prob.n_obs, prob.n_lm, 6, int((prob.kf_fixed == 0).sum()))
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (tracker) / f64 (BA)",
+        "data": "synthetic (procedural EuRoC-shaped stereo texture + synthetic 10-KF landmark window; "
+                "no dataset offline)",
+        "config": {"workload": "config 2 + config 3 per frame: 752x480 stereo, 300 feats, 52-pt pattern, L=3, "
+                               "track_points x3 fwd+bwd; then one BA solve 10 KF x 2000 landmarks/GPU "
+                               "(24,000 obs/GPU), Schur LM <= 20 it; every frame a keyframe",
+                   "image": "752x480", "features": NFEAT, "levels": LEVELS, "keyframes": 10,
+                   "landmarks_per_gpu": prob.n_lm, "observations_per_gpu": prob.n_obs,
+                   "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s) (RCCL)"},
+        "ba_ms_per_iter": round(ba_ms_iter, 4),
+        "ba_iterations": ba_iters,
+        "ba_ms_per_solve": round(ba_solve_ms, 4),
+        "tracker_lk_ms_per_frame": round(lk_ms, 4),
+        "roofline": {"kernel": "lk_track_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": None,
+                     "algorithmic_bytes_per_launch": lk_bytes, "launch_ms": round(lk_ms, 4),
+                     "note": "latency-bound: 900 one-wave workgroups (fwd+bwd chains) on 256 CUs"},
+        "ba_roofline": {"bound": "fp64", "flop_per_iter": flops,
+                        "achieved_tflops": round(flops / (ba_ms_iter * 1e-3) / 1e12, 4),
+                        "peak_tflops": FP64_PEAK_TFLOPS},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(args.cpu_seconds)
+        cb["cores"] = 1
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    ba.ba.close()
+
+
+if __name__ == "__main__":
+    main()

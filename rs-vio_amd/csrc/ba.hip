@@ -5,21 +5,23 @@
 // Huber(2.0) (sliding_window.rs:295-296), and apex-solver's LevenbergMarquardt with
 // SparseSchurComplement (sliding_window.rs:126-135,325) -- restated as DESIGN.md "BA LM".
 //
-// Layout (landmark-major, built once per problem on the host, CSR):
+// Layout (landmark-major, built once per problem on the host):
 //   obs   sorted by (landmark, keyframe, camera)
-//   slot  = (landmark, keyframe) group of 1-2 observations; slots sorted like obs
-//   pairs = for every upper-triangular camera block (fa <= fb), the (slot_a, slot_b) pairs of
-//           landmarks that both keyframes observe (ascending landmark)
-// Per LM iteration (all on one HIP stream, one status read-back):
-//   K4a ba_slot_linearize   thread / slot     residual, Jacobian, Huber; V, g_p, W, U, g_c slot sums
-//   K4b ba_landmark_eliminate thread / landmark (V + lambda I)^-1, Y = W V^-1, Y g_p
-//   K4c ba_schur_blocks     workgroup / 6x6 camera block: S = U + lambda I - sum Y W^T, b, cost
-//   [RCCL all-reduce of S, b, g_c, cost when sharded]
-//   K5  ba_dense_solve      1 workgroup: Cholesky of the 6(W-1) camera system in LDS, SE3 (+) trial poses
-//   K6a ba_backsub_cost     thread / landmark: dp = V^-1 (-g_p - W^T dc), trial point, trial cost
-//   K6b ba_reduce_trial     1 workgroup: fixed-order tree sums of the per-landmark partials
-//   [RCCL all-reduce of the 5 trial scalars when sharded]
-//   K7  ba_lm_decide        1 workgroup: gain ratio, accept/reject, lambda update, termination
+//   slot  = (landmark, keyframe) group of 1-2 observations, sorted like obs
+//   wave  = a run of whole landmarks with <= 64 slots: one lane per slot
+//   chunk = <= 64 (slot_a, slot_b) pairs of one upper-triangular 6x6 camera block (fa <= fb)
+// Per LM iteration (one HIP stream; the host reads the LM state once per chunk of iterations):
+//   K4  ba_linearize_eliminate  wave / landmark group: residual + Jacobian + Huber per slot,
+//                               V, g_p summed over the landmark's lanes, (V + lambda I)^-1,
+//                               Y = W V^-1, Y g_p -- per-slot Schur factors to HBM
+//   K4c ba_schur_chunks         wave / 64 pairs: -Y_a W_b^T (+ U on the diagonal), lane-ordered sums
+//   [RCCL all-reduce of the per-rank reduced system when sharded]
+//   K5  ba_camera_solve         1 workgroup: fixed-order chunk sums -> S, b in LDS, Cholesky,
+//                               substitutions, SE3 (+) trial poses
+//   K6  ba_backsub_cost         wave / landmark group: dp = V^-1 (-g_p - W^T dc), trial point,
+//                               trial cost
+//   [RCCL all-reduce of 4 trial scalars when sharded]
+//   K7  ba_lm_decide            gain ratio, accept / reject (buffer flip), lambda, termination
 // Every reduction has a fixed order (no floating-point atomics): results are run-to-run identical.
 #include <rccl/rccl.h>
 
@@ -35,9 +37,15 @@ namespace rsvio {
 
 namespace {
 
-constexpr int kMaxFree = 20;           // 6 * 20 = 120-dim camera system in LDS
-constexpr int kSlotFields = 55;        // V6 gp3 W18 U21 gc6 cost1
-enum { F_V = 0, F_GP = 6, F_W = 9, F_U = 27, F_GC = 48, F_COST = 54 };
+constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
+constexpr int kMaxN = 6 * kMaxFree;
+constexpr int kLdA = kMaxN + 1;         // odd stride
+// per-slot Schur factors, one contiguous 576-B record per slot (AoS): Y, W, U (packed), b, g_c
+enum { SY = 0, SW = 18, SU = 36, SB = 57, SG = 63, kSlotF = 72 };
+constexpr int kBlockF = 48;             // 36 S + 6 b + 6 g_c per camera block workgroup
+constexpr int kShLd = 257;              // LDS row stride (doubles) of the per-thread block partials
+constexpr int kPartA = 2;               // cost, singular-landmark count per wave
+constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per wave
 
 struct Mat4 {
     double m[16];
@@ -81,7 +89,7 @@ __device__ __forceinline__ bool linearize(const double* pW, const Pose& P, const
     pC[0] = tmp[0] + TCB[3];
     pC[1] = tmp[1] + TCB[7];
     pC[2] = tmp[2] + TCB[11];
-    if (pC[2] <= 0.0) {
+    if (pC[2] <= 0.0) {  // cheirality (factors.rs:391-403)
         r[0] = 1e6;
         r[1] = 1e6;
         if (want_j)
@@ -188,36 +196,100 @@ __device__ void se3_plus(const double* p7, const double* d, double* out) {
     for (int i = 0; i < 4; ++i) out[3 + i] = qn[i] / nn;
 }
 
-// LM bookkeeping that lives on the device (read back once per iteration)
+__device__ __forceinline__ int utri(int a, int c) {  // index of (min, max) in a packed 6x6 upper triangle
+    int i = a < c ? a : c, j = a < c ? c : a;
+    return i * 6 - i * (i - 1) / 2 + (j - i);
+}
+
+// LM bookkeeping that lives on the device (read back once per chunk of iterations)
 struct LmState {
     double lambda, nu, cost, initial_cost;
-    double dc2, gcdc;                    // from K5
-    double new_cost, dp2, gpdp, x2p;     // from K6b (after the all-reduce)
+    double dc2, gcdc;
+    double new_cost, dp2, gpdp, x2;
     int iter, status, done, solve_ok;
-    int accepted;
+    int accepted, cur;                      // cur: which of the two state buffers is current
 };
 
 struct Geometry {
-    int n_kf, n_free, n_lm, n_obs, n_slot, n_pb;
+    int n_kf, n_free, n_lm, n_obs, n_slot, n_pb, n_wave, n_chunk;
     Mat4 TCB[2];
     double huber_delta;
 };
 
-// --------------------------------------------------------------------------------------
-// K4a: per slot (landmark, keyframe): linearise its observations
-// --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_slot_linearize(Geometry G, const double* __restrict__ pose7,
-                                                         const double* __restrict__ pW, const int* __restrict__ slot_lm,
-                                                         const int* __restrict__ slot_kf, const int* __restrict__ slot_obs,
-                                                         const uint8_t* __restrict__ obs_cam,
-                                                         const double* __restrict__ obs_uv, const int* __restrict__ free_idx,
-                                                         double* __restrict__ sf, const LmState* __restrict__ st) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= G.n_slot || st->done) return;
-    const int l = slot_lm[s], kf = slot_kf[s];
-    const bool fr = free_idx[kf] >= 0;
-    const Pose P = pose_from7(pose7 + 7 * kf);
-    double p[3] = {pW[3 * l], pW[3 * l + 1], pW[3 * l + 2]};
+// Structure-of-arrays problem description (device pointers)
+struct Prob {
+    const int* free_idx;     // kf -> free block or -1
+    const int* slot_kf;
+    const int* slot_lm;
+    const int* slot_obs;     // n_slot + 1
+    const int* slot_first;   // first slot of the slot's landmark
+    const int* slot_nk;      // slots of the slot's landmark
+    const int* wave_slot;    // n_wave + 1
+    const uint8_t* obs_cam;
+    const double* obs_uv;
+    const int* chunk_pb;     // n_chunk: camera block of each chunk
+    const int* chunk_pair;   // n_chunk + 1: slot-pair range of each chunk
+    const int* pb_chunk;     // n_pb + 1: chunk range of each camera block
+    const int* pair_a;
+    const int* pair_b;
+    const int* pb_fa;
+    const int* pb_fb;
+};
+
+struct Work {
+    double* pose[2];         // n_kf x 7, current / trial (LmState::cur)
+    double* pw[2];           // n_lm x 3
+    const double* pose_init;
+    const double* pw_init;
+    double* slotf;           // n_slot x kSlotF
+    double* lmd;             // 12 x n_lm : V*^-1 (9), g_p (3)
+    double* partA;           // n_wave x kPartA
+    double* partD;           // n_wave x kPartD
+    double* cpart;           // n_chunk x kBlockF chunk partials
+    int* cnt;                // n_pb arrival counters
+    double* sys;             // n_pb * 36 + 12 n_free + 2
+    double* dc;              // 6 n_free
+    double* trial4;          // 4 (sharded: reduced trial scalars)
+    LmState* st;
+};
+
+__device__ __forceinline__ size_t sys_len(const Geometry& G) { return (size_t)G.n_pb * 36 + 12 * G.n_free + 2; }
+
+// ---------------------------------------------------------------------------------------
+__global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 7 * G.n_kf) {
+        Wk.pose[0][i] = Wk.pose_init[i];
+        Wk.pose[1][i] = Wk.pose_init[i];
+    }
+    if (i < 3 * G.n_lm) {
+        Wk.pw[0][i] = Wk.pw_init[i];
+        Wk.pw[1][i] = Wk.pw_init[i];
+    }
+    if (i < G.n_pb) Wk.cnt[i] = 0;
+    if (i == 0) {
+        LmState s{};
+        s.lambda = lambda0;
+        s.nu = 2.0;
+        *Wk.st = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K4: one wave per landmark group, one lane per (landmark, keyframe) slot
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr, Work Wk) {
+    __shared__ double shv[10][64];   // V (6), g_p (3), cost of each slot
+    __shared__ double shl[12][64];   // V*^-1 (9), g_p (3) at the landmark's first lane
+    __shared__ double shc[2][64];    // landmark cost, singular flag at the first lane
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    const int w = blockIdx.x, lane = threadIdx.x;
+    const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
+    const int s = s0 + lane;
+    const bool act = s < s1;
+    const int cur = st->cur;
+    const int n = G.n_slot;
     double V[6] = {0, 0, 0, 0, 0, 0}, gp[3] = {0, 0, 0}, W[18], U[21], gc[6], cost = 0.0;
 #pragma unroll
     for (int i = 0; i < 18; ++i) W[i] = 0.0;
@@ -225,258 +297,377 @@ __global__ __launch_bounds__(256) void ba_slot_linearize(Geometry G, const doubl
     for (int i = 0; i < 21; ++i) U[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) gc[i] = 0.0;
-    for (int o = slot_obs[s]; o < slot_obs[s + 1]; ++o) {
-        double r[2], J[2][9];
-        linearize(p, P, G.TCB[obs_cam[o]].m, obs_uv + 2 * o, r, J, true);
-        double sq = r[0] * r[0] + r[1] * r[1], rho, w;
-        huber(sq, G.huber_delta, &rho, &w);
-        cost += 0.5 * rho;
-        const double wr0 = w * r[0], wr1 = w * r[1];
-        int k = 0;
+    int kf = 0, first = lane, nk = 1, l = 0;
+    bool fr = false;
+    if (act) {
+        kf = Pr.slot_kf[s];
+        l = Pr.slot_lm[s];
+        first = Pr.slot_first[s] - s0;
+        nk = Pr.slot_nk[s];
+        fr = Pr.free_idx[kf] >= 0;
+        const Pose P = pose_from7(Wk.pose[cur] + 7 * kf);
+        const double* pwp = Wk.pw[cur] + 3 * l;
+        double p[3] = {pwp[0], pwp[1], pwp[2]};
+        for (int o = Pr.slot_obs[s]; o < Pr.slot_obs[s + 1]; ++o) {
+            double r[2], J[2][9];
+            linearize(p, P, G.TCB[Pr.obs_cam[o]].m, Pr.obs_uv + 2 * o, r, J, true);
+            double sq = r[0] * r[0] + r[1] * r[1], rho, wt;
+            huber(sq, G.huber_delta, &rho, &wt);
+            cost += 0.5 * rho;
+            const double wr0 = wt * r[0], wr1 = wt * r[1];
+            int k = 0;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
+            for (int a = 0; a < 3; ++a) {
 #pragma unroll
-            for (int c = a; c < 3; ++c) V[k++] += w * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
-            gp[a] += J[0][a] * wr0 + J[1][a] * wr1;
-        }
-        if (fr) {
-            int u = 0;
+                for (int c = a; c < 3; ++c) V[k++] += wt * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
+                gp[a] += J[0][a] * wr0 + J[1][a] * wr1;
+            }
+            if (fr) {
+                int u = 0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) {
+                for (int a = 0; a < 6; ++a) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) W[a * 3 + c] += w * (J[0][3 + a] * J[0][c] + J[1][3 + a] * J[1][c]);
+                    for (int c = 0; c < 3; ++c) W[a * 3 + c] += wt * (J[0][3 + a] * J[0][c] + J[1][3 + a] * J[1][c]);
 #pragma unroll
-                for (int c = a; c < 6; ++c) U[u++] += w * (J[0][3 + a] * J[0][3 + c] + J[1][3 + a] * J[1][3 + c]);
-                gc[a] += J[0][3 + a] * wr0 + J[1][3 + a] * wr1;
+                    for (int c = a; c < 6; ++c) U[u++] += wt * (J[0][3 + a] * J[0][3 + c] + J[1][3 + a] * J[1][3 + c]);
+                    gc[a] += J[0][3 + a] * wr0 + J[1][3 + a] * wr1;
+                }
             }
         }
     }
-    const int n = G.n_slot;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) sf[(F_V + i) * n + s] = V[i];
+    for (int i = 0; i < 6; ++i) shv[i][lane] = V[i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) sf[(F_GP + i) * n + s] = gp[i];
+    for (int i = 0; i < 3; ++i) shv[6 + i][lane] = gp[i];
+    shv[9][lane] = cost;
+    shc[0][lane] = 0.0;
+    shc[1][lane] = 0.0;
+    __syncthreads();
+    if (act && lane == first) {  // landmark-level sums in slot order, then the 3x3 elimination
+        double Vl[6] = {0, 0, 0, 0, 0, 0}, gl[3] = {0, 0, 0}, cl = 0.0;
+        for (int k = 0; k < nk; ++k) {
 #pragma unroll
-    for (int i = 0; i < 18; ++i) sf[(F_W + i) * n + s] = W[i];
+            for (int i = 0; i < 6; ++i) Vl[i] += shv[i][first + k];
 #pragma unroll
-    for (int i = 0; i < 21; ++i) sf[(F_U + i) * n + s] = U[i];
+            for (int i = 0; i < 3; ++i) gl[i] += shv[6 + i][first + k];
+            cl += shv[9][first + k];
+        }
+        const double lambda = st->lambda;
+        double A[3][3] = {{Vl[0] + lambda, Vl[1], Vl[2]}, {Vl[1], Vl[3] + lambda, Vl[4]}, {Vl[2], Vl[4], Vl[5] + lambda}};
+        double Vi[3][3];
+        const bool ok = inv3(A, Vi);
+        if (!ok)
 #pragma unroll
-    for (int i = 0; i < 6; ++i) sf[(F_GC + i) * n + s] = gc[i];
-    sf[F_COST * n + s] = cost;
-}
-
-// --------------------------------------------------------------------------------------
-// K4b: per landmark: V* = V + lambda I, V*^-1, Y_s = W_s V*^-1, Y_s g_p
-// --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_landmark_eliminate(Geometry G, const int* __restrict__ lm_slot,
-                                                             const int* __restrict__ slot_kf, const int* __restrict__ free_idx,
-                                                             const double* __restrict__ sf, double* __restrict__ Y,
-                                                             double* __restrict__ yg, double* __restrict__ lmd,
-                                                             LmState* __restrict__ st) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= G.n_lm || st->done) return;
-    const int n = G.n_slot;
-    const double lambda = st->lambda;
-    double V[6] = {0, 0, 0, 0, 0, 0}, gp[3] = {0, 0, 0}, cost = 0.0;
-    const int s0 = lm_slot[l], s1 = lm_slot[l + 1];
-    for (int s = s0; s < s1; ++s) {
+            for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int i = 0; i < 6; ++i) V[i] += sf[(F_V + i) * n + s];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) gp[i] += sf[(F_GP + i) * n + s];
-        cost += sf[F_COST * n + s];
-    }
-    double A[3][3] = {{V[0] + lambda, V[1], V[2]}, {V[1], V[3] + lambda, V[4]}, {V[2], V[4], V[5] + lambda}};
-    double Vi[3][3];
-    bool ok = inv3(A, Vi);
-    if (!ok)
+                for (int c = 0; c < 3; ++c) Vi[a][c] = 0.0;
+        const int m = G.n_lm;
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) Vi[a][c] = 0.0;
-    for (int s = s0; s < s1; ++s) {
-        if (free_idx[slot_kf[s]] < 0) continue;
-        double Ys[18];
+            for (int c = 0; c < 3; ++c) {
+                shl[a * 3 + c][lane] = Vi[a][c];
+                Wk.lmd[(a * 3 + c) * m + l] = Vi[a][c];
+            }
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                Ys[a * 3 + c] = (sf[(F_W + a * 3) * n + s] * Vi[0][c] + sf[(F_W + a * 3 + 1) * n + s] * Vi[1][c]) +
-                                sf[(F_W + a * 3 + 2) * n + s] * Vi[2][c];
-#pragma unroll
-        for (int i = 0; i < 18; ++i) Y[i * n + s] = Ys[i];
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-            yg[a * n + s] = (Ys[a * 3] * gp[0] + Ys[a * 3 + 1] * gp[1]) + Ys[a * 3 + 2] * gp[2];
-    }
-    const int m = G.n_lm;
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) lmd[(a * 3 + c) * m + l] = Vi[a][c];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) lmd[(9 + a) * m + l] = gp[a];
-    lmd[12 * m + l] = cost;
-    lmd[13 * m + l] = ok ? 0.0 : 1.0;
-}
-
-// fixed-order tree reduction of `nv` doubles held by every thread of a 256-thread block
-template <int NV>
-__device__ __forceinline__ void block_reduce(double (&v)[NV], double* sh) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) sh[i * 256 + tid] = v[i];
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off)
-#pragma unroll
-            for (int i = 0; i < NV; ++i) sh[i * 256 + tid] += sh[i * 256 + tid + off];
-        __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = sh[i * 256];
-    __syncthreads();
-}
-
-// --------------------------------------------------------------------------------------
-// K4c: one workgroup per upper-triangular 6x6 camera block (fa <= fb)
-//   S_ab = [a == b] (sum U_s + lambda I) - sum_pairs Y_sa W_sb^T
-//   diagonal blocks also produce g_c (sum of slot g_c) and b = -g_c + sum Y g_p;
-//   block 0 also sums the per-landmark costs.
-// out: [n_pb * 36 S blocks][n_free * 6 b][n_free * 6 g_c][cost]
-// --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_schur_blocks(Geometry G, const int* __restrict__ pb_fa,
-                                                       const int* __restrict__ pb_fb, const int* __restrict__ pair_ptr,
-                                                       const int* __restrict__ pair_a, const int* __restrict__ pair_b,
-                                                       const double* __restrict__ sf, const double* __restrict__ Y,
-                                                       const double* __restrict__ yg, const double* __restrict__ lmd,
-                                                       double* __restrict__ out, const LmState* __restrict__ st,
-                                                       int lambda_owner) {
-    __shared__ double sh[12 * 256];
-    if (st->done) return;
-    const int pb = blockIdx.x;
-    const int n = G.n_slot;
-    const int tid = threadIdx.x;
-    if (pb == G.n_pb) {  // cost block (+ count of landmarks whose V + lambda I is not invertible)
-        double c[2] = {0.0, 0.0};
-        for (int l = tid; l < G.n_lm; l += 256) {
-            c[0] += lmd[12 * G.n_lm + l];
-            c[1] += lmd[13 * G.n_lm + l];
+        for (int a = 0; a < 3; ++a) {
+            shl[9 + a][lane] = gl[a];
+            Wk.lmd[(9 + a) * m + l] = gl[a];
         }
-        block_reduce<2>(c, sh);
-        if (tid == 0) {
-            out[G.n_pb * 36 + 12 * G.n_free] = c[0];
-            out[G.n_pb * 36 + 12 * G.n_free + 1] = c[1];
+        shc[0][lane] = cl;
+        shc[1][lane] = ok ? 0.0 : 1.0;
+    }
+    __syncthreads();
+    if (act && fr) {
+        double Vi[9], g3[3];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Vi[i] = shl[i][first];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) g3[i] = shl[9 + i][first];
+        double rec[kSlotF];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            double y[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) y[c] = (W[a * 3] * Vi[c] + W[a * 3 + 1] * Vi[3 + c]) + W[a * 3 + 2] * Vi[6 + c];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                rec[SY + a * 3 + c] = y[c];
+                rec[SW + a * 3 + c] = W[a * 3 + c];
+            }
+            const double yg = (y[0] * g3[0] + y[1] * g3[1]) + y[2] * g3[2];
+            rec[SB + a] = yg - gc[a];  // b = -g_c + sum Y g_p
+            rec[SG + a] = gc[a];
+        }
+#pragma unroll
+        for (int i = 0; i < 21; ++i) rec[SU + i] = U[i];
+        rec[69] = rec[70] = rec[71] = 0.0;
+        double2* dst = reinterpret_cast<double2*>(Wk.slotf + (size_t)s * kSlotF);
+#pragma unroll
+        for (int i = 0; i < kSlotF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+    }
+    if (lane == 0) {  // wave partials in lane (= landmark) order
+        double c = 0.0, b = 0.0;
+        for (int k = 0; k < s1 - s0; ++k) {
+            c += shc[0][k];
+            b += shc[1][k];
+        }
+        Wk.partA[w * kPartA] = c;
+        Wk.partA[w * kPartA + 1] = b;
+    }
+}
+
+// Deterministic sum of n values in global memory: thread t adds elements t, t + T, t + 2T, ...
+// (independent loads, all in flight), then thread 0 adds the T per-thread sums in thread order.
+// The order is fixed by (n, T) alone, so results are run-to-run identical.  Valid in thread 0;
+// every thread of the block must call it.
+template <int T>
+__device__ double block_ordered_sum(const double* __restrict__ v, int n, int stride, double* sh) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < n; i += T) acc += v[(size_t)i * stride];
+    __syncthreads();
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < T; ++k) s += sh[k];
+    __syncthreads();
+    return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// K4c: one wave per chunk of <= 64 slot pairs of one upper-triangular 6x6 camera block
+// (fa <= fb), plus one wave for the cost.  Lane = pair:
+//   S_ab -= Y_a W_b^T   (+ U_a, b_a, g_c,a on diagonal blocks),
+// summed over the chunk's lanes in lane order (LDS), published as a chunk partial; the last
+// chunk of a block to arrive (agent-scope release/acquire + arrival counter) adds the block's
+// chunk partials in chunk order and writes the block of S (and b, g_c).  Deterministic.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, int lambda_owner) {
+    __shared__ double sh[kBlockF * 65];
+    __shared__ int last;
+    if (Wk.st->done) return;
+    const int c = blockIdx.x, lane = threadIdx.x;
+    double* sys = Wk.sys;
+    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free, SC0 = SG0 + 6 * G.n_free;
+    if (c == G.n_chunk) {  // cost + singular-landmark count
+        const double cs = block_ordered_sum<64>(Wk.partA, G.n_wave, kPartA, sh);
+        const double bd = block_ordered_sum<64>(Wk.partA + 1, G.n_wave, kPartA, sh);
+        if (lane == 0) {
+            sys[SC0] = cs;
+            sys[SC0 + 1] = bd;
         }
         return;
     }
-    const int fa = pb_fa[pb], fb = pb_fb[pb];
+    const int pb = Pr.chunk_pb[c];
+    const int fa = Pr.pb_fa[pb], fb = Pr.pb_fb[pb];
     const bool diag = fa == fb;
-    double acc[36];
+    const int p0 = Pr.chunk_pair[c], np = Pr.chunk_pair[c + 1] - p0;
+    const double* sf = Wk.slotf;
+    {
+        double acc[36], bg[12];
 #pragma unroll
-    for (int i = 0; i < 36; ++i) acc[i] = 0.0;
-    for (int p = pair_ptr[pb] + tid; p < pair_ptr[pb + 1]; p += 256) {
-        const int sa = pair_a[p], sb = pair_b[p];
-        double Ya[18], Wb[18];
+        for (int i = 0; i < 36; ++i) acc[i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < 18; ++i) {
-            Ya[i] = Y[i * n + sa];
-            Wb[i] = sf[(F_W + i) * n + sb];
-        }
+        for (int i = 0; i < 12; ++i) bg[i] = 0.0;
+        if (lane < np) {
+            const int p = p0 + lane;
+            const int sa = Pr.pair_a[p], sb = Pr.pair_b[p];
+            const double2* ra = reinterpret_cast<const double2*>(sf + (size_t)sa * kSlotF);
+            const double2* rb = reinterpret_cast<const double2*>(sf + (size_t)sb * kSlotF);
+            double Ya[18], Wb[18];
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int c = 0; c < 6; ++c)
-                acc[a * 6 + c] -= (Ya[a * 3] * Wb[c * 3] + Ya[a * 3 + 1] * Wb[c * 3 + 1]) + Ya[a * 3 + 2] * Wb[c * 3 + 2];
-        if (diag) {
-            int u = 0;
+            for (int i = 0; i < 9; ++i) {
+                const double2 y = ra[SY / 2 + i], w = rb[SW / 2 + i];
+                Ya[2 * i] = y.x; Ya[2 * i + 1] = y.y;
+                Wb[2 * i] = w.x; Wb[2 * i + 1] = w.y;
+            }
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
-                for (int c = a; c < 6; ++c) {
-                    double v = sf[(F_U + u) * n + sa];
-                    acc[a * 6 + c] += v;
-                    if (c != a) acc[c * 6 + a] += v;
-                    ++u;
+                for (int k = 0; k < 6; ++k)
+                    acc[a * 6 + k] = -((Ya[a * 3] * Wb[k * 3] + Ya[a * 3 + 1] * Wb[k * 3 + 1]) + Ya[a * 3 + 2] * Wb[k * 3 + 2]);
+            if (diag) {
+                const double* r = sf + (size_t)sa * kSlotF;
+                int u = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a)
+#pragma unroll
+                    for (int k = a; k < 6; ++k) {
+                        const double v = r[SU + u++];
+                        acc[a * 6 + k] += v;
+                        if (k != a) acc[k * 6 + a] += v;
+                    }
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    bg[a] = r[SB + a];
+                    bg[6 + a] = r[SG + a];
                 }
-        }
-    }
-    // fixed-order reduction of 36 values in three chunks of 12 (LDS = 12 * 256 doubles per pass)
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        double v[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) v[i] = acc[ch * 12 + i];
-        block_reduce<12>(v, sh);
-#pragma unroll
-        for (int i = 0; i < 12; ++i) acc[ch * 12 + i] = v[i];
-    }
-    // lambda I on the camera diagonal is added by one rank only (the blocks are summed over ranks)
-    if (tid < 36) out[pb * 36 + tid] = acc[tid] + ((diag && lambda_owner && (tid / 6 == tid % 6)) ? st->lambda : 0.0);
-    if (diag) {
-        double g[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) g[i] = 0.0;
-        for (int p = pair_ptr[pb] + tid; p < pair_ptr[pb + 1]; p += 256) {
-            const int s = pair_a[p];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                g[a] += sf[(F_GC + a) * n + s];
-                g[6 + a] += yg[a * n + s];
             }
         }
-        block_reduce<12>(g, sh);
-        if (tid < 6) {
-            out[G.n_pb * 36 + 6 * fa + tid] = -g[tid] + g[6 + tid];           // b
-            out[G.n_pb * 36 + 6 * G.n_free + 6 * fa + tid] = g[tid];          // g_c
+#pragma unroll
+        for (int i = 0; i < 36; ++i) sh[i * 65 + lane] = acc[i];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) sh[(36 + i) * 65 + lane] = bg[i];
+    }
+    __syncthreads();
+    const int nf = diag ? kBlockF : 36;
+    if (lane < nf) {
+        double s = 0.0;
+        for (int k = 0; k < np; ++k) s += sh[lane * 65 + k];
+        Wk.cpart[(size_t)c * kBlockF + lane] = s;
+    }
+    // publish the chunk partial; the last arriver of the block combines (MI355X split-K recipe)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nch = Pr.pb_chunk[pb + 1] - Pr.pb_chunk[pb];
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(Wk.cnt + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (old == nch - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Wk.cnt[pb] = 0;  // ready for the next iteration (also zeroed by ba_reset)
+    }
+    __syncthreads();
+    if (lane < nf) {
+        double s = 0.0;
+        const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
+#pragma unroll 8
+        for (int cc = c0; cc < c1; ++cc) s += Wk.cpart[(size_t)cc * kBlockF + lane];
+        if (lane < 36) {
+            if (diag && lambda_owner && lane / 6 == lane % 6) s += Wk.st->lambda;
+            sys[pb * 36 + lane] = s;
+        } else if (lane < 42) {
+            sys[SB0 + 6 * fa + (lane - 36)] = s;   // b = -g_c + sum Y g_p
+        } else {
+            sys[SG0 + 6 * fa + (lane - 42)] = s;   // g_c
         }
     }
 }
 
-// --------------------------------------------------------------------------------------
-// K5: dense camera solve (one workgroup), trial poses
-// --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_dense_solve(Geometry G, const int* __restrict__ pb_fa,
-                                                      const int* __restrict__ pb_fb, const double* __restrict__ sys,
-                                                      const double* __restrict__ pose7, const int* __restrict__ free_idx,
-                                                      double* __restrict__ pose7_trial, double* __restrict__ dc_out,
-                                                      LmState* __restrict__ st) {
-    __shared__ double A[6 * kMaxFree * 6 * kMaxFree];
-    __shared__ double x[6 * kMaxFree];
+// ---------------------------------------------------------------------------------------
+// K5: camera system solve (one workgroup of 256):
+//   S (lower triangle) and b (as row n) from sys -> LDS; blocked right-looking Cholesky of
+//   [S b; b^T .] in panels of 8 columns (panel factor by wave 0 in registers with v_readlane
+//   broadcasts, rank-8 trailing update by all 4 waves), which leaves y = L^-1 b in row n;
+//   back substitution L^T dc = y by wave 0; |dc|^2, g_c.dc; SE3 (+) trial poses.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double rl64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+constexpr int kNB = 8;  // Cholesky panel width
+
+__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
+    __shared__ double A[(kMaxN + 1) * kLdA];
+    __shared__ double dL[kMaxN];
+    __shared__ int pbf[2 * kMaxFree * (kMaxFree + 1) / 2];
     __shared__ int fail;
-    __shared__ double red[2 * 256];
+    LmState* st = Wk.st;
     if (st->done) return;
-    const int n = 6 * G.n_free;
-    const int tid = threadIdx.x;
-    if (tid == 0) fail = 0;
-    for (int pb = 0; pb < G.n_pb; ++pb) {
-        const int fa = pb_fa[pb], fb = pb_fb[pb];
-        for (int e = tid; e < 36; e += 256) {
-            const int a = e / 6, c = e % 6;
-            const double v = sys[pb * 36 + e];
-            A[(6 * fa + a) * n + 6 * fb + c] = v;
-            A[(6 * fb + c) * n + 6 * fa + a] = v;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nF = G.n_free, n = 6 * nF;
+    const double* sys = Wk.sys;
+    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * nF, SC0 = SG0 + 6 * nF;
+    for (int pb = tid; pb < G.n_pb; pb += 256) {
+        pbf[2 * pb] = Pr.pb_fa[pb];
+        pbf[2 * pb + 1] = Pr.pb_fb[pb];
+    }
+    if (tid == 0) fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
+    __syncthreads();
+    // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
+    // blocks (fa < fb, upper) are transposed into the lower triangle
+#pragma unroll 8
+    for (int e = tid; e < SB0; e += 256) {
+        const double v = sys[e];
+        const int pb = e / 36, k = e - 36 * (e / 36);
+        const int fa = pbf[2 * pb], fb = pbf[2 * pb + 1];
+        const int r = 6 * fa + k / 6, c = 6 * fb + k % 6;
+        if (fa == fb) {
+            if (r >= c) A[r * kLdA + c] = v;
+        } else {
+            A[c * kLdA + r] = v;
         }
     }
-    for (int i = tid; i < n; i += 256) x[i] = sys[G.n_pb * 36 + i];
-    if (tid == 0 && sys[G.n_pb * 36 + 12 * G.n_free + 1] != 0.0) fail = 1;  // a landmark block was singular
+    for (int i = tid; i < n; i += 256) A[n * kLdA + i] = sys[SB0 + i];  // b as row n
     __syncthreads();
-    // right-looking Cholesky, lower triangle in A
-    for (int j = 0; j < n; ++j) {
-        if (tid == 0) {
-            const double d = A[j * n + j];
-            if (!(d > 0.0) || !isfinite(d)) fail = 1;
-            A[j * n + j] = sqrt(d);
+    for (int jb = 0; jb < n && !fail; jb += kNB) {
+        const int nb = min(kNB, n - jb);
+        if (wave == 0) {
+            // rows jb + lane (q = 0) and jb + 64 + lane (q = 1), up to row n (the b row)
+            double a[2][kNB];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int r = jb + lane + 64 * q;
+#pragma unroll
+                for (int t = 0; t < kNB; ++t) a[q][t] = (r <= n && t < nb) ? A[r * kLdA + jb + t] : 0.0;
+            }
+            bool bad = false;
+#pragma unroll
+            for (int t = 0; t < kNB; ++t) {
+                if (t < nb && !bad) {
+                    const double d = rl64(a[0][t], t);  // row jb + t lives in lane t
+                    if (!(d > 0.0) || !isfinite(d)) {
+                        bad = true;
+                    } else {
+                        const double ljj = sqrt(d);
+                        if (lane == 0) dL[jb + t] = ljj;
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const int r = jb + lane + 64 * q;
+                            if (r > jb + t && r <= n) a[q][t] = a[q][t] / ljj;
+                        }
+#pragma unroll
+                        for (int t2 = t + 1; t2 < kNB; ++t2) {
+                            if (t2 < nb) {
+                                const double c = rl64(a[0][t], t2);  // L[jb + t2][jb + t]
+#pragma unroll
+                                for (int q = 0; q < 2; ++q) {
+                                    const int r = jb + lane + 64 * q;
+                                    if (r >= jb + t2 && r <= n) a[q][t2] -= a[q][t] * c;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (bad) {
+                if (lane == 0) fail = 1;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int r = jb + lane + 64 * q;
+#pragma unroll
+                    for (int t = 0; t < kNB; ++t)
+                        if (t < nb && r >= jb + t && r <= n) A[r * kLdA + jb + t] = a[q][t];
+                }
+            }
         }
         __syncthreads();
         if (fail) break;
-        const double ljj = A[j * n + j];
-        for (int i = j + 1 + tid; i < n; i += 256) A[i * n + j] /= ljj;
-        __syncthreads();
-        const int m = n - j - 1;
-        for (int e = tid; e < m * m; e += 256) {
-            const int i = j + 1 + e / m, k = j + 1 + e % m;
-            if (k <= i) A[i * n + k] -= A[i * n + j] * A[k * n + j];
+        // rank-nb trailing update: A[r][k] -= sum_t L[r][jb+t] L[k][jb+t], jb+nb <= k <= min(r, n-1)
+        const int c0 = jb + nb;
+        const int m = n - c0;  // trailing columns; rows c0 .. n (m + 1 rows incl. the b row)
+        for (int e = tid; e < (m + 1) * m; e += 256) {
+            const int r = c0 + e / m, k = c0 + e % m;
+            if (k > r) continue;
+            const double* Lr = A + r * kLdA + jb;
+            const double* Lk = A + k * kLdA + jb;
+            double s = 0.0;
+#pragma unroll
+            for (int t = 0; t < kNB; ++t)
+                if (t < nb) s += Lr[t] * Lk[t];
+            A[r * kLdA + k] -= s;
         }
         __syncthreads();
     }
@@ -488,209 +679,238 @@ __global__ __launch_bounds__(256) void ba_dense_solve(Geometry G, const int* __r
         }
         return;
     }
-    // forward L y = b (column oriented), then backward L^T x = y
-    for (int j = 0; j < n; ++j) {
-        if (tid == 0) x[j] /= A[j * n + j];
-        __syncthreads();
-        for (int i = j + 1 + tid; i < n; i += 256) x[i] -= A[i * n + j] * x[j];
-        __syncthreads();
+    if (wave != 0) return;
+    // L^T dc = y by wave 0: lane holds y_i for i = lane, lane + 64
+    double yv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = lane + 64 * q;
+        yv[q] = i < n ? A[n * kLdA + i] : 0.0;
     }
     for (int j = n - 1; j >= 0; --j) {
-        if (tid == 0) x[j] /= A[j * n + j];
-        __syncthreads();
-        for (int i = tid; i < j; i += 256) x[i] -= A[j * n + i] * x[j];
-        __syncthreads();
-    }
-    for (int i = tid; i < n; i += 256) dc_out[i] = x[i];
-    // dc^2 and g_c . dc
-    double v0 = 0.0, v1 = 0.0;
-    const double* gc = sys + G.n_pb * 36 + n;
-    for (int i = tid; i < n; i += 256) {
-        v0 += x[i] * x[i];
-        v1 += gc[i] * x[i];
-    }
-    red[tid] = v0;
-    red[256 + tid] = v1;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off) {
-            red[tid] += red[tid + off];
-            red[256 + tid] += red[256 + tid + off];
+        const int qj = j >> 6;
+        const double yj = qj == 0 ? rl64(yv[0], j & 63) : rl64(yv[1], j & 63);
+        const double xj = yj / dL[j];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = lane + 64 * q;
+            if (i < j) yv[q] -= A[j * kLdA + i] * xj;
+            else if (i == j) yv[q] = xj;
         }
-        __syncthreads();
     }
-    for (int k = tid; k < G.n_kf; k += 256) {
-        const int f = free_idx[k];
+    const int cur = st->cur;
+    double d2 = 0.0, gd = 0.0;
+    // rows 0-2 of A are no longer needed: dc, dc_i^2 and g_c,i dc_i staged for the sums below
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = lane + 64 * q;
+        if (i < n) {
+            const double x = yv[q];
+            Wk.dc[i] = x;
+            A[i] = x;
+            A[kLdA + i] = x * x;
+            A[2 * kLdA + i] = sys[SG0 + i] * x;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < G.n_kf; k += 64) {
+        const int f = Pr.free_idx[k];
+        const double* p = Wk.pose[cur] + 7 * k;
+        double* q = Wk.pose[1 - cur] + 7 * k;
         if (f < 0)
-            for (int i = 0; i < 7; ++i) pose7_trial[7 * k + i] = pose7[7 * k + i];
+            for (int i = 0; i < 7; ++i) q[i] = p[i];
         else
-            se3_plus(pose7 + 7 * k, x + 6 * f, pose7_trial + 7 * k);
+            se3_plus(p, A + 6 * f, q);
     }
-    if (tid == 0) {
+    if (lane == 0) {
+        for (int i = 0; i < n; ++i) {
+            d2 += A[kLdA + i];
+            gd += A[2 * kLdA + i];
+        }
         st->solve_ok = 1;
-        st->dc2 = red[0];
-        st->gcdc = red[256];
+        st->dc2 = d2;
+        st->gcdc = gd;
     }
 }
 
-// --------------------------------------------------------------------------------------
-// K6a: per landmark: back-substitution, trial point and trial cost
-// partials (SoA, n_lm each): new_cost, dp^2, g_p . dp, |p|^2
-// --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_backsub_cost(Geometry G, const int* __restrict__ lm_slot,
-                                                       const int* __restrict__ slot_kf, const int* __restrict__ slot_obs,
-                                                       const uint8_t* __restrict__ obs_cam,
-                                                       const double* __restrict__ obs_uv, const int* __restrict__ free_idx,
-                                                       const double* __restrict__ sf, const double* __restrict__ lmd,
-                                                       const double* __restrict__ dc, const double* __restrict__ pose7_trial,
-                                                       const double* __restrict__ pW, double* __restrict__ pW_trial,
-                                                       double* __restrict__ part, const LmState* __restrict__ st) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= G.n_lm || st->done || !st->solve_ok) return;
-    const int n = G.n_slot, m = G.n_lm;
-    double rhs[3] = {-lmd[9 * m + l], -lmd[10 * m + l], -lmd[11 * m + l]};
-    const int s0 = lm_slot[l], s1 = lm_slot[l + 1];
-    for (int s = s0; s < s1; ++s) {
-        const int f = free_idx[slot_kf[s]];
-        if (f < 0) continue;
-        const double* d6 = dc + 6 * f;
+// ---------------------------------------------------------------------------------------
+// K6: one wave per landmark group: back-substitution, trial point, trial cost
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work Wk) {
+    __shared__ double sht[3][64];     // W_s^T dc_f per slot
+    __shared__ double shp[3][64];     // trial point at the landmark's first lane
+    __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
+    const LmState* st = Wk.st;
+    if (st->done || !st->solve_ok) return;
+    const int w = blockIdx.x, lane = threadIdx.x;
+    const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
+    const int s = s0 + lane;
+    const bool act = s < s1;
+    const int cur = st->cur, n = G.n_slot, m = G.n_lm;
+    int kf = 0, first = lane, nk = 1, l = 0;
+    double t3[3] = {0.0, 0.0, 0.0};
+    if (act) {
+        kf = Pr.slot_kf[s];
+        l = Pr.slot_lm[s];
+        first = Pr.slot_first[s] - s0;
+        nk = Pr.slot_nk[s];
+        const int f = Pr.free_idx[kf];
+        if (f >= 0) {
+            const double* d6 = Wk.dc + 6 * f;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double acc = 0.0;
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0.0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) acc += sf[(F_W + a * 3 + c) * n + s] * d6[a];
-            rhs[c] -= acc;
+                for (int a = 0; a < 6; ++a) acc += Wk.slotf[(size_t)s * kSlotF + SW + a * 3 + c] * d6[a];
+                t3[c] = acc;
+            }
         }
     }
-    double dp[3], p[3], pt[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-        dp[c] = (lmd[(c * 3) * m + l] * rhs[0] + lmd[(c * 3 + 1) * m + l] * rhs[1]) + lmd[(c * 3 + 2) * m + l] * rhs[2];
-    double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
+    for (int c = 0; c < 3; ++c) sht[c][lane] = t3[c];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        p[c] = pW[3 * l + c];
-        pt[c] = p[c] + dp[c];
-        pW_trial[3 * l + c] = pt[c];
-        dp2 += dp[c] * dp[c];
-        gpdp += lmd[(9 + c) * m + l] * dp[c];
-        p2 += p[c] * p[c];
+    for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
+    __syncthreads();
+    if (act && lane == first) {
+        double rhs[3] = {-Wk.lmd[9 * m + l], -Wk.lmd[10 * m + l], -Wk.lmd[11 * m + l]};
+        for (int k = 0; k < nk; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) rhs[c] -= sht[c][first + k];
+        const double* pc = Wk.pw[cur] + 3 * l;
+        double* pt = Wk.pw[1 - cur] + 3 * l;
+        double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double dp = (Wk.lmd[(c * 3) * m + l] * rhs[0] + Wk.lmd[(c * 3 + 1) * m + l] * rhs[1]) +
+                              Wk.lmd[(c * 3 + 2) * m + l] * rhs[2];
+            const double p = pc[c];
+            const double q = p + dp;
+            shp[c][lane] = q;
+            pt[c] = q;
+            dp2 += dp * dp;
+            gpdp += Wk.lmd[(9 + c) * m + l] * dp;
+            p2 += p * p;
+        }
+        shs[1][lane] = dp2;
+        shs[2][lane] = gpdp;
+        shs[3][lane] = p2;
     }
+    __syncthreads();
     double cost = 0.0;
-    for (int s = s0; s < s1; ++s) {
-        const Pose P = pose_from7(pose7_trial + 7 * slot_kf[s]);
-        for (int o = slot_obs[s]; o < slot_obs[s + 1]; ++o) {
+    if (act) {
+        const Pose P = pose_from7(Wk.pose[1 - cur] + 7 * kf);
+        double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
+        for (int o = Pr.slot_obs[s]; o < Pr.slot_obs[s + 1]; ++o) {
             double r[2], J[2][9];
-            linearize(pt, P, G.TCB[obs_cam[o]].m, obs_uv + 2 * o, r, J, false);
-            double rho, w;
-            huber(r[0] * r[0] + r[1] * r[1], G.huber_delta, &rho, &w);
+            linearize(q, P, G.TCB[Pr.obs_cam[o]].m, Pr.obs_uv + 2 * o, r, J, false);
+            double rho, wt;
+            huber(r[0] * r[0] + r[1] * r[1], G.huber_delta, &rho, &wt);
             cost += 0.5 * rho;
         }
     }
-    part[l] = cost;
-    part[m + l] = dp2;
-    part[2 * m + l] = gpdp;
-    part[3 * m + l] = p2;
-}
-
-// K6b: fixed-order sums of the per-landmark partials (+ free pose |x|^2 on rank 0's view)
-__global__ __launch_bounds__(256) void ba_reduce_trial(Geometry G, const double* __restrict__ part,
-                                                       const double* __restrict__ pose7, const int* __restrict__ free_idx,
-                                                       double* __restrict__ out4, const LmState* __restrict__ st,
-                                                       int include_poses) {
-    __shared__ double sh[4 * 256];
-    if (st->done) return;
-    double v[4] = {0.0, 0.0, 0.0, 0.0};
-    if (st->solve_ok) {
-        for (int l = threadIdx.x; l < G.n_lm; l += 256)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] += part[i * G.n_lm + l];
-    }
-    block_reduce<4>(v, sh);
-    if (threadIdx.x == 0) {
-        double x2 = v[3];
-        if (include_poses)
-            for (int k = 0; k < G.n_kf; ++k)
-                if (free_idx[k] >= 0)
-                    for (int i = 0; i < 7; ++i) x2 += pose7[7 * k + i] * pose7[7 * k + i];
-        out4[0] = v[0];
-        out4[1] = v[1];
-        out4[2] = v[2];
-        out4[3] = x2;
+    shs[0][lane] = cost;
+    __syncthreads();
+    if (lane < kPartD) {
+        double acc = 0.0;
+        for (int k = 0; k < s1 - s0; ++k) acc += shs[lane][k];
+        Wk.partD[w * kPartD + lane] = acc;
     }
 }
 
-// K7: LM decision (single thread); accepted -> copy trial state into the current state
-__global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, LmState* __restrict__ st, const double* __restrict__ sys,
-                                                    const double* __restrict__ trial4, double* __restrict__ pose7,
-                                                    const double* __restrict__ pose7_trial, double* __restrict__ pW,
-                                                    const double* __restrict__ pW_trial, int max_iter, double cost_tol,
-                                                    double param_tol) {
-    __shared__ int accept;
-    if (st->done) return;
-    if (threadIdx.x == 0) {
-        LmState s = *st;
-        const double cost = sys[G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
-        if (s.iter == 0) s.initial_cost = cost;
-        s.cost = cost;
-        s.iter += 1;
-        accept = 0;
-        if (!isfinite(cost)) {
-            s.status = RSVIO_LM_NUMERICAL_FAILURE;
+// Trial scalars of this rank: fixed-order sums of the K6 wave partials (+ |x|^2 of the free
+// poses on the owner rank).  Valid in thread 0.  Called by all 256 threads.
+__device__ void trial_scalars(const Geometry& G, const Prob& Pr, const Work& Wk, int include_poses, double out[4],
+                              double* sh) {
+    const LmState* st = Wk.st;
+    for (int k = 0; k < kPartD; ++k)
+        out[k] = block_ordered_sum<256>(Wk.partD + k, st->solve_ok ? G.n_wave : 0, kPartD, sh);
+    if (threadIdx.x == 0 && include_poses)
+        for (int kf = 0; kf < G.n_kf; ++kf)
+            if (Pr.free_idx[kf] >= 0)
+                for (int i = 0; i < 7; ++i) out[3] += Wk.pose[st->cur][7 * kf + i] * Wk.pose[st->cur][7 * kf + i];
+}
+
+__global__ __launch_bounds__(256) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
+    __shared__ double sh[256];
+    if (Wk.st->done) return;
+    double v[4];
+    trial_scalars(G, Pr, Wk, include_poses, v, sh);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; ++k) Wk.trial4[k] = v[k];
+}
+
+// ---------------------------------------------------------------------------------------
+// K7: LM decision (build's LM).  pre_reduced: trial scalars come from trial4.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, int max_iter,
+                                                    double cost_tol, double param_tol) {
+    __shared__ double sh[256];
+    LmState* stp = Wk.st;
+    if (stp->done) return;
+    double tv[4];
+    if (pre_reduced) {
+        for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
+    } else {
+        trial_scalars(G, Pr, Wk, 1, tv, sh);
+    }
+    if (threadIdx.x != 0) return;
+    LmState s = *stp;
+    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
+    if (s.iter == 0) s.initial_cost = cost;
+    s.cost = cost;
+    s.iter += 1;
+    s.accepted = 0;
+    if (!isfinite(cost)) {
+        s.status = RSVIO_LM_NUMERICAL_FAILURE;
+        s.done = 1;
+    } else if (!s.solve_ok) {
+        s.lambda *= s.nu;
+        s.nu *= 2.0;
+        if (s.lambda > 1e32) {
+            s.status = RSVIO_LM_TRUST_REGION;
             s.done = 1;
-        } else if (!s.solve_ok) {
-            s.lambda *= s.nu;
-            s.nu *= 2.0;
-            if (s.lambda > 1e32) {
-                s.status = RSVIO_LM_TRUST_REGION;
-                s.done = 1;
-            }
+        }
+    } else {
+        s.new_cost = tv[0];
+        s.dp2 = tv[1];
+        s.gpdp = tv[2];
+        s.x2 = tv[3];
+        const double dx2 = s.dc2 + s.dp2;
+        const double dxn = sqrt(dx2), xn = sqrt(s.x2);
+        if (dxn <= param_tol * (xn + param_tol)) {
+            s.status = RSVIO_LM_PARAMETER_TOLERANCE;
+            s.done = 1;
         } else {
-            s.new_cost = trial4[0];
-            s.dp2 = trial4[1];
-            s.gpdp = trial4[2];
-            s.x2p = trial4[3];
-            const double dx2 = s.dc2 + s.dp2;
-            const double dxn = sqrt(dx2), xn = sqrt(s.x2p);
-            if (dxn <= param_tol * (xn + param_tol)) {
-                s.status = RSVIO_LM_PARAMETER_TOLERANCE;
-                s.done = 1;
+            const double pred = 0.5 * (s.lambda * dx2 - (s.gcdc + s.gpdp));
+            const double rho = (cost - s.new_cost) / pred;
+            if (isfinite(s.new_cost) && rho > 0.0) {
+                const double dcost = cost - s.new_cost;
+                s.accepted = 1;
+                s.cur = 1 - s.cur;  // the trial buffers become current
+                const double f = 2.0 * rho - 1.0;
+                s.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
+                s.nu = 2.0;
+                s.cost = s.new_cost;
+                if (dcost <= cost_tol * (s.cost + dcost)) {
+                    s.status = RSVIO_LM_COST_TOLERANCE;
+                    s.done = 1;
+                }
             } else {
-                const double pred = 0.5 * (s.lambda * dx2 - (s.gcdc + s.gpdp));
-                const double rho = (cost - s.new_cost) / pred;
-                if (isfinite(s.new_cost) && rho > 0.0) {
-                    const double dcost = cost - s.new_cost;
-                    accept = 1;
-                    const double f = 2.0 * rho - 1.0;
-                    s.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
-                    s.nu = 2.0;
-                    s.cost = s.new_cost;
-                    if (dcost <= cost_tol * (s.cost + dcost)) {
-                        s.status = RSVIO_LM_COST_TOLERANCE;
-                        s.done = 1;
-                    }
-                } else {
-                    s.lambda *= s.nu;
-                    s.nu *= 2.0;
-                    if (s.lambda > 1e32) {
-                        s.status = RSVIO_LM_TRUST_REGION;
-                        s.done = 1;
-                    }
+                s.lambda *= s.nu;
+                s.nu *= 2.0;
+                if (s.lambda > 1e32) {
+                    s.status = RSVIO_LM_TRUST_REGION;
+                    s.done = 1;
                 }
             }
         }
-        s.accepted = accept;
-        if (!s.done && s.iter >= max_iter) {
-            s.status = RSVIO_LM_MAX_ITERATIONS;
-            s.done = 1;
-        }
-        *st = s;
     }
-    __syncthreads();
-    if (accept) {
-        for (int i = threadIdx.x; i < 7 * G.n_kf; i += blockDim.x) pose7[i] = pose7_trial[i];
-        for (int i = threadIdx.x; i < 3 * G.n_lm; i += blockDim.x) pW[i] = pW_trial[i];
+    if (!s.done && s.iter >= max_iter) {
+        s.status = RSVIO_LM_MAX_ITERATIONS;
+        s.done = 1;
     }
+    *stp = s;
 }
 
 }  // namespace
@@ -702,14 +922,14 @@ struct BundleAdjuster {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Geometry G{};
     bool has_problem = false;
-    // device
-    DevBuf<double> d_pose, d_pose_init, d_pose_trial, d_pw, d_pw_init, d_pw_trial, d_uv;
+    int iter_chunk = 3;     // LM iterations enqueued between status read-backs
+    DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_uv;
     DevBuf<uint8_t> d_cam;
-    DevBuf<int> d_free, d_slot_lm, d_slot_kf, d_slot_obs, d_lm_slot, d_pb_fa, d_pb_fb, d_pair_ptr, d_pair_a, d_pair_b;
-    DevBuf<double> d_sf, d_Y, d_yg, d_lmd, d_sys, d_dc, d_part, d_trial4;
+    DevBuf<int> d_free, d_slot_kf, d_slot_lm, d_slot_obs, d_slot_first, d_slot_nk, d_wave_slot, d_chunk_pb,
+        d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb, d_cnt;
+    DevBuf<double> d_slotf, d_lmd, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
     DevBuf<LmState> d_state;
     HostBuf<LmState> h_state;
-    // multi-rank
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 
@@ -735,9 +955,34 @@ struct BundleAdjuster {
         if (b.n < n) b.alloc(std::max<size_t>(n, 1));
     }
     template <class T>
+    void up(DevBuf<T>& b, const std::vector<T>& v) {
+        grow(b, v.size());
+        if (!v.empty()) RSVIO_HIP(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+    }
+    template <class T>
     void up(DevBuf<T>& b, const T* src, size_t n) {
         grow(b, n);
         if (n) RSVIO_HIP(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, stream));
+    }
+
+    Prob prob() const {
+        Prob p;
+        p.free_idx = d_free.p; p.slot_kf = d_slot_kf.p; p.slot_lm = d_slot_lm.p; p.slot_obs = d_slot_obs.p;
+        p.slot_first = d_slot_first.p; p.slot_nk = d_slot_nk.p; p.wave_slot = d_wave_slot.p;
+        p.obs_cam = d_cam.p; p.obs_uv = d_uv.p;
+        p.chunk_pb = d_chunk_pb.p; p.chunk_pair = d_chunk_pair.p; p.pb_chunk = d_pb_chunk.p;
+        p.pair_a = d_pair_a.p; p.pair_b = d_pair_b.p; p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
+        return p;
+    }
+    Work work() const {
+        Work w;
+        w.pose[0] = d_pose2.p; w.pose[1] = d_pose2.p + 7 * (size_t)G.n_kf;
+        w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
+        w.pose_init = d_pose_init.p; w.pw_init = d_pw_init.p;
+        w.slotf = d_slotf.p; w.lmd = d_lmd.p; w.partA = d_partA.p; w.partD = d_partD.p;
+        w.cpart = d_cpart.p; w.cnt = d_cnt.p;
+        w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p; w.st = d_state.p;
+        return w;
     }
 
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
@@ -751,10 +996,11 @@ struct BundleAdjuster {
         for (int k = 0; k < n_kf; ++k)
             if (!kf_fixed[k]) free_idx[k] = n_free++;
         if (n_free > kMaxFree) throw std::invalid_argument("too many free keyframes");
+        if (n_free < 1) throw std::invalid_argument("no free keyframe");
         for (int i = 0; i < n_obs; ++i)
             if (obs_lm[i] < 0 || obs_lm[i] >= n_lm || obs_kf[i] < 0 || obs_kf[i] >= n_kf || obs_cam[i] > 1)
                 throw std::invalid_argument("observation index out of range");
-        // landmark-major CSR of observations sorted by (landmark, keyframe, camera)
+        // observations sorted by (landmark, keyframe, camera)
         std::vector<int> order(n_obs);
         std::iota(order.begin(), order.end(), 0);
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
@@ -764,23 +1010,36 @@ struct BundleAdjuster {
         });
         std::vector<double> uv(2 * (size_t)n_obs);
         std::vector<uint8_t> cam(n_obs);
-        std::vector<int> slot_lm, slot_kf, slot_obs, lm_slot(n_lm + 1, 0);
+        std::vector<int> slot_kf, slot_lm, slot_obs, lm_slot(n_lm + 1, 0);
         for (int q = 0; q < n_obs; ++q) {
             const int o = order[q];
             uv[2 * q] = obs_uv[2 * o];
             uv[2 * q + 1] = obs_uv[2 * o + 1];
             cam[q] = obs_cam[o];
             if (q == 0 || obs_lm[o] != obs_lm[order[q - 1]] || obs_kf[o] != obs_kf[order[q - 1]]) {
-                slot_lm.push_back(obs_lm[o]);
                 slot_kf.push_back(obs_kf[o]);
+                slot_lm.push_back(obs_lm[o]);
                 slot_obs.push_back(q);
                 lm_slot[obs_lm[o] + 1] += 1;
             }
         }
-        const int n_slot = (int)slot_lm.size();
+        const int n_slot = (int)slot_kf.size();
         slot_obs.push_back(n_obs);
         for (int l = 0; l < n_lm; ++l) lm_slot[l + 1] += lm_slot[l];
-        // camera blocks (fa <= fb), row-major upper triangle, and their slot pairs
+        std::vector<int> slot_first(n_slot), slot_nk(n_slot), wave_slot{0};
+        for (int l = 0; l < n_lm; ++l) {
+            const int nk = lm_slot[l + 1] - lm_slot[l];
+            if (nk > 64) throw std::invalid_argument("a landmark is observed by more than 64 keyframes");
+            for (int s = lm_slot[l]; s < lm_slot[l + 1]; ++s) {
+                slot_first[s] = lm_slot[l];
+                slot_nk[s] = nk;
+            }
+            // greedy: whole landmarks per wave, <= 64 slots
+            if (nk && lm_slot[l + 1] - wave_slot.back() > 64) wave_slot.push_back(lm_slot[l]);
+        }
+        if (n_slot > wave_slot.back()) wave_slot.push_back(n_slot);
+        const int n_wave = (int)wave_slot.size() - 1;
+        // camera blocks (fa <= fb) and their slot pairs (ascending landmark)
         std::vector<int> pb_fa, pb_fb, pb_of((size_t)n_free * n_free, -1);
         for (int a = 0; a < n_free; ++a)
             for (int b = a; b < n_free; ++b) {
@@ -800,62 +1059,59 @@ struct BundleAdjuster {
                     pairs[pb_of[fa * n_free + fb]].push_back({sa, sb});
                 }
             }
-        std::vector<int> pair_ptr(n_pb + 1, 0), pa, pbv;
+        // chunks of <= 64 pairs; a block with no pair still gets one (empty) chunk so that its
+        // entries are written
+        std::vector<int> pa, pbv, chunk_pb, chunk_pair{0}, pb_chunk{0};
         for (int b = 0; b < n_pb; ++b) {
-            pair_ptr[b + 1] = pair_ptr[b] + (int)pairs[b].size();
+            const int np = (int)pairs[b].size();
+            for (int c0 = 0; c0 < std::max(np, 1); c0 += 64) {
+                chunk_pb.push_back(b);
+                chunk_pair.push_back(chunk_pair.back() + std::min(64, np - c0));
+            }
+            pb_chunk.push_back((int)chunk_pb.size());
             for (auto& pr : pairs[b]) {
                 pa.push_back(pr.first);
                 pbv.push_back(pr.second);
             }
         }
-        G.n_kf = n_kf;
-        G.n_free = n_free;
-        G.n_lm = n_lm;
-        G.n_obs = n_obs;
-        G.n_slot = n_slot;
-        G.n_pb = n_pb;
+        G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = n_slot;
+        G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = (int)chunk_pb.size();
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
         up(d_pose_init, pose7, 7 * (size_t)n_kf);
         up(d_pw_init, pW, 3 * (size_t)n_lm);
-        grow(d_pose, 7 * (size_t)n_kf);
-        grow(d_pose_trial, 7 * (size_t)n_kf);
-        grow(d_pw, 3 * (size_t)n_lm);
-        grow(d_pw_trial, 3 * (size_t)n_lm);
-        up(d_uv, uv.data(), uv.size());
-        up(d_cam, cam.data(), cam.size());
-        up(d_free, free_idx.data(), free_idx.size());
-        up(d_slot_lm, slot_lm.data(), slot_lm.size());
-        up(d_slot_kf, slot_kf.data(), slot_kf.size());
-        up(d_slot_obs, slot_obs.data(), slot_obs.size());
-        up(d_lm_slot, lm_slot.data(), lm_slot.size());
-        up(d_pb_fa, pb_fa.data(), pb_fa.size());
-        up(d_pb_fb, pb_fb.data(), pb_fb.size());
-        up(d_pair_ptr, pair_ptr.data(), pair_ptr.size());
-        up(d_pair_a, pa.data(), pa.size());
-        up(d_pair_b, pbv.data(), pbv.size());
-        grow(d_sf, (size_t)kSlotFields * n_slot);
-        grow(d_Y, (size_t)18 * n_slot);
-        grow(d_yg, (size_t)6 * n_slot);
-        grow(d_lmd, (size_t)14 * n_lm);
+        grow(d_pose2, 14 * (size_t)n_kf);
+        grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
+        up(d_uv, uv);
+        up(d_cam, cam);
+        up(d_free, free_idx);
+        up(d_slot_kf, slot_kf);
+        up(d_slot_lm, slot_lm);
+        up(d_slot_obs, slot_obs);
+        up(d_slot_first, slot_first);
+        up(d_slot_nk, slot_nk);
+        up(d_wave_slot, wave_slot);
+        up(d_chunk_pb, chunk_pb);
+        up(d_chunk_pair, chunk_pair);
+        up(d_pb_chunk, pb_chunk);
+        grow(d_cnt, n_pb);
+        grow(d_cpart, (size_t)kBlockF * G.n_chunk);
+        up(d_pair_a, pa);
+        up(d_pair_b, pbv);
+        up(d_pb_fa, pb_fa);
+        up(d_pb_fb, pb_fb);
+        grow(d_slotf, (size_t)kSlotF * std::max(n_slot, 1));
+        grow(d_lmd, (size_t)12 * std::max(n_lm, 1));
+        grow(d_partA, (size_t)kPartA * std::max(n_wave, 1));
+        grow(d_partD, (size_t)kPartD * std::max(n_wave, 1));
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
         grow(d_dc, (size_t)6 * n_free);
-        grow(d_part, (size_t)4 * n_lm);
         grow(d_trial4, 4);
         grow(d_state, 1);
+        enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
+        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
         has_problem = true;
-    }
-
-    void reset_state(double lambda0) {
-        RSVIO_HIP(hipMemcpyAsync(d_pose.p, d_pose_init.p, sizeof(double) * 7 * G.n_kf, hipMemcpyDeviceToDevice, stream));
-        if (G.n_lm)
-            RSVIO_HIP(hipMemcpyAsync(d_pw.p, d_pw_init.p, sizeof(double) * 3 * G.n_lm, hipMemcpyDeviceToDevice, stream));
-        LmState s{};
-        s.lambda = lambda0;
-        s.nu = 2.0;
-        *h_state.p = s;
-        RSVIO_HIP(hipMemcpyAsync(d_state.p, h_state.p, sizeof(LmState), hipMemcpyHostToDevice, stream));
     }
 
     void allreduce(double* buf, size_t n) {
@@ -864,38 +1120,34 @@ struct BundleAdjuster {
             throw std::runtime_error("RCCL all-reduce failed");
     }
 
-    void enqueue_linear_system() {
-        const int B = 256;
-        if (G.n_slot)
-            hipLaunchKernelGGL(ba_slot_linearize, dim3((G.n_slot + B - 1) / B), dim3(B), 0, stream, G, d_pose.p, d_pw.p,
-                               d_slot_lm.p, d_slot_kf.p, d_slot_obs.p, d_cam.p, d_uv.p, d_free.p, d_sf.p, d_state.p);
-        if (G.n_lm)
-            hipLaunchKernelGGL(ba_landmark_eliminate, dim3((G.n_lm + B - 1) / B), dim3(B), 0, stream, G, d_lm_slot.p,
-                               d_slot_kf.p, d_free.p, d_sf.p, d_Y.p, d_yg.p, d_lmd.p, d_state.p);
-        hipLaunchKernelGGL(ba_schur_blocks, dim3(G.n_pb + 1), dim3(256), 0, stream, G, d_pb_fa.p, d_pb_fb.p,
-                           d_pair_ptr.p, d_pair_a.p, d_pair_b.p, d_sf.p, d_Y.p, d_yg.p, d_lmd.p, d_sys.p, d_state.p,
-                           rank == 0 ? 1 : 0);
+    void enqueue_reset(double lambda0) {
+        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb);
+        hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work(), lambda0);
         RSVIO_HIP(hipGetLastError());
-        // S, b, g_c and the cost are sums over landmarks: sum the per-rank partials
+    }
+
+    // K4 + K4c: this rank's reduced camera system in d_sys, summed over ranks when sharded
+    void enqueue_linear_system() {
+        const Prob pr = prob();
+        const Work wk = work();
+        if (G.n_wave) hipLaunchKernelGGL(ba_linearize_eliminate, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
+        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+        RSVIO_HIP(hipGetLastError());
         allreduce(d_sys.p, (size_t)36 * G.n_pb + 12 * G.n_free + 2);
     }
 
     void enqueue_iteration(const rsvio_lm_cfg& cfg) {
-        const int B = 256;
+        const Prob pr = prob();
+        const Work wk = work();
         enqueue_linear_system();
-        hipLaunchKernelGGL(ba_dense_solve, dim3(1), dim3(256), 0, stream, G, d_pb_fa.p, d_pb_fb.p, d_sys.p, d_pose.p,
-                           d_free.p, d_pose_trial.p, d_dc.p, d_state.p);
-        if (G.n_lm)
-            hipLaunchKernelGGL(ba_backsub_cost, dim3((G.n_lm + B - 1) / B), dim3(B), 0, stream, G, d_lm_slot.p,
-                               d_slot_kf.p, d_slot_obs.p, d_cam.p, d_uv.p, d_free.p, d_sf.p, d_lmd.p, d_dc.p,
-                               d_pose_trial.p, d_pw.p, d_pw_trial.p, d_part.p, d_state.p);
-        hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(256), 0, stream, G, d_part.p, d_pose.p, d_free.p, d_trial4.p,
-                           d_state.p, rank == 0 ? 1 : 0);
-        RSVIO_HIP(hipGetLastError());
-        allreduce(d_trial4.p, 4);
-        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(256), 0, stream, G, d_state.p, d_sys.p, d_trial4.p, d_pose.p,
-                           d_pose_trial.p, d_pw.p, d_pw_trial.p, cfg.max_iterations, cfg.cost_tolerance,
-                           cfg.parameter_tolerance);
+        hipLaunchKernelGGL(ba_camera_solve, dim3(1), dim3(256), 0, stream, G, pr, wk);
+        if (G.n_wave) hipLaunchKernelGGL(ba_backsub_cost, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
+        if (comm) {
+            hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(256), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+            allreduce(d_trial4.p, 4);
+        }
+        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(256), 0, stream, G, pr, wk, comm ? 1 : 0, cfg.max_iterations,
+                           cfg.cost_tolerance, cfg.parameter_tolerance);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -903,21 +1155,21 @@ struct BundleAdjuster {
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = cfg.huber_delta;
         res->iterations = 0;
-        // sliding_window.rs:303-319: too few residuals / underconstrained -> skip (Ok(false))
-        if (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm) {
-            if (!comm) {
-                res->status = RSVIO_LM_SKIPPED;
-                res->initial_cost = res->final_cost = 0.0;
-                res->solve_ms = 0.0;
-                return;
-            }
+        // sliding_window.rs:303-319: too few residuals / underconstrained -> skipped (Ok(false))
+        if (!comm && (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm)) {
+            res->status = RSVIO_LM_SKIPPED;
+            res->initial_cost = res->final_cost = 0.0;
+            res->solve_ms = 0.0;
+            return;
         }
-        // with sharding every rank adds lambda/nranks to its diagonal so the sum carries lambda once
-        reset_state(cfg.lambda_init);
         RSVIO_HIP(hipEventRecord(ev0, stream));
+        enqueue_reset(cfg.lambda_init);
         const int max_it = std::max(cfg.max_iterations, 1);
-        for (int it = 0; it < max_it; ++it) {
-            enqueue_iteration(cfg);
+        int enq = 0;
+        while (enq < max_it) {
+            const int k = std::min(iter_chunk, max_it - enq);
+            for (int i = 0; i < k; ++i) enqueue_iteration(cfg);
+            enq += k;
             RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
             RSVIO_HIP(hipStreamSynchronize(stream));
             if (h_state.p->done) break;
@@ -934,13 +1186,23 @@ struct BundleAdjuster {
         res->solve_ms = ms;
     }
 
+    void get_state(double* pose7, double* pW) {
+        const int cur = h_state.p->cur;
+        const Work wk = work();
+        RSVIO_HIP(hipMemcpyAsync(pose7, wk.pose[cur], sizeof(double) * 7 * G.n_kf, hipMemcpyDeviceToHost, stream));
+        if (G.n_lm)
+            RSVIO_HIP(hipMemcpyAsync(pW, wk.pw[cur], sizeof(double) * 3 * G.n_lm, hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+    }
+
     void build_system(double lambda, double huber_delta, double* S, double* b, double* cost) {
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
-        reset_state(lambda);
+        enqueue_reset(lambda);
         enqueue_linear_system();
         std::vector<double> sys((size_t)36 * G.n_pb + 12 * G.n_free + 2);
         RSVIO_HIP(hipMemcpyAsync(sys.data(), d_sys.p, sizeof(double) * sys.size(), hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
         const int n = 6 * G.n_free;
         std::vector<int> fa, fb;
@@ -953,7 +1215,7 @@ struct BundleAdjuster {
             for (int e = 0; e < 36; ++e) {
                 const int a = e / 6, c = e % 6;
                 S[(size_t)(6 * fa[pb] + a) * n + 6 * fb[pb] + c] = sys[pb * 36 + e];
-                S[(size_t)(6 * fb[pb] + c) * n + 6 * fa[pb] + a] = sys[pb * 36 + e];
+                if (fa[pb] != fb[pb]) S[(size_t)(6 * fb[pb] + c) * n + 6 * fa[pb] + a] = sys[pb * 36 + e];
             }
         for (int i = 0; i < n; ++i) b[i] = sys[36 * G.n_pb + i];
         *cost = sys[36 * G.n_pb + 12 * G.n_free];
@@ -1018,11 +1280,7 @@ int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res) {
 int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W) {
     if (!ba || !pose7 || (!p_W && ba->b.G.n_lm)) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
-        auto& B = ba->b;
-        RSVIO_HIP(hipMemcpyAsync(pose7, B.d_pose.p, sizeof(double) * 7 * B.G.n_kf, hipMemcpyDeviceToHost, B.stream));
-        if (B.G.n_lm)
-            RSVIO_HIP(hipMemcpyAsync(p_W, B.d_pw.p, sizeof(double) * 3 * B.G.n_lm, hipMemcpyDeviceToHost, B.stream));
-        RSVIO_HIP(hipStreamSynchronize(B.stream));
+        ba->b.get_state(pose7, p_W);
         return (int)RSVIO_OK;
     });
 }
@@ -1037,12 +1295,7 @@ int rsvio_ba_solve(rsvio_ba* ba, int32_t n_kf, double* pose7, const uint8_t* kf_
         auto& B = ba->b;
         B.set_problem(n_kf, pose7, kf_fixed, n_lm, p_W, n_obs, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2);
         B.run(*cfg, res);
-        if (res->status > 0) {  // success: hand back the optimised state (sliding_window.rs:364-374)
-            RSVIO_HIP(hipMemcpyAsync(pose7, B.d_pose.p, sizeof(double) * 7 * n_kf, hipMemcpyDeviceToHost, B.stream));
-            if (n_lm)
-                RSVIO_HIP(hipMemcpyAsync(p_W, B.d_pw.p, sizeof(double) * 3 * n_lm, hipMemcpyDeviceToHost, B.stream));
-            RSVIO_HIP(hipStreamSynchronize(B.stream));
-        }
+        if (res->status > 0) B.get_state(pose7, p_W);  // success: hand back the optimised state (:364-374)
         return (int)RSVIO_OK;
     });
 }
