@@ -7,7 +7,8 @@
 //
 // Mapping: lane i < 52 owns pattern point i (its offset, template intensity, its column of
 // H^-1 J^T, its bilinear sample).  Everything the reference sums over the 52 points is summed
-// in the reference's order -- a sequential chain over lanes 0..51 through v_readlane -- so
+// in the reference's order -- sequential add chains over lanes 0..51, staged through LDS and
+// read back by broadcast ds_read_b128, several independent chains interleaved -- so
 // the result is bit-identical to the scalar Rust/oracle arithmetic (no FMA contraction,
 // correctly rounded f32 divide/sqrt).  The only deviation: sin/cos of the SE(2) increment
 // are evaluated in f64 and rounded to f32 (glibc sinf differs from that on < 1e-4 of the
@@ -29,22 +30,36 @@ __constant__ int8_t kPattern[64][2] = {
     {-3, -3}, {-1, -3}, {1, -3},  {3, -3},  {5, -3},  {7, -3},  {-5, -5}, {-3, -5}, {-1, -5},
     {1, -5},  {3, -5},  {5, -5},  {-3, -7}, {-1, -7}, {1, -7},  {3, -7}};
 
-__device__ __forceinline__ float rl(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-// acc = 0; acc += v_k, k = 0..51 (Rust `sum += x` loops)
-__device__ __forceinline__ float chain_from_zero(float v) {
-    float acc = 0.0f;
+// N independent sequential f32 sums over lanes 0..51, in lane order (the reference's loop order):
+// every lane stages its N values in LDS, then every lane reads them back with broadcast
+// ds_read_b128 and runs the N dependent add chains interleaved.  FROM_ZERO: acc = 0; acc += v_k
+// (Rust `sum += x` loops); otherwise acc = v_0; acc = v_k + acc (nalgebra gemv / gemm column
+// accumulation).  All lanes end with the same sums.  sh: N * 64 floats of this wave's LDS.
+template <int N, bool FROM_ZERO>
+__device__ __forceinline__ void lane_chains(const float (&v)[N], float (&out)[N], float* sh, int lane) {
 #pragma unroll
-    for (int k = 0; k < NP; ++k) acc = acc + rl(v, k);
-    return acc;
-}
-// acc = v_0; acc = v_k + acc, k = 1..51 (nalgebra gemv / gemm column accumulation)
-__device__ __forceinline__ float chain_first(float v) {
-    float acc = rl(v, 0);
+    for (int i = 0; i < N; ++i) sh[i * 64 + lane] = v[i];
+    __builtin_amdgcn_wave_barrier();
+    float acc[N];
 #pragma unroll
-    for (int k = 1; k < NP; ++k) acc = rl(v, k) + acc;
-    return acc;
+    for (int i = 0; i < N; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const float4 x = reinterpret_cast<const float4*>(sh + i * 64)[q];
+            if (!FROM_ZERO && q == 0)
+                acc[i] = x.x;
+            else
+                acc[i] = acc[i] + x.x;
+            acc[i] = acc[i] + x.y;
+            acc[i] = acc[i] + x.z;
+            acc[i] = acc[i] + x.w;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = acc[i];
 }
 
 __device__ __forceinline__ uint32_t sat_u32(float v) {
@@ -105,9 +120,26 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
 }
 
 // image_utilities.rs:82-106, twist [vx, vy, theta]
+// sin / cos of an f32 angle evaluated in f64 and rounded once to f32.  The tracker's increments
+// are tiny, so |theta| < 1/16 takes a Taylor path (truncation < 1e-19 relative, i.e. the f64
+// value is within a few f64 ulp of the true one, as OCML's sin/cos are); larger angles use OCML.
+__device__ __forceinline__ void sincos_f64_rounded(float theta, float* s, float* c) {
+    const double t = (double)theta;
+    if (fabs(t) < 0.0625) {
+        const double t2 = t * t;
+        const double sp = -1.0 / 6.0 + t2 * (1.0 / 120.0 + t2 * (-1.0 / 5040.0 + t2 * (1.0 / 362880.0)));
+        const double cp = -0.5 + t2 * (1.0 / 24.0 + t2 * (-1.0 / 720.0 + t2 * (1.0 / 40320.0 + t2 * (-1.0 / 3628800.0))));
+        *s = (float)(t + t * (t2 * sp));
+        *c = (float)(1.0 + t2 * cp);
+    } else {
+        *s = (float)sin(t);
+        *c = (float)cos(t);
+    }
+}
+
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
-    float s = (float)sin((double)theta);
-    float c = (float)cos((double)theta);
+    float s, c;
+    sincos_f64_rounded(theta, &s, &c);
     float sin_by, omc_by;
     if (fabsf(theta) < __FLT_EPSILON__) {
         float th2 = theta * theta;
@@ -173,7 +205,7 @@ struct Template {
 
 // Pattern52::new (patch.rs:124-162) + set_data_jac_se2 (:75-123)
 __device__ bool make_template(const LevelImg& im, float posx, float posy, int lane, float patx,
-                              float paty, Template& T) {
+                              float paty, Template& T, float* sh) {
     const bool act = lane < NP;
     const float ox = act ? (float)kPattern[lane][0] : 0.0f;
     const float oy = act ? (float)kPattern[lane][1] : 0.0f;
@@ -190,10 +222,12 @@ __device__ bool make_template(const LevelImg& im, float posx, float posy, int la
         J2 = vg[1] * jw02 + vg[2] * jw12;
     }
     float data = in ? v : -1.0f;
-    const float sum = chain_from_zero(in ? v : 0.0f);
-    const float gs0 = chain_from_zero(in ? J0 : 0.0f);
-    const float gs1 = chain_from_zero(in ? J1 : 0.0f);
-    const float gs2 = chain_from_zero(in ? J2 : 0.0f);
+    float s4[4];
+    {
+        const float x4[4] = {in ? v : 0.0f, in ? J0 : 0.0f, in ? J1 : 0.0f, in ? J2 : 0.0f};
+        lane_chains<4, true>(x4, s4, sh, lane);
+    }
+    const float sum = s4[0], gs0 = s4[1], gs1 = s4[2], gs2 = s4[3];
     const int nvalid = __popcll(__ballot(in));
     const float mean = sum / (float)nvalid;
     const float mean_inv = (float)nvalid / sum;
@@ -209,12 +243,12 @@ __device__ bool make_template(const LevelImg& im, float posx, float posy, int la
     J1 *= mean_inv;
     J2 *= mean_inv;
     float H[3][3];
-    H[0][0] = chain_first(J0 * J0);
-    H[0][1] = chain_first(J0 * J1);
-    H[0][2] = chain_first(J0 * J2);
-    H[1][1] = chain_first(J1 * J1);
-    H[1][2] = chain_first(J1 * J2);
-    H[2][2] = chain_first(J2 * J2);
+    {
+        const float x6[6] = {J0 * J0, J0 * J1, J0 * J2, J1 * J1, J1 * J2, J2 * J2};
+        float h6[6];
+        lane_chains<6, false>(x6, h6, sh, lane);
+        H[0][0] = h6[0]; H[0][1] = h6[1]; H[0][2] = h6[2]; H[1][1] = h6[3]; H[1][2] = h6[4]; H[2][2] = h6[5];
+    }
     H[1][0] = H[0][1];
     H[2][0] = H[0][2];
     H[2][1] = H[1][2];
@@ -231,7 +265,7 @@ __device__ bool make_template(const LevelImg& im, float posx, float posy, int la
 
 // track_point_at_level (feature_tracker.rs:344-395) with Pattern52::residual (patch.rs:163-232)
 __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx, float paty, int lane,
-                               Aff& A, int max_iter, float thresh) {
+                               Aff& A, int max_iter, float thresh, float* sh) {
     const bool act = lane < NP;
     const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
     for (int it = 0; it < max_iter; ++it) {
@@ -252,16 +286,25 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
             float p00 = (float)r0[0], p10 = (float)r0[1], p01 = (float)r1[0], p11 = (float)r1[1];
             v = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
         }
-        const float sum = chain_from_zero(inb ? v : 0.0f);
+        float sum;
+        {
+            const float x1[1] = {inb ? v : 0.0f};
+            float s1[1];
+            lane_chains<1, true>(x1, s1, sh, lane);
+            sum = s1[0];
+        }
         const int nv = __popcll(__ballot(inb));
         if (sum < __FLT_EPSILON__) return false;
         const bool use = inb && v >= 0.0f && T.data >= 0.0f;
         const float r = use ? ((float)nv * v / sum - T.data) : 0.0f;
         const int nres = __popcll(__ballot(use));
         if (!(nres > NP / 2)) return false;
-        const float i0 = chain_first((-T.h0) * r);
-        const float i1 = chain_first((-T.h1) * r);
-        const float i2 = chain_first((-T.h2) * r);
+        float inc[3];
+        {
+            const float x3[3] = {(-T.h0) * r, (-T.h1) * r, (-T.h2) * r};
+            lane_chains<3, false>(x3, inc, sh, lane);
+        }
+        const float i0 = inc[0], i1 = inc[1], i2 = inc[2];
         if (!(isfinite(i0) && isfinite(i1) && isfinite(i2))) return false;
         const float nrm = sqrtf(i0 * i0 + i1 * i1 + i2 * i2);
         if (nrm > 1e6f) return false;
@@ -283,7 +326,7 @@ __device__ __forceinline__ LevelImg level_of(const uint8_t* pyr, uint32_t w, uin
 // track_one_point (feature_tracker.rs:292-342)
 __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, uint32_t h, int levels,
                           const Aff& T0, int lane, float patx, float paty, int max_iter, float thresh,
-                          Aff& out) {
+                          Aff& out, float* sh) {
     Aff T1;
     T1.m00 = 1.0f; T1.m01 = 0.0f; T1.m10 = 0.0f; T1.m11 = 1.0f;
     T1.m20 = 0.0f; T1.m21 = 0.0f; T1.m22 = 1.0f;
@@ -294,9 +337,9 @@ __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, 
         T1.m02 /= sdn;
         T1.m12 /= sdn;
         Template tp;
-        if (!make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp))
+        if (!make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp, sh))
             return false;
-        if (!track_at_level(level_of(pyr1, w, h, i), tp, patx, paty, lane, T1, max_iter, thresh))
+        if (!track_at_level(level_of(pyr1, w, h, i), tp, patx, paty, lane, T1, max_iter, thresh, sh))
             return false;
         T1.m02 *= sdn;
         T1.m12 *= sdn;
@@ -316,6 +359,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
     const int idx = job - L.start[b];
     if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
+    __shared__ float sh[6 * 64];
     const int lane = threadIdx.x;
     const float patx = lane < NP ? (float)kPattern[lane][0] / 2.0f : 0.0f;
     const float paty = lane < NP ? (float)kPattern[lane][1] / 2.0f : 0.0f;
@@ -325,10 +369,10 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
     Aff fwd, bwd;
     bool ok = track_one(L.pyr0[b], L.pyr1[b], L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
-                        L.thresh, fwd);
+                        L.thresh, fwd, sh);
     if (ok)
         ok = track_one(L.pyr1[b], L.pyr0[b], L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
-                       L.thresh, bwd);
+                       L.thresh, bwd, sh);
     if (ok) {
         // feature_tracker.rs:277-281: squared translation distance < 0.4
         float dx = T0.m02 - bwd.m02, dy = T0.m12 - bwd.m12;

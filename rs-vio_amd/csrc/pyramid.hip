@@ -103,7 +103,15 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
         const float* __restrict__ vw = T.weights + (size_t)e * T.max_taps;
         const uint8_t* __restrict__ col = src + (size_t)vl * L.w + xl + c;
         float acc = 0.0f;
-        for (int k = 0; k < vc; ++k) acc += (float)col[(size_t)k * L.w] * vw[k];
+        // taps loaded 8 at a time (independent loads in flight), summed in tap order
+        for (int k = 0; k < vc; k += 8) {
+            float px[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) px[u] = (k + u < vc) ? (float)col[(size_t)(k + u) * L.w] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (k + u < vc) acc += px[u] * vw[k + u];
+        }
         tmp[r * LDS_COLS + c] = acc;
     }
     __syncthreads();
