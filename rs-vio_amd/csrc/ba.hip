@@ -37,6 +37,8 @@ namespace rsvio {
 
 namespace {
 
+RSVIO_DBG_DECL
+
 constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
 constexpr int kMaxN = 6 * kMaxFree;
 constexpr int kLdA = kMaxN + 1;         // odd stride
@@ -566,10 +568,153 @@ __device__ __forceinline__ double rl64(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-constexpr int kNB = 8;  // Cholesky panel width
+constexpr int kNB = 8;  // Cholesky panel width (blocked path, n > 60)
 
+// Fixed-pairing butterfly sum over the wave; lane 0's value is returned to every lane.
+__device__ __forceinline__ double wave_sum_det(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return rl64(v, 0);
+}
+
+// 1/sqrt(x), f64: hardware estimate + two Newton steps (full f64 precision for normal x > 0).
+__device__ __forceinline__ double rsqrt_f64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double hx = 0.5 * x;
+        y = y * (1.5 - hx * y * y);
+    }
+    return y;
+}
+
+// Column step K of the register-resident Cholesky (compile-time K: the row stays in registers).
+template <int NP, int K>
+__device__ __forceinline__ void chol_step(double (&a)[NP], int lane, double* colb, const double2* colb2, double* dL,
+                                          bool& bad, double piv) {
+    bad |= !(piv > 0.0) || !isfinite(piv);
+    const double inv = rsqrt_f64(piv);
+    dL[K] = inv;  // every lane stores the same value
+    const double lk = a[K] * inv;
+    a[K] = lk;
+    // next pivot straight from registers: on lane K+1, L[K+1][K] is its own lk, so the
+    // critical path does not wait for the LDS broadcast (bitwise the same update as below)
+    double piv_next = 0.0;
+    if constexpr (K + 1 < NP) piv_next = rl64(fma(-lk, lk, a[K + 1]), K + 1);
+    // column K broadcast back through LDS; alternating buffers let step K+1's pivot chain
+    // overlap step K's trailing update
+    constexpr int kOff = (K & 1) * 64;
+    colb[kOff + lane] = lk;
+    // trailing update of this lane's row in chunks of 32 columns (16 x 16 B broadcast reads)
+#pragma unroll
+    for (int c2 = (K + 1) / 2; c2 < NP / 2; c2 += 16) {
+        double2 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (c2 + u < NP / 2) v[u] = colb2[kOff / 2 + c2 + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int c = 2 * (c2 + u);
+            if (c2 + u < NP / 2) {
+                if (c > K) a[c] = fma(-lk, v[u].x, a[c]);
+                a[c + 1] = fma(-lk, v[u].y, a[c + 1]);
+            }
+        }
+    }
+    if constexpr (K + 1 < NP) chol_step<NP, K + 1>(a, lane, colb, colb2, dL, bad, piv_next);
+}
+
+// Register-resident Cholesky of the (n+1) x n augmented system [S; b^T] for n <= NP = 6 NF <= 60,
+// one wave: lane r owns row r (lanes n..NP-1 are identity padding, lane NP holds b), so the
+// factorisation is NP fully unrolled right-looking column steps whose column broadcasts are
+// readlanes; row NP ends as y = L^-1 b.  Back substitution L^T dc = y reads L transposed from
+// LDS.  Same result as the blocked path up to f64 rounding (tolerance parity).
+template <int NF>
+__device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* dL, int n,
+                                 int lane) {
+    constexpr int NP = 6 * NF;
+    LmState* st = Wk.st;
+    double a[NP];
+    double* colb = A + 100 * kLdA;  // 16-byte aligned (A is, 100 * kLdA is even)
+    // row image of this lane: lower triangle (c <= r) of S, identity padding, b as row NP
+    const int src = lane < n ? lane : (lane == NP ? n : -1);
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {
+        double v = 0.0;
+        if (src >= 0 && c < n && (c <= lane || lane == NP)) v = A[src * kLdA + c];
+        if (lane >= n && lane < NP && c == lane) v = 1.0;
+        a[c] = v;
+    }
+    bool bad = false;
+    // opaque zero offset: one LDS base register + immediate offsets for every broadcast read
+    int zero = 0;
+    __asm__ volatile("" : "+s"(zero));
+    chol_step<NP, 0>(a, lane, colb + 2 * zero, reinterpret_cast<const double2*>(colb + 2 * zero), dL, bad,
+                      rl64(a[0], 0));
+    if (bad) {
+        if (lane == 0) {
+            st->solve_ok = 0;
+            st->dc2 = 0.0;
+            st->gcdc = 0.0;
+        }
+        return;
+    }
+    STAMP(7);
+    // L (lower) and y (row NP) back to LDS, rows r <= NP
+#pragma unroll
+    for (int c = 0; c < NP; ++c)
+        if (lane <= NP) A[lane * kLdA + c] = a[c];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    // lane i gathers column i of L (row j, column i = L^T[i][j]) up front, then the solve is
+    // branch-free: x_j = y_j / L_jj broadcast by readlane, y_i -= L_ji x_j for i < j
+    const int li = lane < NP ? lane : 0;
+    double yv = A[NP * kLdA + li];
+    double lt[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) lt[j] = A[j * kLdA + li];
+#pragma unroll
+    for (int j = NP - 1; j >= 0; --j) {
+        const double xj = rl64(yv, j) * dL[j];
+        const double upd = fma(-lt[j], xj, yv);
+        yv = lane < j ? upd : (lane == j ? xj : yv);
+    }
+    STAMP(3);
+    const double* sys = Wk.sys;
+    const int SG0 = G.n_pb * 36 + 6 * G.n_free;
+    const double x = lane < n ? yv : 0.0;
+    const double d2 = wave_sum_det(x * x);
+    const double gd = wave_sum_det(lane < n ? sys[SG0 + lane] * x : 0.0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n) {
+        Wk.dc[lane] = x;
+        A[lane] = x;  // row 0 of A reused as dc for the pose updates
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    STAMP(4);
+    const int cur = st->cur;
+    for (int k = lane; k < G.n_kf; k += 64) {
+        const int f = Pr.free_idx[k];
+        const double* p = Wk.pose[cur] + 7 * k;
+        double* q = Wk.pose[1 - cur] + 7 * k;
+        if (f < 0)
+            for (int i = 0; i < 7; ++i) q[i] = p[i];
+        else
+            se3_plus(p, A + 6 * f, q);
+    }
+    STAMP(5);
+    if (lane == 0) {
+        st->solve_ok = 1;
+        st->dc2 = d2;
+        st->gcdc = gd;
+    }
+    STAMP(6);
+}
+
+template <int NF>
 __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
-    __shared__ double A[(kMaxN + 1) * kLdA];
+    __shared__ __attribute__((aligned(16))) double A[(kMaxN + 1) * kLdA];
     __shared__ double dL[kMaxN];
     __shared__ int pbf[2 * kMaxFree * (kMaxFree + 1) / 2];
     __shared__ int fail;
@@ -583,6 +728,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         pbf[2 * pb] = Pr.pb_fa[pb];
         pbf[2 * pb + 1] = Pr.pb_fb[pb];
     }
+    STAMP(0);
     if (tid == 0) fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
     __syncthreads();
     // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
@@ -601,6 +747,20 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     }
     for (int i = tid; i < n; i += 256) A[n * kLdA + i] = sys[SB0 + i];  // b as row n
     __syncthreads();
+    STAMP(1);
+    if constexpr (NF > 0) {
+        if (wave != 0 || fail) {
+            if (tid == 0 && fail) {
+                st->solve_ok = 0;
+                st->dc2 = 0.0;
+                st->gcdc = 0.0;
+            }
+            return;
+        }
+        STAMP(2);
+        camera_solve_reg<NF>(G, Pr, Wk, A, dL, n, lane);
+        return;
+    } else {
     for (int jb = 0; jb < n && !fail; jb += kNB) {
         const int nb = min(kNB, n - jb);
         if (wave == 0) {
@@ -679,6 +839,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         }
         return;
     }
+    STAMP(2);
     if (wave != 0) return;
     // L^T dc = y by wave 0: lane holds y_i for i = lane, lane + 64
     double yv[2];
@@ -698,6 +859,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             else if (i == j) yv[q] = xj;
         }
     }
+    STAMP(3);
     const int cur = st->cur;
     double d2 = 0.0, gd = 0.0;
     // rows 0-2 of A are no longer needed: dc, dc_i^2 and g_c,i dc_i staged for the sums below
@@ -714,6 +876,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
+    STAMP(4);
     for (int k = lane; k < G.n_kf; k += 64) {
         const int f = Pr.free_idx[k];
         const double* p = Wk.pose[cur] + 7 * k;
@@ -723,6 +886,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         else
             se3_plus(p, A + 6 * f, q);
     }
+    STAMP(5);
     if (lane == 0) {
         for (int i = 0; i < n; ++i) {
             d2 += A[kLdA + i];
@@ -732,6 +896,8 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         st->dc2 = d2;
         st->gcdc = gd;
     }
+    STAMP(6);
+    }  // blocked path
 }
 
 // ---------------------------------------------------------------------------------------
@@ -818,17 +984,35 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
     }
 }
 
-// Trial scalars of this rank: fixed-order sums of the K6 wave partials (+ |x|^2 of the free
-// poses on the owner rank).  Valid in thread 0.  Called by all 256 threads.
+// Trial scalars of this rank: the K6 wave partials (+ |x|^2 of the free poses on the owner
+// rank) summed in a fixed order: per-thread strided sums, a fixed-pairing butterfly inside
+// each wave, then the 4 wave sums in wave order.  Valid in thread 0.  Called by all 256 threads.
 __device__ void trial_scalars(const Geometry& G, const Prob& Pr, const Work& Wk, int include_poses, double out[4],
                               double* sh) {
     const LmState* st = Wk.st;
-    for (int k = 0; k < kPartD; ++k)
-        out[k] = block_ordered_sum<256>(Wk.partD + k, st->solve_ok ? G.n_wave : 0, kPartD, sh);
-    if (threadIdx.x == 0 && include_poses)
-        for (int kf = 0; kf < G.n_kf; ++kf)
-            if (Pr.free_idx[kf] >= 0)
-                for (int i = 0; i < 7; ++i) out[3] += Wk.pose[st->cur][7 * kf + i] * Wk.pose[st->cur][7 * kf + i];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nw = st->solve_ok ? G.n_wave : 0;
+    double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < nw; i += 256) {
+        const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
+        acc[0] += v.x;
+        acc[1] += v.y;
+        acc[2] += v.z;
+        acc[3] += v.w;
+    }
+    if (include_poses) {
+        const double* p = Wk.pose[st->cur];
+        for (int e = tid; e < 7 * G.n_kf; e += 256)
+            if (Pr.free_idx[e / 7] >= 0) acc[3] += p[e] * p[e];
+    }
+#pragma unroll
+    for (int k = 0; k < kPartD; ++k) {
+        const double w = wave_sum_det(acc[k]);
+        if (lane == 0) sh[wave * kPartD + k] = w;
+    }
+    __syncthreads();
+    if (tid == 0)
+        for (int k = 0; k < kPartD; ++k) out[k] = ((sh[k] + sh[kPartD + k]) + sh[2 * kPartD + k]) + sh[3 * kPartD + k];
 }
 
 __global__ __launch_bounds__(256) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
@@ -849,11 +1033,13 @@ __global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk
     LmState* stp = Wk.st;
     if (stp->done) return;
     double tv[4];
+    STAMP(8);
     if (pre_reduced) {
         for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
     } else {
         trial_scalars(G, Pr, Wk, 1, tv, sh);
     }
+    STAMP(9);
     if (threadIdx.x != 0) return;
     LmState s = *stp;
     const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
@@ -911,9 +1097,12 @@ __global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk
         s.done = 1;
     }
     *stp = s;
+    STAMP(10);
 }
 
 }  // namespace
+
+RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 
 // ======================================================================================
 struct BundleAdjuster {
@@ -1136,11 +1325,24 @@ struct BundleAdjuster {
         allreduce(d_sys.p, (size_t)36 * G.n_pb + 12 * G.n_free + 2);
     }
 
+    // register-resident factorisation for n_free <= 10 (padded to an even count), blocked otherwise
+    void launch_camera_solve(const Prob& pr, const Work& wk) {
+        const dim3 g(1), b(256);
+        switch (G.n_free <= 10 ? (G.n_free + 1) / 2 : 0) {
+            case 1: hipLaunchKernelGGL(ba_camera_solve<2>, g, b, 0, stream, G, pr, wk); break;
+            case 2: hipLaunchKernelGGL(ba_camera_solve<4>, g, b, 0, stream, G, pr, wk); break;
+            case 3: hipLaunchKernelGGL(ba_camera_solve<6>, g, b, 0, stream, G, pr, wk); break;
+            case 4: hipLaunchKernelGGL(ba_camera_solve<8>, g, b, 0, stream, G, pr, wk); break;
+            case 5: hipLaunchKernelGGL(ba_camera_solve<10>, g, b, 0, stream, G, pr, wk); break;
+            default: hipLaunchKernelGGL(ba_camera_solve<0>, g, b, 0, stream, G, pr, wk); break;
+        }
+    }
+
     void enqueue_iteration(const rsvio_lm_cfg& cfg) {
         const Prob pr = prob();
         const Work wk = work();
         enqueue_linear_system();
-        hipLaunchKernelGGL(ba_camera_solve, dim3(1), dim3(256), 0, stream, G, pr, wk);
+        launch_camera_solve(pr, wk);
         if (G.n_wave) hipLaunchKernelGGL(ba_backsub_cost, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
         if (comm) {
             hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(256), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);

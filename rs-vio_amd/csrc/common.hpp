@@ -42,6 +42,31 @@ int guarded(F&& f) {
     }
 }
 
+// Diagnostic phase stamps (make stamps -> lib/librsvio_gpu_stamps.so, tools/*_probe.py only):
+// thread 0 of block b writes the shader clock into slot k of row b after draining its
+// outstanding memory operations.  Compiled out of the product library.
+#ifdef RSVIO_STAMPS
+#define RSVIO_DBG_DECL static __device__ unsigned long long g_dbg[4096 * 16];
+#define STAMP(k)                                                              \
+    do {                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {                          \
+            __builtin_amdgcn_s_waitcnt(0);                                    \
+            g_dbg[blockIdx.x * 16 + (k)] = (unsigned long long)clock64();     \
+        }                                                                     \
+    } while (0)
+#define RSVIO_DBG_READER(name)                                                             \
+    extern "C" int name(unsigned long long* out, int n) {                                  \
+        if (n > 4096 * 16) n = 4096 * 16;                                                  \
+        return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(unsigned long long) * n); \
+    }
+#else
+#define RSVIO_DBG_DECL
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#define RSVIO_DBG_READER(name)
+#endif
+
 // Pyramid level geometry: level i = (w / 2^i) x (h / 2^i), packed back to back
 // (feature_tracker.rs:215-216).
 __host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }

@@ -19,6 +19,8 @@ namespace rsvio {
 
 namespace {
 
+RSVIO_DBG_DECL
+
 constexpr int NP = 52;
 
 // patch.rs:19-72 -- the 52-point pattern (pixel offsets before the 1/2 scale of :126)
@@ -269,6 +271,9 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
     const bool act = lane < NP;
     const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
     for (int it = 0; it < max_iter; ++it) {
+#ifdef RSVIO_STAMPS
+        if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 16 + 15] += 1;
+#endif
         float x = A.m00 * patx;
         x = A.m01 * paty + x;
         float y = A.m10 * patx;
@@ -368,11 +373,17 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     T0.m00 = a[0]; T0.m01 = a[1]; T0.m10 = a[2]; T0.m11 = a[3]; T0.m02 = a[4]; T0.m12 = a[5];
     T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
     Aff fwd, bwd;
+#ifdef RSVIO_STAMPS
+    if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 16 + 15] = 0;
+#endif
+    STAMP(0);
     bool ok = track_one(L.pyr0[b], L.pyr1[b], L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
                         L.thresh, fwd, sh);
+    STAMP(1);
     if (ok)
         ok = track_one(L.pyr1[b], L.pyr0[b], L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
                        L.thresh, bwd, sh);
+    STAMP(2);
     if (ok) {
         // feature_tracker.rs:277-281: squared translation distance < 0.4
         float dx = T0.m02 - bwd.m02, dy = T0.m12 - bwd.m12;
@@ -390,6 +401,8 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
 }
 
 }  // namespace
+
+RSVIO_DBG_READER(rsvio_dbg_lk_stamps)
 
 void enqueue_track(const TrackLaunch& L, hipStream_t s) {
     const int total = L.start[L.nb];

@@ -1,0 +1,30 @@
+"""Phase-stamp probe for the BA kernels (diagnostic build lib/librsvio_gpu_stamps.so).
+Prints shader-clock cycles between STAMP points of block 0 of the last launch."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+os.environ["RSVIO_LIB"] = str(ROOT / "rs-vio_amd" / "lib" / "librsvio_gpu_stamps.so")
+sys.path[:0] = [str(ROOT), str(ROOT / "rs-vio_amd")]
+
+import numpy as np  # noqa: E402
+
+from rsvio import _lib  # noqa: E402
+from rsvio import synthetic as S  # noqa: E402
+from rsvio.ba import BundleAdjuster  # noqa: E402
+
+lib = _lib.load()
+prob = S.ba_problem(n_kf=10, n_lm=2000, kf_per_lm=6, seed=7)
+ba = BundleAdjuster(max_keyframes=10, max_landmarks=2000, max_observations=prob.n_obs)
+for rep in range(5):
+    ba.set_problem_from(prob)
+    r = ba.run()
+print("status", r.status, "iters", r.iterations, "solve_ms", r.solve_ms)
+buf = (C.c_ulonglong * 64)()
+lib.rsvio_dbg_ba_stamps(buf, 64)
+st = np.array(buf[:16], dtype=np.int64)
+print("camera_solve phases (cycles):", np.diff(st[:7]).tolist(), "total", st[6] - st[0])
+print("  register path: factor %d, back substitution %d" % (st[7] - st[2], st[3] - st[7]))
+print("lm_decide phases (cycles):", np.diff(st[8:11]).tolist())

@@ -1,0 +1,63 @@
+"""Phase-stamp probe for lk_track_kernel (diagnostic build lib/librsvio_gpu_stamps.so): per
+feature forward/backward cycles and LK iteration counts, plus a least-squares split into
+cycles per template and cycles per iteration."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+os.environ["RSVIO_LIB"] = str(ROOT / "rs-vio_amd" / "lib" / "librsvio_gpu_stamps.so")
+sys.path[:0] = [str(ROOT), str(ROOT / "rs-vio_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rsvio import _lib  # noqa: E402
+from rsvio import synthetic as S  # noqa: E402
+
+W, H = 752, 480
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+N = 300
+lib = _lib.load()
+frames = list(S.stereo_sequence(2, W, H))
+aff = S.track_features(frames[0][0], N)
+dev = torch.device("cuda", 0)
+imgs = torch.from_numpy(np.stack([frames[0][0], frames[1][0]])).to(dev)
+pb = int(lib.rsvio_pyramid_bytes(W, H, L))
+pyr = torch.empty((2, pb), dtype=torch.uint8, device=dev)
+ctx = C.c_void_p()
+_lib.check(lib.rsvio_track_ctx_create(W, H, L, 0, C.byref(ctx)))
+s = torch.cuda.current_stream()
+lib.rsvio_build_pyramids_d(ctx, imgs.data_ptr(), 2, pyr.data_ptr(), s.cuda_stream)
+a_dev = torch.from_numpy(aff).to(dev)
+out = torch.empty_like(a_dev)
+val = torch.empty(N, dtype=torch.uint8, device=dev)
+b = (_lib.TrackBatch * 1)()
+b[0] = _lib.TrackBatch(pyr[0].data_ptr(), pyr[1].data_ptr(), a_dev.data_ptr(), out.data_ptr(), val.data_ptr(), N)
+for _ in range(3):
+    lib.rsvio_track_points_d(ctx, b, 1, 20, C.c_float(0.01), s.cuda_stream)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(s)
+lib.rsvio_track_points_d(ctx, b, 1, 20, C.c_float(0.01), s.cuda_stream)
+e1.record(s)
+torch.cuda.synchronize()
+buf = (C.c_ulonglong * (N * 16))()
+lib.rsvio_dbg_lk_stamps(buf, N * 16)
+st = np.array(buf[:], dtype=np.int64).reshape(N, 16)
+fw = st[:, 1] - st[:, 0]
+bw = st[:, 2] - st[:, 1]
+it = st[:, 15]
+tot = fw + bw
+v = val.cpu().numpy()
+print(f"L={L} kernel {e0.elapsed_time(e1) * 1e3:.1f} us; valid {v.mean():.3f}")
+print("per-feature cycles: median %d  p90 %d  max %d; iterations median %d max %d" %
+      (np.median(tot), np.percentile(tot, 90), tot.max(), np.median(it), it.max()))
+m = v.astype(bool)
+X = np.stack([np.full(m.sum(), 2 * L, float), it[m].astype(float)], 1)
+coef, *_ = np.linalg.lstsq(X, tot[m].astype(float), rcond=None)
+print("fit (valid features): %.0f cycles/template, %.0f cycles/iteration" % (coef[0], coef[1]))
+k = np.argmax(tot)
+print("slowest feature: cycles fwd %d bwd %d iterations %d valid %d" % (fw[k], bw[k], it[k], v[k]))
+span = st[:, 2].max() - st[:, 0].min()
+print("first start -> last end: %d cycles" % span)
