@@ -14,7 +14,8 @@
 //   K4  ba_linearize_eliminate  wave / landmark group: residual + Jacobian + Huber per slot,
 //                               V, g_p summed over the landmark's lanes, (V + lambda I)^-1,
 //                               Y = W V^-1, Y g_p -- per-slot Schur factors to HBM
-//   K4c ba_schur_chunks         wave / 64 pairs: -Y_a W_b^T (+ U on the diagonal), lane-ordered sums
+//   K4c ba_schur_chunks         wave / 64 pairs: -Y_a W_b^T (+ U on the diagonal), lane-ordered chunk sums
+//   K4d ba_schur_combine        wave / camera block: chunk partials in chunk order -> S, b, g_c; cost
 //   [RCCL all-reduce of the per-rank reduced system when sharded]
 //   K5  ba_camera_solve         1 workgroup: fixed-order chunk sums -> S, b in LDS, Cholesky,
 //                               substitutions, SE3 (+) trial poses
@@ -45,7 +46,6 @@ constexpr int kLdA = kMaxN + 1;         // odd stride
 // per-slot Schur factors, one contiguous 576-B record per slot (AoS): Y, W, U (packed), b, g_c
 enum { SY = 0, SW = 18, SU = 36, SB = 57, SG = 63, kSlotF = 72 };
 constexpr int kBlockF = 48;             // 36 S + 6 b + 6 g_c per camera block workgroup
-constexpr int kShLd = 257;              // LDS row stride (doubles) of the per-thread block partials
 constexpr int kPartA = 2;               // cost, singular-landmark count per wave
 constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per wave
 
@@ -61,8 +61,8 @@ struct Pose {
 // nalgebra UnitQuaternion::to_rotation_matrix after normalisation (apex SE3::from)
 __device__ __forceinline__ Pose pose_from7(const double* p7) {
     double w = p7[3], x = p7[4], y = p7[5], z = p7[6];
-    double n = sqrt(w * w + x * x + y * y + z * z);
-    w /= n; x /= n; y /= n; z /= n;
+    const double in = 1.0 / sqrt(w * w + x * x + y * y + z * z);  // one division, 4 products
+    w *= in; x *= in; y *= in; z *= in;
     double ww = w * w, xx = x * x, yy = y * y, zz = z * z;
     double xy = x * y * 2.0, wz = w * z * 2.0, wy = w * y * 2.0;
     double xz = x * z * 2.0, yz = y * z * 2.0, wx = w * x * 2.0;
@@ -176,10 +176,16 @@ __device__ void se3_plus(const double* p7, const double* d, double* out) {
         A = 0.5 - th2 / 24.0;
         Bc = 1.0 / 6.0 - th2 / 120.0;
     } else {
-        double s = sin(0.5 * th) / th;
-        qd[0] = cos(0.5 * th); qd[1] = s * om[0]; qd[2] = s * om[1]; qd[3] = s * om[2];
-        A = (1.0 - cos(th)) / th2;
-        Bc = (th - sin(th)) / (th2 * th);
+        // one sincos of theta/2: sin(th) = 2 s c, 1 - cos(th) = 2 s^2 (same values as the
+        // oracle's libm calls to within an ulp; tolerance parity)
+        double sh, ch;
+        sincos(0.5 * th, &sh, &ch);
+        const double ith = 1.0 / th;
+        const double s = sh * ith;
+        qd[0] = ch; qd[1] = s * om[0]; qd[2] = s * om[1]; qd[3] = s * om[2];
+        const double ith2 = ith * ith;
+        A = 2.0 * sh * sh * ith2;
+        Bc = (th - 2.0 * sh * ch) * ith2 * ith;
     }
     double wx[3] = {om[1] * rho[2] - om[2] * rho[1], om[2] * rho[0] - om[0] * rho[2], om[0] * rho[1] - om[1] * rho[0]};
     double wwx[3] = {om[1] * wx[2] - om[2] * wx[1], om[2] * wx[0] - om[0] * wx[2], om[0] * wx[1] - om[1] * wx[0]};
@@ -194,8 +200,8 @@ __device__ void se3_plus(const double* p7, const double* d, double* out) {
     double w0 = p7[3], x0 = p7[4], y0 = p7[5], z0 = p7[6];
     double qn[4] = {w0 * qd[0] - x0 * qd[1] - y0 * qd[2] - z0 * qd[3], w0 * qd[1] + x0 * qd[0] + y0 * qd[3] - z0 * qd[2],
                     w0 * qd[2] - x0 * qd[3] + y0 * qd[0] + z0 * qd[1], w0 * qd[3] + x0 * qd[2] - y0 * qd[1] + z0 * qd[0]};
-    double nn = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
-    for (int i = 0; i < 4; ++i) out[3 + i] = qn[i] / nn;
+    const double inn = 1.0 / sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    for (int i = 0; i < 4; ++i) out[3 + i] = qn[i] * inn;
 }
 
 __device__ __forceinline__ int utri(int a, int c) {  // index of (min, max) in a packed 6x6 upper triangle
@@ -248,7 +254,6 @@ struct Work {
     double* partA;           // n_wave x kPartA
     double* partD;           // n_wave x kPartD
     double* cpart;           // n_chunk x kBlockF chunk partials
-    int* cnt;                // n_pb arrival counters
     double* sys;             // n_pb * 36 + 12 n_free + 2
     double* dc;              // 6 n_free
     double* trial4;          // 4 (sharded: reduced trial scalars)
@@ -268,7 +273,6 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[0][i] = Wk.pw_init[i];
         Wk.pw[1][i] = Wk.pw_init[i];
     }
-    if (i < G.n_pb) Wk.cnt[i] = 0;
     if (i == 0) {
         LmState s{};
         s.lambda = lambda0;
@@ -286,12 +290,12 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
     __shared__ double shc[2][64];    // landmark cost, singular flag at the first lane
     const LmState* st = Wk.st;
     if (st->done) return;
+    STAMP(11);
     const int w = blockIdx.x, lane = threadIdx.x;
     const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
     const int s = s0 + lane;
     const bool act = s < s1;
     const int cur = st->cur;
-    const int n = G.n_slot;
     double V[6] = {0, 0, 0, 0, 0, 0}, gp[3] = {0, 0, 0}, W[18], U[21], gc[6], cost = 0.0;
 #pragma unroll
     for (int i = 0; i < 18; ++i) W[i] = 0.0;
@@ -345,6 +349,7 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
     shc[0][lane] = 0.0;
     shc[1][lane] = 0.0;
     __syncthreads();
+    STAMP(12);
     if (act && lane == first) {  // landmark-level sums in slot order, then the 3x3 elimination
         double Vl[6] = {0, 0, 0, 0, 0, 0}, gl[3] = {0, 0, 0}, cl = 0.0;
         for (int k = 0; k < nk; ++k) {
@@ -380,6 +385,7 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
         shc[1][lane] = ok ? 0.0 : 1.0;
     }
     __syncthreads();
+    STAMP(13);
     if (act && fr) {
         double Vi[9], g3[3];
 #pragma unroll
@@ -417,6 +423,21 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
         Wk.partA[w * kPartA] = c;
         Wk.partA[w * kPartA + 1] = b;
     }
+    STAMP(14);
+}
+
+__device__ __forceinline__ double rl64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Fixed-pairing butterfly sum over the wave; lane 0's value is returned to every lane.
+__device__ __forceinline__ double wave_sum_det(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return rl64(v, 0);
 }
 
 // Deterministic sum of n values in global memory: thread t adds elements t, t + T, t + 2T, ...
@@ -440,117 +461,134 @@ __device__ double block_ordered_sum(const double* __restrict__ v, int n, int str
 
 // ---------------------------------------------------------------------------------------
 // K4c: one wave per chunk of <= 64 slot pairs of one upper-triangular 6x6 camera block
-// (fa <= fb), plus one wave for the cost.  Lane = pair:
-//   S_ab -= Y_a W_b^T   (+ U_a, b_a, g_c,a on diagonal blocks),
-// summed over the chunk's lanes in lane order (LDS), published as a chunk partial; the last
-// chunk of a block to arrive (agent-scope release/acquire + arrival counter) adds the block's
-// chunk partials in chunk order and writes the block of S (and b, g_c).  Deterministic.
+// (fa <= fb).  Lane = pair:  S_ab -= Y_a W_b^T  (+ U_a, b_a, g_c,a on diagonal blocks).
+// The lane partials are transposed through LDS and summed in lane order; the chunk partial
+// (48 values) goes to cpart.  No atomics: K4d combines the chunks of each block in order.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, int lambda_owner) {
+__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk) {
     __shared__ double sh[kBlockF * 65];
-    __shared__ int last;
     if (Wk.st->done) return;
+    STAMP(16);
     const int c = blockIdx.x, lane = threadIdx.x;
-    double* sys = Wk.sys;
-    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free, SC0 = SG0 + 6 * G.n_free;
-    if (c == G.n_chunk) {  // cost + singular-landmark count
-        const double cs = block_ordered_sum<64>(Wk.partA, G.n_wave, kPartA, sh);
-        const double bd = block_ordered_sum<64>(Wk.partA + 1, G.n_wave, kPartA, sh);
-        if (lane == 0) {
-            sys[SC0] = cs;
-            sys[SC0 + 1] = bd;
-        }
-        return;
-    }
     const int pb = Pr.chunk_pb[c];
-    const int fa = Pr.pb_fa[pb], fb = Pr.pb_fb[pb];
-    const bool diag = fa == fb;
+    const bool diag = Pr.pb_fa[pb] == Pr.pb_fb[pb];
     const int p0 = Pr.chunk_pair[c], np = Pr.chunk_pair[c + 1] - p0;
     const double* sf = Wk.slotf;
-    {
-        double acc[36], bg[12];
+    double acc[36], bg[12];
 #pragma unroll
-        for (int i = 0; i < 36; ++i) acc[i] = 0.0;
+    for (int i = 0; i < 36; ++i) acc[i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < 12; ++i) bg[i] = 0.0;
-        if (lane < np) {
-            const int p = p0 + lane;
-            const int sa = Pr.pair_a[p], sb = Pr.pair_b[p];
-            const double2* ra = reinterpret_cast<const double2*>(sf + (size_t)sa * kSlotF);
-            const double2* rb = reinterpret_cast<const double2*>(sf + (size_t)sb * kSlotF);
-            double Ya[18], Wb[18];
+    for (int i = 0; i < 12; ++i) bg[i] = 0.0;
+    if (lane < np) {
+        const int p = p0 + lane;
+        const int sa = Pr.pair_a[p], sb = Pr.pair_b[p];
+        const double2* ra = reinterpret_cast<const double2*>(sf + (size_t)sa * kSlotF);
+        const double2* rb = reinterpret_cast<const double2*>(sf + (size_t)sb * kSlotF);
+        double Ya[18], Wb[18];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                const double2 y = ra[SY / 2 + i], w = rb[SW / 2 + i];
-                Ya[2 * i] = y.x; Ya[2 * i + 1] = y.y;
-                Wb[2 * i] = w.x; Wb[2 * i + 1] = w.y;
+        for (int i = 0; i < 9; ++i) {
+            const double2 y = ra[SY / 2 + i], w = rb[SW / 2 + i];
+            Ya[2 * i] = y.x; Ya[2 * i + 1] = y.y;
+            Wb[2 * i] = w.x; Wb[2 * i + 1] = w.y;
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                acc[a * 6 + k] = -((Ya[a * 3] * Wb[k * 3] + Ya[a * 3 + 1] * Wb[k * 3 + 1]) + Ya[a * 3 + 2] * Wb[k * 3 + 2]);
+        if (diag) {
+            double r[34];  // record entries 36..69: U (21), b (6), g_c (6), pad
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const double2 v = ra[SU / 2 + i];
+                r[2 * i] = v.x; r[2 * i + 1] = v.y;
             }
+            int u = 0;
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
-                for (int k = 0; k < 6; ++k)
-                    acc[a * 6 + k] = -((Ya[a * 3] * Wb[k * 3] + Ya[a * 3 + 1] * Wb[k * 3 + 1]) + Ya[a * 3 + 2] * Wb[k * 3 + 2]);
-            if (diag) {
-                const double* r = sf + (size_t)sa * kSlotF;
-                int u = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int k = a; k < 6; ++k) {
-                        const double v = r[SU + u++];
-                        acc[a * 6 + k] += v;
-                        if (k != a) acc[k * 6 + a] += v;
-                    }
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    bg[a] = r[SB + a];
-                    bg[6 + a] = r[SG + a];
+                for (int k = a; k < 6; ++k) {
+                    const double v = r[u++];
+                    acc[a * 6 + k] += v;
+                    if (k != a) acc[k * 6 + a] += v;
                 }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                bg[a] = r[SB - SU + a];
+                bg[6 + a] = r[SG - SU + a];
             }
         }
-#pragma unroll
-        for (int i = 0; i < 36; ++i) sh[i * 65 + lane] = acc[i];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) sh[(36 + i) * 65 + lane] = bg[i];
     }
+    STAMP(17);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) sh[i * 65 + lane] = acc[i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) sh[(36 + i) * 65 + lane] = bg[i];
     __syncthreads();
     const int nf = diag ? kBlockF : 36;
     if (lane < nf) {
+        const double* row = sh + lane * 65;
         double s = 0.0;
-        for (int k = 0; k < np; ++k) s += sh[lane * 65 + k];
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) s += row[k];  // lanes >= np hold zeros
         Wk.cpart[(size_t)c * kBlockF + lane] = s;
     }
-    // publish the chunk partial; the last arriver of the block combines (MI355X split-K recipe)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int nch = Pr.pb_chunk[pb + 1] - Pr.pb_chunk[pb];
-    if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(Wk.cnt + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (old == nch - 1) ? 1 : 0;
+    STAMP(18);
+}
+
+// Cost and singular-landmark count of this rank from the K4 wave partials (one wave, fixed
+// order); written to sys[SC0], sys[SC0 + 1].  Returns the singular count on every lane.
+__device__ double cost_partials(const Geometry& G, const Work& Wk, int lane, int SC0) {
+    double c = 0.0, b = 0.0;
+    for (int w = lane; w < G.n_wave; w += 64) {
+        c += Wk.partA[w * kPartA];
+        b += Wk.partA[w * kPartA + 1];
     }
-    __syncthreads();
-    if (!last) return;
+    c = wave_sum_det(c);
+    b = wave_sum_det(b);
     if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Wk.cnt[pb] = 0;  // ready for the next iteration (also zeroed by ba_reset)
+        Wk.sys[SC0] = c;
+        Wk.sys[SC0 + 1] = b;
     }
-    __syncthreads();
-    if (lane < nf) {
-        double s = 0.0;
-        const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
+    return b;
+}
+
+// Entry k (< 48) of camera block pb: its chunk partials in chunk order (+ lambda on the
+// diagonal of S on the owner rank).
+__device__ __forceinline__ double block_entry(const Prob& Pr, const Work& Wk, int pb, int k, bool diag,
+                                              int lambda_owner) {
+    const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
+    double v = 0.0;
 #pragma unroll 8
-        for (int cc = c0; cc < c1; ++cc) s += Wk.cpart[(size_t)cc * kBlockF + lane];
-        if (lane < 36) {
-            if (diag && lambda_owner && lane / 6 == lane % 6) s += Wk.st->lambda;
-            sys[pb * 36 + lane] = s;
-        } else if (lane < 42) {
-            sys[SB0 + 6 * fa + (lane - 36)] = s;   // b = -g_c + sum Y g_p
-        } else {
-            sys[SG0 + 6 * fa + (lane - 42)] = s;   // g_c
-        }
+    for (int cc = c0; cc < c1; ++cc) v += Wk.cpart[(size_t)cc * kBlockF + k];
+    if (k < 36 && diag && lambda_owner && k / 6 == k % 6) v += Wk.st->lambda;
+    return v;
+}
+
+// K4d: one wave per camera block: S, b, g_c from the block's chunk partials in chunk order
+// (+ lambda on the diagonal on the owner rank); one extra wave for the cost and the
+// singular-landmark count of this rank.
+__global__ __launch_bounds__(64) void ba_schur_combine(Geometry G, Prob Pr, Work Wk, int lambda_owner) {
+    if (Wk.st->done) return;
+    const int pb = blockIdx.x, lane = threadIdx.x;
+    double* sys = Wk.sys;
+    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free, SC0 = SG0 + 6 * G.n_free;
+    if (pb == G.n_pb) {
+        cost_partials(G, Wk, lane, SC0);
+        return;
+    }
+    STAMP(19);
+    const int fa = Pr.pb_fa[pb];
+    const bool diag = fa == Pr.pb_fb[pb];
+    const int nf = diag ? kBlockF : 36;
+    if (lane >= nf) return;
+    const double v = block_entry(Pr, Wk, pb, lane, diag, lambda_owner);
+    if (lane < 36) {
+        sys[pb * 36 + lane] = v;
+    } else if (lane < 42) {
+        sys[SB0 + 6 * fa + (lane - 36)] = v;   // b = -g_c + sum Y g_p
+    } else {
+        sys[SG0 + 6 * fa + (lane - 42)] = v;   // g_c
     }
 }
 
@@ -561,21 +599,9 @@ __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work 
 //   broadcasts, rank-8 trailing update by all 4 waves), which leaves y = L^-1 b in row n;
 //   back substitution L^T dc = y by wave 0; |dc|^2, g_c.dc; SE3 (+) trial poses.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ double rl64(double v, int lane) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 constexpr int kNB = 8;  // Cholesky panel width (blocked path, n > 60)
 
-// Fixed-pairing butterfly sum over the wave; lane 0's value is returned to every lane.
-__device__ __forceinline__ double wave_sum_det(double v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return rl64(v, 0);
-}
 
 // 1/sqrt(x), f64: hardware estimate + two Newton steps (full f64 precision for normal x > 0).
 __device__ __forceinline__ double rsqrt_f64(double x) {
@@ -630,8 +656,8 @@ __device__ __forceinline__ void chol_step(double (&a)[NP], int lane, double* col
 // readlanes; row NP ends as y = L^-1 b.  Back substitution L^T dc = y reads L transposed from
 // LDS.  Same result as the blocked path up to f64 rounding (tolerance parity).
 template <int NF>
-__device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* dL, int n,
-                                 int lane) {
+__device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* dL,
+                                 const double* gcl, int n, int lane) {
     constexpr int NP = 6 * NF;
     LmState* st = Wk.st;
     double a[NP];
@@ -680,11 +706,9 @@ __device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& 
         yv = lane < j ? upd : (lane == j ? xj : yv);
     }
     STAMP(3);
-    const double* sys = Wk.sys;
-    const int SG0 = G.n_pb * 36 + 6 * G.n_free;
     const double x = lane < n ? yv : 0.0;
     const double d2 = wave_sum_det(x * x);
-    const double gd = wave_sum_det(lane < n ? sys[SG0 + lane] * x : 0.0);
+    const double gd = wave_sum_det(lane < n ? gcl[lane] * x : 0.0);
     __builtin_amdgcn_wave_barrier();
     if (lane < n) {
         Wk.dc[lane] = x;
@@ -716,6 +740,7 @@ template <int NF>
 __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
     __shared__ __attribute__((aligned(16))) double A[(kMaxN + 1) * kLdA];
     __shared__ double dL[kMaxN];
+    __shared__ double gcl[kMaxN];
     __shared__ int pbf[2 * kMaxFree * (kMaxFree + 1) / 2];
     __shared__ int fail;
     LmState* st = Wk.st;
@@ -732,11 +757,17 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     if (tid == 0) fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
     __syncthreads();
     // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
-    // blocks (fa < fb, upper) are transposed into the lower triangle
-#pragma unroll 8
-    for (int e = tid; e < SB0; e += 256) {
+    // blocks (fa < fb, upper) are transposed into the lower triangle; b as row n, g_c in gcl
+#pragma unroll 4
+    for (int e = tid; e < SB0 + 12 * nF; e += 256) {
         const double v = sys[e];
-        const int pb = e / 36, k = e - 36 * (e / 36);
+        if (e >= SB0) {  // b, g_c
+            const int i = e - SB0;
+            if (i < n) A[n * kLdA + i] = v;
+            else gcl[i - n] = v;
+            continue;
+        }
+        const int pb = e / 36, k = e - 36 * pb;
         const int fa = pbf[2 * pb], fb = pbf[2 * pb + 1];
         const int r = 6 * fa + k / 6, c = 6 * fb + k % 6;
         if (fa == fb) {
@@ -745,7 +776,6 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             A[c * kLdA + r] = v;
         }
     }
-    for (int i = tid; i < n; i += 256) A[n * kLdA + i] = sys[SB0 + i];  // b as row n
     __syncthreads();
     STAMP(1);
     if constexpr (NF > 0) {
@@ -758,7 +788,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             return;
         }
         STAMP(2);
-        camera_solve_reg<NF>(G, Pr, Wk, A, dL, n, lane);
+        camera_solve_reg<NF>(G, Pr, Wk, A, dL, gcl, n, lane);
         return;
     } else {
     for (int jb = 0; jb < n && !fail; jb += kNB) {
@@ -871,7 +901,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             Wk.dc[i] = x;
             A[i] = x;
             A[kLdA + i] = x * x;
-            A[2 * kLdA + i] = sys[SG0 + i] * x;
+            A[2 * kLdA + i] = gcl[i] * x;
         }
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -909,11 +939,12 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
     __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const LmState* st = Wk.st;
     if (st->done || !st->solve_ok) return;
+    STAMP(20);
     const int w = blockIdx.x, lane = threadIdx.x;
     const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
     const int s = s0 + lane;
     const bool act = s < s1;
-    const int cur = st->cur, n = G.n_slot, m = G.n_lm;
+    const int cur = st->cur, m = G.n_lm;
     int kf = 0, first = lane, nk = 1, l = 0;
     double t3[3] = {0.0, 0.0, 0.0};
     if (act) {
@@ -982,6 +1013,7 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
         for (int k = 0; k < s1 - s0; ++k) acc += shs[lane][k];
         Wk.partD[w * kPartD + lane] = acc;
     }
+    STAMP(21);
 }
 
 // Trial scalars of this rank: the K6 wave partials (+ |x|^2 of the free poses on the owner
@@ -1115,7 +1147,7 @@ struct BundleAdjuster {
     DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_uv;
     DevBuf<uint8_t> d_cam;
     DevBuf<int> d_free, d_slot_kf, d_slot_lm, d_slot_obs, d_slot_first, d_slot_nk, d_wave_slot, d_chunk_pb,
-        d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb, d_cnt;
+        d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb;
     DevBuf<double> d_slotf, d_lmd, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
     DevBuf<LmState> d_state;
     HostBuf<LmState> h_state;
@@ -1169,7 +1201,7 @@ struct BundleAdjuster {
         w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
         w.pose_init = d_pose_init.p; w.pw_init = d_pw_init.p;
         w.slotf = d_slotf.p; w.lmd = d_lmd.p; w.partA = d_partA.p; w.partD = d_partD.p;
-        w.cpart = d_cpart.p; w.cnt = d_cnt.p;
+        w.cpart = d_cpart.p;
         w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p; w.st = d_state.p;
         return w;
     }
@@ -1283,7 +1315,6 @@ struct BundleAdjuster {
         up(d_chunk_pb, chunk_pb);
         up(d_chunk_pair, chunk_pair);
         up(d_pb_chunk, pb_chunk);
-        grow(d_cnt, n_pb);
         grow(d_cpart, (size_t)kBlockF * G.n_chunk);
         up(d_pair_a, pa);
         up(d_pair_b, pbv);
@@ -1315,25 +1346,27 @@ struct BundleAdjuster {
         RSVIO_HIP(hipGetLastError());
     }
 
-    // K4 + K4c: this rank's reduced camera system in d_sys, summed over ranks when sharded
+    // K4 + K4c + K4d: this rank's reduced camera system in d_sys, summed over ranks when sharded
     void enqueue_linear_system() {
         const Prob pr = prob();
         const Work wk = work();
         if (G.n_wave) hipLaunchKernelGGL(ba_linearize_eliminate, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
-        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(64), 0, stream, G, pr, wk);
+        RSVIO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(ba_schur_combine, dim3(G.n_pb + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
         allreduce(d_sys.p, (size_t)36 * G.n_pb + 12 * G.n_free + 2);
     }
 
-    // register-resident factorisation for n_free <= 10 (padded to an even count), blocked otherwise
+    // register-resident factorisation for n_free <= 10, blocked LDS factorisation otherwise
     void launch_camera_solve(const Prob& pr, const Work& wk) {
         const dim3 g(1), b(256);
-        switch (G.n_free <= 10 ? (G.n_free + 1) / 2 : 0) {
-            case 1: hipLaunchKernelGGL(ba_camera_solve<2>, g, b, 0, stream, G, pr, wk); break;
-            case 2: hipLaunchKernelGGL(ba_camera_solve<4>, g, b, 0, stream, G, pr, wk); break;
-            case 3: hipLaunchKernelGGL(ba_camera_solve<6>, g, b, 0, stream, G, pr, wk); break;
-            case 4: hipLaunchKernelGGL(ba_camera_solve<8>, g, b, 0, stream, G, pr, wk); break;
-            case 5: hipLaunchKernelGGL(ba_camera_solve<10>, g, b, 0, stream, G, pr, wk); break;
+        switch (G.n_free <= 10 ? G.n_free : 0) {
+#define RSVIO_CAM(NF) \
+    case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk); break;
+            RSVIO_CAM(1) RSVIO_CAM(2) RSVIO_CAM(3) RSVIO_CAM(4) RSVIO_CAM(5)
+            RSVIO_CAM(6) RSVIO_CAM(7) RSVIO_CAM(8) RSVIO_CAM(9) RSVIO_CAM(10)
+#undef RSVIO_CAM
             default: hipLaunchKernelGGL(ba_camera_solve<0>, g, b, 0, stream, G, pr, wk); break;
         }
     }

@@ -46,17 +46,17 @@ int guarded(F&& f) {
 // thread 0 of block b writes the shader clock into slot k of row b after draining its
 // outstanding memory operations.  Compiled out of the product library.
 #ifdef RSVIO_STAMPS
-#define RSVIO_DBG_DECL static __device__ unsigned long long g_dbg[4096 * 16];
+#define RSVIO_DBG_DECL static __device__ unsigned long long g_dbg[4096 * 32];
 #define STAMP(k)                                                              \
     do {                                                                      \
         if (threadIdx.x == 0 && blockIdx.x < 4096) {                          \
             __builtin_amdgcn_s_waitcnt(0);                                    \
-            g_dbg[blockIdx.x * 16 + (k)] = (unsigned long long)clock64();     \
+            g_dbg[blockIdx.x * 32 + (k)] = (unsigned long long)clock64();     \
         }                                                                     \
     } while (0)
 #define RSVIO_DBG_READER(name)                                                             \
     extern "C" int name(unsigned long long* out, int n) {                                  \
-        if (n > 4096 * 16) n = 4096 * 16;                                                  \
+        if (n > 4096 * 32) n = 4096 * 32;                                                  \
         return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(unsigned long long) * n); \
     }
 #else

@@ -272,7 +272,7 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
     const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
     for (int it = 0; it < max_iter; ++it) {
 #ifdef RSVIO_STAMPS
-        if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 16 + 15] += 1;
+        if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] += 1;
 #endif
         float x = A.m00 * patx;
         x = A.m01 * paty + x;
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
     Aff fwd, bwd;
 #ifdef RSVIO_STAMPS
-    if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 16 + 15] = 0;
+    if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] = 0;
 #endif
     STAMP(0);
     bool ok = track_one(L.pyr0[b], L.pyr1[b], L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,

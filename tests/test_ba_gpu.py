@@ -161,3 +161,18 @@ def test_sliding_window_mirror(gpu, oracle):
     assert sw.last_result.status > 0
     # second solve starts from the f32 map points (sliding_window.rs:249-254)
     assert sw.optimize()
+
+
+@pytest.mark.parametrize("n_kf", [2, 3, 4, 6, 8, 11, 12])
+def test_window_sizes_match_oracle(gpu, oracle, n_kf):
+    """Every camera-solve variant (register path for 1..10 free keyframes, blocked path above)."""
+    from rsvio import synthetic as S
+    prob = S.ba_problem(n_kf=n_kf, n_lm=40 * n_kf, kf_per_lm=min(n_kf, 4), seed=100 + n_kf, init_seed=200 + n_kf)
+    ba = _adjuster(gpu, prob)
+    res = ba.run()
+    pose, pw = ba.state()
+    po, pwo, ro = oracle.ba_solve(prob)
+    assert res.status == ro.status and res.iterations == ro.iterations
+    assert np.abs(pose - po).max() < 1e-7
+    assert np.abs(pw - pwo).max() < 1e-6
+    ba.close()

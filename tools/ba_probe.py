@@ -28,3 +28,29 @@ st = np.array(buf[:16], dtype=np.int64)
 print("camera_solve phases (cycles):", np.diff(st[:7]).tolist(), "total", st[6] - st[0])
 print("  register path: factor %d, back substitution %d" % (st[7] - st[2], st[3] - st[7]))
 print("lm_decide phases (cycles):", np.diff(st[8:11]).tolist())
+
+# multi-block kernels: per-block stamps of the last launch (rows = blocks)
+nb = 4096
+big = (C.c_ulonglong * (nb * 32))()
+lib.rsvio_dbg_ba_stamps(big, nb * 32)
+T = np.array(big[:], dtype=np.int64).reshape(nb, 32)
+
+
+def report(name, cols, labels):
+    rows = T[:, cols[0]] > 0
+    for c in cols[1:]:
+        rows &= T[:, c] > 0
+    X = T[rows][:, cols]
+    if len(X) == 0:
+        print(name, "no stamps")
+        return
+    t0 = X[:, 0].min()
+    print(f"{name}: {len(X)} blocks, span {X[:, -1].max() - t0} cycles, start spread {X[:, 0].max() - t0}")
+    for i in range(1, len(cols)):
+        d = X[:, i] - X[:, i - 1]
+        print(f"   {labels[i - 1]:>22s}: median {int(np.median(d)):7d}  max {int(d.max()):7d}")
+
+
+report("linearize_eliminate", [11, 12, 13, 14], ["obs linearize", "landmark inverse", "Y/record + partials"])
+report("schur_chunks", [16, 17, 18], ["pair products", "lane-ordered chunk sum"])
+report("backsub_cost", [20, 21], ["whole block"])

@@ -42,9 +42,9 @@ e0.record(s)
 lib.rsvio_track_points_d(ctx, b, 1, 20, C.c_float(0.01), s.cuda_stream)
 e1.record(s)
 torch.cuda.synchronize()
-buf = (C.c_ulonglong * (N * 16))()
-lib.rsvio_dbg_lk_stamps(buf, N * 16)
-st = np.array(buf[:], dtype=np.int64).reshape(N, 16)
+buf = (C.c_ulonglong * (N * 32))()
+lib.rsvio_dbg_lk_stamps(buf, N * 32)
+st = np.array(buf[:], dtype=np.int64).reshape(N, 32)
 fw = st[:, 1] - st[:, 0]
 bw = st[:, 2] - st[:, 1]
 it = st[:, 15]
