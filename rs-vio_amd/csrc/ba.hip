@@ -1560,8 +1560,7 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
     if (!ba || !unique_id || nranks < 1 || rank < 0 || rank >= nranks) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
         auto& B = ba->b;
-        if (nranks == 1) return (int)RSVIO_OK;
-        ncclUniqueId id;
+        ncclUniqueId id;  // a 1-rank communicator is legal: it runs the sharded code path on one GPU
         __builtin_memcpy(&id, unique_id, sizeof(id));
         RSVIO_HIP(hipSetDevice(B.P.device));
         if (ncclCommInitRank(&B.comm, nranks, id, rank) != ncclSuccess) {

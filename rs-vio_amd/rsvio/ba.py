@@ -52,9 +52,8 @@ class BundleAdjuster:
             pass
 
     def attach_comm(self, nranks: int, rank: int, unique_id: bytes):
-        if nranks > 1:
-            buf = (C.c_uint8 * len(unique_id)).from_buffer_copy(unique_id)
-            check(_lib.load().rsvio_ba_attach_comm(self._h, nranks, rank, buf))
+        buf = (C.c_uint8 * len(unique_id)).from_buffer_copy(unique_id)
+        check(_lib.load().rsvio_ba_attach_comm(self._h, nranks, rank, buf))
 
     @staticmethod
     def rccl_unique_id() -> bytes:

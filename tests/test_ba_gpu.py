@@ -176,3 +176,22 @@ def test_window_sizes_match_oracle(gpu, oracle, n_kf):
     assert np.abs(pose - po).max() < 1e-7
     assert np.abs(pw - pwo).max() < 1e-6
     ba.close()
+
+
+def test_sharded_code_path_single_rank(gpu, cfg3):
+    """The sharded path (RCCL all-reduce of sys, per-rank trial scalars + 32-B all-reduce,
+    pre-reduced LM decision) on a 1-rank communicator equals the unsharded path bit for bit."""
+    from rsvio.ba import BundleAdjuster
+    a = _adjuster(gpu, cfg3)
+    ra = a.run()
+    pa, wa = a.state()
+    b = BundleAdjuster(max_keyframes=21, max_landmarks=cfg3.n_lm, max_observations=cfg3.n_obs)
+    b.attach_comm(1, 0, BundleAdjuster.rccl_unique_id())
+    b.set_problem_from(cfg3)
+    rb = b.run()
+    pb, wb = b.state()
+    assert (ra.status, ra.iterations) == (rb.status, rb.iterations)
+    assert ra.final_cost == rb.final_cost
+    assert np.array_equal(pa, pb) and np.array_equal(wa, wb)
+    a.close()
+    b.close()
