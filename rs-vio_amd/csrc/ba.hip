@@ -17,8 +17,8 @@
 //   K4c ba_schur_chunks         wave / 64 pairs: -Y_a W_b^T (+ U on the diagonal), lane-ordered chunk sums
 //   K4d ba_schur_combine        wave / camera block: chunk partials in chunk order -> S, b, g_c; cost
 //   [RCCL all-reduce of the per-rank reduced system when sharded]
-//   K5  ba_camera_solve         1 workgroup: fixed-order chunk sums -> S, b in LDS, Cholesky,
-//                               substitutions, SE3 (+) trial poses
+//   K5  ba_camera_solve         1 workgroup: S, b in LDS; pipelined 4-wave LDL^T (n <= 60) or
+//                               blocked Cholesky; substitutions, SE3 (+) trial poses
 //   K6  ba_backsub_cost         wave / landmark group: dp = V^-1 (-g_p - W^T dc), trial point,
 //                               trial cost
 //   [RCCL all-reduce of 4 trial scalars when sharded]
@@ -594,90 +594,161 @@ __global__ __launch_bounds__(64) void ba_schur_combine(Geometry G, Prob Pr, Work
 
 // ---------------------------------------------------------------------------------------
 // K5: camera system solve (one workgroup of 256):
-//   S (lower triangle) and b (as row n) from sys -> LDS; blocked right-looking Cholesky of
-//   [S b; b^T .] in panels of 8 columns (panel factor by wave 0 in registers with v_readlane
-//   broadcasts, rank-8 trailing update by all 4 waves), which leaves y = L^-1 b in row n;
-//   back substitution L^T dc = y by wave 0; |dc|^2, g_c.dc; SE3 (+) trial poses.
+//   S (lower triangle) and b (as row n) from sys -> LDS, then
+//   n <= 60 (<= 10 free keyframes): pipelined 4-wave register LDL^T of [S; b^T] (chol_pipe),
+//     unit-L back substitution by wave 0;
+//   n > 60: blocked right-looking Cholesky in LDS (panels of 8: panel factor by wave 0 with
+//     v_readlane broadcasts, rank-8 trailing update by all 4 waves), back substitution by wave 0;
+//   |dc|^2, g_c.dc; SE3 (+) trial poses.
 // ---------------------------------------------------------------------------------------
 
 constexpr int kNB = 8;  // Cholesky panel width (blocked path, n > 60)
 
 
-// 1/sqrt(x), f64: hardware estimate + two Newton steps (full f64 precision for normal x > 0).
-__device__ __forceinline__ double rsqrt_f64(double x) {
-    double y = __builtin_amdgcn_rsq(x);
+
+// 1/d, f64: hardware estimate + two Newton steps (full f64 precision for normal d).
+__device__ __forceinline__ double rcp_f64(double d) {
+    double y = __builtin_amdgcn_rcp(d);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const double hx = 0.5 * x;
-        y = y * (1.5 - hx * y * y);
-    }
+    for (int i = 0; i < 2; ++i) y = fma(y, fma(-d, y, 1.0), y);
     return y;
 }
 
-// Column step K of the register-resident Cholesky (compile-time K: the row stays in registers).
-template <int NP, int K>
-__device__ __forceinline__ void chol_step(double (&a)[NP], int lane, double* colb, const double2* colb2, double* dL,
-                                          bool& bad, double piv) {
-    bad |= !(piv > 0.0) || !isfinite(piv);
-    const double inv = rsqrt_f64(piv);
-    dL[K] = inv;  // every lane stores the same value
-    const double lk = a[K] * inv;
-    a[K] = lk;
-    // next pivot straight from registers: on lane K+1, L[K+1][K] is its own lk, so the
-    // critical path does not wait for the LDS broadcast (bitwise the same update as below)
-    double piv_next = 0.0;
-    if constexpr (K + 1 < NP) piv_next = rl64(fma(-lk, lk, a[K + 1]), K + 1);
-    // column K broadcast back through LDS; alternating buffers let step K+1's pivot chain
-    // overlap step K's trailing update
-    constexpr int kOff = (K & 1) * 64;
-    colb[kOff + lane] = lk;
-    // trailing update of this lane's row in chunks of 32 columns (16 x 16 B broadcast reads)
-#pragma unroll
-    for (int c2 = (K + 1) / 2; c2 < NP / 2; c2 += 16) {
-        double2 v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-            if (c2 + u < NP / 2) v[u] = colb2[kOff / 2 + c2 + u];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int c = 2 * (c2 + u);
-            if (c2 + u < NP / 2) {
-                if (c > K) a[c] = fma(-lk, v[u].x, a[c]);
-                a[c + 1] = fma(-lk, v[u].y, a[c + 1]);
-            }
+// Pipelined 4-wave LDL^T of the augmented system [S; b^T]: wave WV owns the contiguous columns
+// [WV*CW, WV*CW + CW) of every row (lane = row; lane NP = b).  A wave first consumes the
+// columns of the waves before it (waits on an LDS progress counter, then rank-1 updates its own
+// columns) and then factors its own columns, publishing each finished column to LDS: the unit
+// L column (Lc, kept for the back substitution) and the unscaled column D L (Uc, which the
+// updates use).  No barrier: one wave's serial pivot chain (pivot -> 1/d -> next pivot, from
+// registers) overlaps the trailing updates of the waves after it.  LDL^T needs no square root,
+// which shortens that chain; row NP ends as z = D^-1 L^-1 b.
+constexpr int kLcLd = 65;
+
+template <int NP, int CW, int WV, int K>
+__device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double* Lc, double* Uc, int* progress,
+                                               int& seen, bool& bad, double inv) {
+    constexpr int c0 = WV * CW;
+    constexpr int c1 = (c0 + CW < NP) ? c0 + CW : NP;
+    constexpr int KN = (K + 1 < c0) ? K + 2 : K + 1;  // consume columns in pairs
+    if constexpr (K < c0) {
+        // consume columns K (.. KN-1) of earlier waves (the LDS counter is re-read only when behind)
+        if (seen < KN) {
+            do {
+                seen = __hip_atomic_load(progress, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (seen >= KN) break;
+                __builtin_amdgcn_s_sleep(1);
+            } while (true);
         }
+        const double lr = Lc[K * kLcLd + lane];
+        const double* u = Uc + K * kLcLd;
+        if constexpr (KN == K + 2) {
+            const double lr2 = Lc[(K + 1) * kLcLd + lane];
+            const double* u2 = Uc + (K + 1) * kLcLd;
+            double v1[CW], v2[CW];
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) {
+                v1[jj] = u[c0 + jj];
+                v2[jj] = u2[c0 + jj];
+            }
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj)
+                if (c0 + jj < NP) a[jj] = fma(-lr2, v2[jj], fma(-lr, v1[jj], a[jj]));
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj)
+                if (c0 + jj < NP) a[jj] = fma(-lr, u[c0 + jj], a[jj]);
+        }
+        if constexpr (KN == c0) {  // first own pivot
+            const double piv = rl64(a[0], c0);
+            bad |= !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+    } else if constexpr (K < c1) {
+        // own column K (inv = 1/d_K ready); the next pivot comes straight from registers (on
+        // lane K+1, L[K+1][K] and (DL)[K+1][K] are its own values), so its 1/d chain overlaps
+        // this column's trailing FMAs
+        constexpr int j = K - c0;
+#ifdef RSVIO_STAMPS
+        if (K == c0 && lane == 0) g_dbg[28 + WV] = (unsigned long long)clock64();
+#endif
+        const double uk = a[j];
+        const double l = uk * inv;
+        a[j] = l;
+        Lc[K * kLcLd + lane] = l;
+        Uc[K * kLcLd + lane] = uk;
+        double piv = 1.0;
+        const double* u = Uc + K * kLcLd;
+        if constexpr (j + 1 < CW && K + 1 < NP) {
+            // column K+1 by readlane (no LDS round trip on the pivot chain)
+            a[j + 1] = fma(-l, rl64(uk, K + 1), a[j + 1]);
+            piv = rl64(a[j + 1], K + 1);
+        }
+#pragma unroll
+        for (int jj = j + 2; jj < CW; ++jj)
+            if (c0 + jj < NP) a[jj] = fma(-l, u[c0 + jj], a[jj]);
+        if constexpr (j + 1 < CW && K + 1 < NP) {
+            bad |= !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+        __hip_atomic_store(progress, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if constexpr (K + 1 < NP) chol_step<NP, K + 1>(a, lane, colb, colb2, dL, bad, piv_next);
+    // materialise this step's updates here (keeps the compiler from sinking the FMAs past the
+    // next wait loop, which would keep every loaded column alive)
+#pragma unroll
+    for (int jj = 0; jj < CW; ++jj) __asm__ volatile("" : "+v"(a[jj]));
+    constexpr int KNEXT = (K < c0) ? KN : K + 1;
+    if constexpr (KNEXT < c1) chol_pipe_step<NP, CW, WV, KNEXT>(a, lane, Lc, Uc, progress, seen, bad, inv);
 }
 
-// Register-resident Cholesky of the (n+1) x n augmented system [S; b^T] for n <= NP = 6 NF <= 60,
-// one wave: lane r owns row r (lanes n..NP-1 are identity padding, lane NP holds b), so the
-// factorisation is NP fully unrolled right-looking column steps whose column broadcasts are
-// readlanes; row NP ends as y = L^-1 b.  Back substitution L^T dc = y reads L transposed from
-// LDS.  Same result as the blocked path up to f64 rounding (tolerance parity).
-template <int NF>
-__device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* dL,
-                                 const double* gcl, int n, int lane) {
-    constexpr int NP = 6 * NF;
-    LmState* st = Wk.st;
-    double a[NP];
-    double* colb = A + 100 * kLdA;  // 16-byte aligned (A is, 100 * kLdA is even)
-    // row image of this lane: lower triangle (c <= r) of S, identity padding, b as row NP
+template <int NP, int CW, int WV>
+__device__ void chol_pipe(const double* A, double* Lc, double* Uc, int* progress, int* badw, int n, int lane) {
+    constexpr int c0 = WV * CW;
+    double a[CW];
     const int src = lane < n ? lane : (lane == NP ? n : -1);
 #pragma unroll
-    for (int c = 0; c < NP; ++c) {
+    for (int jj = 0; jj < CW; ++jj) {
+        const int c = c0 + jj;
         double v = 0.0;
         if (src >= 0 && c < n && (c <= lane || lane == NP)) v = A[src * kLdA + c];
         if (lane >= n && lane < NP && c == lane) v = 1.0;
-        a[c] = v;
+        a[jj] = v;
     }
+    __syncthreads();  // every wave holds its columns: A may now be overwritten by Lc / Uc
     bool bad = false;
-    // opaque zero offset: one LDS base register + immediate offsets for every broadcast read
-    int zero = 0;
-    __asm__ volatile("" : "+s"(zero));
-    chol_step<NP, 0>(a, lane, colb + 2 * zero, reinterpret_cast<const double2*>(colb + 2 * zero), dL, bad,
-                      rl64(a[0], 0));
-    if (bad) {
+    if constexpr (c0 < NP) {
+        double inv = 0.0;
+        if constexpr (c0 == 0) {
+            const double piv = rl64(a[0], 0);
+            bad = !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+        int seen = 0;
+        chol_pipe_step<NP, CW, WV, 0>(a, lane, Lc, Uc, progress, seen, bad, inv);
+    }
+    if (lane == 0) badw[WV] = bad ? 1 : 0;
+#ifdef RSVIO_STAMPS
+    if (lane == 0) g_dbg[24 + WV] = (unsigned long long)clock64();
+#endif
+}
+
+template <int NF>
+__device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, const double* gcl,
+                                int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
+    constexpr int NP = 6 * NF, CW = (NP + 3) / 4;
+    const int lane = tid & 63, wave = tid >> 6;
+    LmState* st = Wk.st;
+    // Lc / Uc overwrite A once every wave has loaded its columns (A[0..n) is reused for dc later)
+    double* Lc = A + 128;
+    double* Uc = Lc + NP * kLcLd;
+    switch (wave) {
+        case 0: chol_pipe<NP, CW, 0>(A, Lc, Uc, progress, badw, n, lane); break;
+        case 1: chol_pipe<NP, CW, 1>(A, Lc, Uc, progress, badw, n, lane); break;
+        case 2: chol_pipe<NP, CW, 2>(A, Lc, Uc, progress, badw, n, lane); break;
+        default: chol_pipe<NP, CW, 3>(A, Lc, Uc, progress, badw, n, lane); break;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    if (badw[0] | badw[1] | badw[2] | badw[3]) {
         if (lane == 0) {
             st->solve_ok = 0;
             st->dc2 = 0.0;
@@ -686,24 +757,17 @@ __device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& 
         return;
     }
     STAMP(7);
-    // L (lower) and y (row NP) back to LDS, rows r <= NP
-#pragma unroll
-    for (int c = 0; c < NP; ++c)
-        if (lane <= NP) A[lane * kLdA + c] = a[c];
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    // lane i gathers column i of L (row j, column i = L^T[i][j]) up front, then the solve is
-    // branch-free: x_j = y_j / L_jj broadcast by readlane, y_i -= L_ji x_j for i < j
     const int li = lane < NP ? lane : 0;
-    double yv = A[NP * kLdA + li];
+    const double* Li = Lc + li * kLcLd;  // column li of L: L[j][li] for j >= li, y_li at row NP
+    double yv = Li[NP];
     double lt[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) lt[j] = A[j * kLdA + li];
+    for (int j = 0; j < NP; ++j) lt[j] = Li[j];
 #pragma unroll
-    for (int j = NP - 1; j >= 0; --j) {
-        const double xj = rl64(yv, j) * dL[j];
+    for (int j = NP - 1; j >= 0; --j) {  // L^T x = z (unit diagonal)
+        const double xj = rl64(yv, j);
         const double upd = fma(-lt[j], xj, yv);
-        yv = lane < j ? upd : (lane == j ? xj : yv);
+        yv = lane < j ? upd : yv;
     }
     STAMP(3);
     const double x = lane < n ? yv : 0.0;
@@ -712,20 +776,22 @@ __device__ void camera_solve_reg(const Geometry& G, const Prob& Pr, const Work& 
     __builtin_amdgcn_wave_barrier();
     if (lane < n) {
         Wk.dc[lane] = x;
-        A[lane] = x;  // row 0 of A reused as dc for the pose updates
+        A[lane] = x;  // row 0 of A reused as dc for the pose updates (Lc lies past row NP)
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     STAMP(4);
-    const int cur = st->cur;
-    for (int k = lane; k < G.n_kf; k += 64) {
-        const int f = Pr.free_idx[k];
-        const double* p = Wk.pose[cur] + 7 * k;
-        double* q = Wk.pose[1 - cur] + 7 * k;
-        if (f < 0)
-            for (int i = 0; i < 7; ++i) q[i] = p[i];
-        else
-            se3_plus(p, A + 6 * f, q);
+    if (lane < G.n_kf) {  // trial poses from the prefetched current poses
+        double* q = Wk.pose[1 - st->cur] + 7 * lane;
+        if (fidx < 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) q[i] = p7[i];
+        } else {
+            double qv[7];
+            se3_plus(p7, A + 6 * fidx, qv);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) q[i] = qv[i];
+        }
     }
     STAMP(5);
     if (lane == 0) {
@@ -741,7 +807,8 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     __shared__ __attribute__((aligned(16))) double A[(kMaxN + 1) * kLdA];
     __shared__ double dL[kMaxN];
     __shared__ double gcl[kMaxN];
-    __shared__ int pbf[2 * kMaxFree * (kMaxFree + 1) / 2];
+    __shared__ int badw[4];
+    __shared__ int progress;
     __shared__ int fail;
     LmState* st = Wk.st;
     if (st->done) return;
@@ -749,38 +816,65 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     const int nF = G.n_free, n = 6 * nF;
     const double* sys = Wk.sys;
     const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * nF, SC0 = SG0 + 6 * nF;
-    for (int pb = tid; pb < G.n_pb; pb += 256) {
-        pbf[2 * pb] = Pr.pb_fa[pb];
-        pbf[2 * pb + 1] = Pr.pb_fb[pb];
+    const int cur = st->cur;
+    // the trial-pose inputs of wave 0 are fetched now, behind the fill (register path)
+    double p7[7] = {0, 0, 0, 1, 0, 0, 0};
+    int fidx = -1;
+    if (NF > 0 && wave == 0 && lane < G.n_kf) {
+        fidx = Pr.free_idx[lane];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
     }
     STAMP(0);
-    if (tid == 0) fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
-    __syncthreads();
+    if (tid == 0) {
+        fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
+        progress = 0;
+    }
     // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
-    // blocks (fa < fb, upper) are transposed into the lower triangle; b as row n, g_c in gcl
-#pragma unroll 4
-    for (int e = tid; e < SB0 + 12 * nF; e += 256) {
-        const double v = sys[e];
+    // blocks (fa < fb, upper) are transposed into the lower triangle; b as row n, g_c in gcl.
+    // Each element's value and its block's keyframe pair are loaded together (one round trip).
+    const int nel = SB0 + 12 * nF;
+    auto place = [&](int e, double v, int fa, int fb) {
         if (e >= SB0) {  // b, g_c
             const int i = e - SB0;
             if (i < n) A[n * kLdA + i] = v;
             else gcl[i - n] = v;
-            continue;
+            return;
         }
-        const int pb = e / 36, k = e - 36 * pb;
-        const int fa = pbf[2 * pb], fb = pbf[2 * pb + 1];
+        const int k = e % 36;
         const int r = 6 * fa + k / 6, c = 6 * fb + k % 6;
         if (fa == fb) {
             if (r >= c) A[r * kLdA + c] = v;
         } else {
             A[c * kLdA + r] = v;
         }
+    };
+    constexpr int kFillB = 9;  // 9 x 256 >= 55 * 36 + 120 (n_free <= 10)
+    for (int e0 = tid; e0 < nel; e0 += kFillB * 256) {
+        double v[kFillB];
+        int fa[kFillB], fb[kFillB];
+#pragma unroll
+        for (int u = 0; u < kFillB; ++u) {
+            const int e = e0 + u * 256;
+            v[u] = 0.0;
+            fa[u] = fb[u] = 0;
+            if (e < nel) {
+                v[u] = sys[e];
+                if (e < SB0) {
+                    fa[u] = Pr.pb_fa[e / 36];
+                    fb[u] = Pr.pb_fb[e / 36];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kFillB; ++u)
+            if (e0 + u * 256 < nel) place(e0 + u * 256, v[u], fa[u], fb[u]);
     }
     __syncthreads();
     STAMP(1);
     if constexpr (NF > 0) {
-        if (wave != 0 || fail) {
-            if (tid == 0 && fail) {
+        if (fail) {
+            if (tid == 0) {
                 st->solve_ok = 0;
                 st->dc2 = 0.0;
                 st->gcdc = 0.0;
@@ -788,7 +882,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             return;
         }
         STAMP(2);
-        camera_solve_reg<NF>(G, Pr, Wk, A, dL, gcl, n, lane);
+        camera_solve_w4<NF>(G, Pr, Wk, A, gcl, badw, &progress, n, tid, p7, fidx);
         return;
     } else {
     for (int jb = 0; jb < n && !fail; jb += kNB) {

@@ -24,9 +24,10 @@ for rep in range(5):
 print("status", r.status, "iters", r.iterations, "solve_ms", r.solve_ms)
 buf = (C.c_ulonglong * 64)()
 lib.rsvio_dbg_ba_stamps(buf, 64)
-st = np.array(buf[:16], dtype=np.int64)
+st = np.array(buf[:32], dtype=np.int64)
 print("camera_solve phases (cycles):", np.diff(st[:7]).tolist(), "total", st[6] - st[0])
 print("  register path: factor %d, back substitution %d" % (st[7] - st[2], st[3] - st[7]))
+print("  pipe waves: own-phase start", (st[28:32] - st[2]).tolist(), "end", (np.array(buf[24:28], dtype=np.int64) - st[2]).tolist())
 print("lm_decide phases (cycles):", np.diff(st[8:11]).tolist())
 
 # multi-block kernels: per-block stamps of the last launch (rows = blocks)
