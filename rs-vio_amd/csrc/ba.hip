@@ -281,6 +281,33 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
     }
 }
 
+__device__ __forceinline__ double rl64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Row-local DPP move of a double (both halves through the same lane permutation).
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Deterministic sum over the 64 lanes (all lanes active), returned to every lane: a fixed
+// pairing inside each row of 16 (quad_perm xor 1, xor 2, half-row mirror, row mirror -- each
+// step adds the same two values on both partners, so all 16 lanes agree bitwise), then the four
+// row totals in row order.
+__device__ __forceinline__ double wave_sum_det(double v) {
+    v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp64<0x141>(v);  // row_half_mirror
+    v += dpp64<0x140>(v);  // row_mirror
+    return ((rl64(v, 0) + rl64(v, 16)) + rl64(v, 32)) + rl64(v, 48);
+}
+
 // ---------------------------------------------------------------------------------------
 // K4: one wave per landmark group, one lane per (landmark, keyframe) slot
 // ---------------------------------------------------------------------------------------
@@ -414,31 +441,18 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
 #pragma unroll
         for (int i = 0; i < kSlotF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
     }
-    if (lane == 0) {  // wave partials in lane (= landmark) order
-        double c = 0.0, b = 0.0;
-        for (int k = 0; k < s1 - s0; ++k) {
-            c += shc[0][k];
-            b += shc[1][k];
+    {  // wave partials: fixed-pairing butterflies over the lanes (first lanes hold the values)
+        const double c = wave_sum_det(shc[0][lane]);
+        const double b = wave_sum_det(shc[1][lane]);
+        if (lane == 0) {
+            Wk.partA[w * kPartA] = c;
+            Wk.partA[w * kPartA + 1] = b;
         }
-        Wk.partA[w * kPartA] = c;
-        Wk.partA[w * kPartA + 1] = b;
     }
     STAMP(14);
 }
 
-__device__ __forceinline__ double rl64(double v, int lane) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
-// Fixed-pairing butterfly sum over the wave; lane 0's value is returned to every lane.
-__device__ __forceinline__ double wave_sum_det(double v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return rl64(v, 0);
-}
 
 // Deterministic sum of n values in global memory: thread t adds elements t, t + T, t + 2T, ...
 // (independent loads, all in flight), then thread 0 adds the T per-thread sums in thread order.
@@ -1102,10 +1116,14 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
     }
     shs[0][lane] = cost;
     __syncthreads();
-    if (lane < kPartD) {
-        double acc = 0.0;
-        for (int k = 0; k < s1 - s0; ++k) acc += shs[lane][k];
-        Wk.partD[w * kPartD + lane] = acc;
+    {  // wave partials: fixed-pairing butterflies over the lanes
+        double v[kPartD];
+#pragma unroll
+        for (int i = 0; i < kPartD; ++i) v[i] = wave_sum_det(shs[i][lane]);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
+        }
     }
     STAMP(21);
 }
@@ -1117,20 +1135,31 @@ __device__ void trial_scalars(const Geometry& G, const Prob& Pr, const Work& Wk,
                               double* sh) {
     const LmState* st = Wk.st;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nw = st->solve_ok ? G.n_wave : 0;
+    // every load is issued before the state is known (one round trip): the wave partials, and
+    // the free-pose squares of both state buffers (the current one is picked afterwards)
     double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = tid; i < nw; i += 256) {
+    double sq[2] = {0.0, 0.0};
+    for (int i = tid; i < G.n_wave; i += 256) {
         const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
         acc[0] += v.x;
         acc[1] += v.y;
         acc[2] += v.z;
         acc[3] += v.w;
     }
-    if (include_poses) {
-        const double* p = Wk.pose[st->cur];
-        for (int e = tid; e < 7 * G.n_kf; e += 256)
-            if (Pr.free_idx[e / 7] >= 0) acc[3] += p[e] * p[e];
-    }
+    if (include_poses)
+        for (int e = tid; e < 7 * G.n_kf; e += 256) {
+            const bool fr = Pr.free_idx[e / 7] >= 0;
+            const double p0 = Wk.pose[0][e], p1 = Wk.pose[1][e];
+            if (fr) {
+                sq[0] += p0 * p0;
+                sq[1] += p1 * p1;
+            }
+        }
+    const int solve_ok = st->solve_ok, cur = st->cur;
+    if (!solve_ok)
+#pragma unroll
+        for (int k = 0; k < kPartD; ++k) acc[k] = 0.0;
+    acc[3] += sq[cur];
 #pragma unroll
     for (int k = 0; k < kPartD; ++k) {
         const double w = wave_sum_det(acc[k]);
@@ -1157,6 +1186,7 @@ __global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk
                                                     double cost_tol, double param_tol) {
     __shared__ double sh[256];
     LmState* stp = Wk.st;
+    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
     if (stp->done) return;
     double tv[4];
     STAMP(8);
@@ -1168,7 +1198,6 @@ __global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk
     STAMP(9);
     if (threadIdx.x != 0) return;
     LmState s = *stp;
-    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
     if (s.iter == 0) s.initial_cost = cost;
     s.cost = cost;
     s.iter += 1;
@@ -1237,7 +1266,8 @@ struct BundleAdjuster {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Geometry G{};
     bool has_problem = false;
-    int iter_chunk = 3;     // LM iterations enqueued between status read-backs
+    int iter_chunk = 2;       // LM iterations enqueued per status read-back after the first chunk
+    int last_iterations = 3;  // first chunk = previous solve's iteration count
     DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_uv;
     DevBuf<uint8_t> d_cam;
     DevBuf<int> d_free, d_slot_kf, d_slot_lm, d_slot_obs, d_slot_first, d_slot_nk, d_wave_slot, d_chunk_pb,
@@ -1494,17 +1524,21 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventRecord(ev0, stream));
         enqueue_reset(cfg.lambda_init);
         const int max_it = std::max(cfg.max_iterations, 1);
-        int enq = 0;
+        // The host reads the LM state once per chunk of iterations.  The first chunk is the
+        // previous solve's iteration count (consecutive windows converge alike), so the common
+        // case costs one read-back and no iteration enqueued after convergence.
+        int enq = 0, k = std::min(std::max(last_iterations, 1), max_it);
         while (enq < max_it) {
-            const int k = std::min(iter_chunk, max_it - enq);
+            k = std::min(k, max_it - enq);
             for (int i = 0; i < k; ++i) enqueue_iteration(cfg);
             enq += k;
+            RSVIO_HIP(hipEventRecord(ev1, stream));
             RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
             RSVIO_HIP(hipStreamSynchronize(stream));
             if (h_state.p->done) break;
+            k = iter_chunk;
         }
-        RSVIO_HIP(hipEventRecord(ev1, stream));
-        RSVIO_HIP(hipEventSynchronize(ev1));
+        last_iterations = h_state.p->iter;
         float ms = 0.0f;
         RSVIO_HIP(hipEventElapsedTime(&ms, ev0, ev1));
         const LmState& s = *h_state.p;
