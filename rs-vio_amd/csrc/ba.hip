@@ -225,16 +225,15 @@ struct Geometry {
 };
 
 // Structure-of-arrays problem description (device pointers)
+// Slot header, padded layout: slot (wave w, lane i) is entry 64 w + i, two int4 per slot
+//   {kf, landmark, lane of the landmark's first slot, slots of the landmark}
+//   {free block of kf or -1, observations (0 = padding, <= 2), camera bits, 0}
+// and its observations' normalised coordinates inline (2 double2): everything a lane needs
+// before the pose / point loads arrives in one round trip.
 struct Prob {
     const int* free_idx;     // kf -> free block or -1
-    const int* slot_kf;
-    const int* slot_lm;
-    const int* slot_obs;     // n_slot + 1
-    const int* slot_first;   // first slot of the slot's landmark
-    const int* slot_nk;      // slots of the slot's landmark
-    const int* wave_slot;    // n_wave + 1
-    const uint8_t* obs_cam;
-    const double* obs_uv;
+    const int4* slot_hdr;    // 2 per padded slot
+    const double2* slot_uv;  // 2 per padded slot
     const int* chunk_pb;     // n_chunk: camera block of each chunk
     const int* chunk_pair;   // n_chunk + 1: slot-pair range of each chunk
     const int* pb_chunk;     // n_pb + 1: chunk range of each camera block
@@ -253,6 +252,7 @@ struct Work {
     double* lmd;             // 12 x n_lm : V*^-1 (9), g_p (3)
     double* partA;           // n_wave x kPartA
     double* partD;           // n_wave x kPartD
+    int* cnt;                // K6 arrival counter (fused LM decision)
     double* cpart;           // n_chunk x kBlockF chunk partials
     double* sys;             // n_pb * 36 + 12 n_free + 2
     double* dc;              // 6 n_free
@@ -274,6 +274,7 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[1][i] = Wk.pw_init[i];
     }
     if (i == 0) {
+        *Wk.cnt = 0;
         LmState s{};
         s.lambda = lambda0;
         s.nu = 2.0;
@@ -315,13 +316,14 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
     __shared__ double shv[10][64];   // V (6), g_p (3), cost of each slot
     __shared__ double shl[12][64];   // V*^-1 (9), g_p (3) at the landmark's first lane
     __shared__ double shc[2][64];    // landmark cost, singular flag at the first lane
+    const int w = blockIdx.x, lane = threadIdx.x;
+    const int s = 64 * w + lane;
+    const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
+    const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
     const LmState* st = Wk.st;
     if (st->done) return;
     STAMP(11);
-    const int w = blockIdx.x, lane = threadIdx.x;
-    const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
-    const int s = s0 + lane;
-    const bool act = s < s1;
+    const bool act = h1.y > 0;
     const int cur = st->cur;
     double V[6] = {0, 0, 0, 0, 0, 0}, gp[3] = {0, 0, 0}, W[18], U[21], gc[6], cost = 0.0;
 #pragma unroll
@@ -330,20 +332,16 @@ __global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr
     for (int i = 0; i < 21; ++i) U[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) gc[i] = 0.0;
-    int kf = 0, first = lane, nk = 1, l = 0;
-    bool fr = false;
+    const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
+    const bool fr = h1.x >= 0;
     if (act) {
-        kf = Pr.slot_kf[s];
-        l = Pr.slot_lm[s];
-        first = Pr.slot_first[s] - s0;
-        nk = Pr.slot_nk[s];
-        fr = Pr.free_idx[kf] >= 0;
         const Pose P = pose_from7(Wk.pose[cur] + 7 * kf);
         const double* pwp = Wk.pw[cur] + 3 * l;
         double p[3] = {pwp[0], pwp[1], pwp[2]};
-        for (int o = Pr.slot_obs[s]; o < Pr.slot_obs[s + 1]; ++o) {
+        for (int o = 0; o < h1.y; ++o) {
             double r[2], J[2][9];
-            linearize(p, P, G.TCB[Pr.obs_cam[o]].m, Pr.obs_uv + 2 * o, r, J, true);
+            const double uv[2] = {uvq[o].x, uvq[o].y};
+            linearize(p, P, G.TCB[(h1.z >> o) & 1].m, uv, r, J, true);
             double sq = r[0] * r[0] + r[1] * r[1], rho, wt;
             huber(sq, G.huber_delta, &rho, &wt);
             cost += 0.5 * rho;
@@ -1038,116 +1036,34 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     }  // blocked path
 }
 
-// ---------------------------------------------------------------------------------------
-// K6: one wave per landmark group: back-substitution, trial point, trial cost
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work Wk) {
-    __shared__ double sht[3][64];     // W_s^T dc_f per slot
-    __shared__ double shp[3][64];     // trial point at the landmark's first lane
-    __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
+// Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
+// owner rank), per-lane strided sums then a fixed-pairing wave reduction; every load is issued
+// before the state is read (the free-pose squares of both buffers; the current one is picked
+// afterwards).  Result on every lane.  Used by the fused K6 tail, K6r and K7 alike, so the
+// sharded and single-rank paths reduce in the same order.
+template <bool COHERENT = false>
+__device__ void trial_scalars_wave(const Geometry& G, const Prob& Pr, const Work& Wk, int include_poses,
+                                   double out[4]) {
     const LmState* st = Wk.st;
-    if (st->done || !st->solve_ok) return;
-    STAMP(20);
-    const int w = blockIdx.x, lane = threadIdx.x;
-    const int s0 = Pr.wave_slot[w], s1 = Pr.wave_slot[w + 1];
-    const int s = s0 + lane;
-    const bool act = s < s1;
-    const int cur = st->cur, m = G.n_lm;
-    int kf = 0, first = lane, nk = 1, l = 0;
-    double t3[3] = {0.0, 0.0, 0.0};
-    if (act) {
-        kf = Pr.slot_kf[s];
-        l = Pr.slot_lm[s];
-        first = Pr.slot_first[s] - s0;
-        nk = Pr.slot_nk[s];
-        const int f = Pr.free_idx[kf];
-        if (f >= 0) {
-            const double* d6 = Wk.dc + 6 * f;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double acc = 0.0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) acc += Wk.slotf[(size_t)s * kSlotF + SW + a * 3 + c] * d6[a];
-                t3[c] = acc;
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) sht[c][lane] = t3[c];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
-    __syncthreads();
-    if (act && lane == first) {
-        double rhs[3] = {-Wk.lmd[9 * m + l], -Wk.lmd[10 * m + l], -Wk.lmd[11 * m + l]};
-        for (int k = 0; k < nk; ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) rhs[c] -= sht[c][first + k];
-        const double* pc = Wk.pw[cur] + 3 * l;
-        double* pt = Wk.pw[1 - cur] + 3 * l;
-        double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const double dp = (Wk.lmd[(c * 3) * m + l] * rhs[0] + Wk.lmd[(c * 3 + 1) * m + l] * rhs[1]) +
-                              Wk.lmd[(c * 3 + 2) * m + l] * rhs[2];
-            const double p = pc[c];
-            const double q = p + dp;
-            shp[c][lane] = q;
-            pt[c] = q;
-            dp2 += dp * dp;
-            gpdp += Wk.lmd[(9 + c) * m + l] * dp;
-            p2 += p * p;
-        }
-        shs[1][lane] = dp2;
-        shs[2][lane] = gpdp;
-        shs[3][lane] = p2;
-    }
-    __syncthreads();
-    double cost = 0.0;
-    if (act) {
-        const Pose P = pose_from7(Wk.pose[1 - cur] + 7 * kf);
-        double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
-        for (int o = Pr.slot_obs[s]; o < Pr.slot_obs[s + 1]; ++o) {
-            double r[2], J[2][9];
-            linearize(q, P, G.TCB[Pr.obs_cam[o]].m, Pr.obs_uv + 2 * o, r, J, false);
-            double rho, wt;
-            huber(r[0] * r[0] + r[1] * r[1], G.huber_delta, &rho, &wt);
-            cost += 0.5 * rho;
-        }
-    }
-    shs[0][lane] = cost;
-    __syncthreads();
-    {  // wave partials: fixed-pairing butterflies over the lanes
-        double v[kPartD];
-#pragma unroll
-        for (int i = 0; i < kPartD; ++i) v[i] = wave_sum_det(shs[i][lane]);
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
-        }
-    }
-    STAMP(21);
-}
-
-// Trial scalars of this rank: the K6 wave partials (+ |x|^2 of the free poses on the owner
-// rank) summed in a fixed order: per-thread strided sums, a fixed-pairing butterfly inside
-// each wave, then the 4 wave sums in wave order.  Valid in thread 0.  Called by all 256 threads.
-__device__ void trial_scalars(const Geometry& G, const Prob& Pr, const Work& Wk, int include_poses, double out[4],
-                              double* sh) {
-    const LmState* st = Wk.st;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // every load is issued before the state is known (one round trip): the wave partials, and
-    // the free-pose squares of both state buffers (the current one is picked afterwards)
+    const int lane = threadIdx.x & 63;
     double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
     double sq[2] = {0.0, 0.0};
-    for (int i = tid; i < G.n_wave; i += 256) {
-        const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
-        acc[0] += v.x;
-        acc[1] += v.y;
-        acc[2] += v.z;
-        acc[3] += v.w;
+    for (int i = lane; i < G.n_wave; i += 64) {
+        if constexpr (COHERENT) {  // partials of this launch: device-coherent (sc1) loads
+#pragma unroll
+            for (int k = 0; k < kPartD; ++k)
+                acc[k] += __hip_atomic_load(Wk.partD + (size_t)i * kPartD + k, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
+            acc[0] += v.x;
+            acc[1] += v.y;
+            acc[2] += v.z;
+            acc[3] += v.w;
+        }
     }
     if (include_poses)
-        for (int e = tid; e < 7 * G.n_kf; e += 256) {
+        for (int e = lane; e < 7 * G.n_kf; e += 64) {
             const bool fr = Pr.free_idx[e / 7] >= 0;
             const double p0 = Wk.pose[0][e], p1 = Wk.pose[1][e];
             if (fr) {
@@ -1161,43 +1077,13 @@ __device__ void trial_scalars(const Geometry& G, const Prob& Pr, const Work& Wk,
         for (int k = 0; k < kPartD; ++k) acc[k] = 0.0;
     acc[3] += sq[cur];
 #pragma unroll
-    for (int k = 0; k < kPartD; ++k) {
-        const double w = wave_sum_det(acc[k]);
-        if (lane == 0) sh[wave * kPartD + k] = w;
-    }
-    __syncthreads();
-    if (tid == 0)
-        for (int k = 0; k < kPartD; ++k) out[k] = ((sh[k] + sh[kPartD + k]) + sh[2 * kPartD + k]) + sh[3 * kPartD + k];
+    for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
 }
 
-__global__ __launch_bounds__(256) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
-    __shared__ double sh[256];
-    if (Wk.st->done) return;
-    double v[4];
-    trial_scalars(G, Pr, Wk, include_poses, v, sh);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 4; ++k) Wk.trial4[k] = v[k];
-}
-
-// ---------------------------------------------------------------------------------------
-// K7: LM decision (build's LM).  pre_reduced: trial scalars come from trial4.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, int max_iter,
-                                                    double cost_tol, double param_tol) {
-    __shared__ double sh[256];
-    LmState* stp = Wk.st;
-    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
-    if (stp->done) return;
-    double tv[4];
-    STAMP(8);
-    if (pre_reduced) {
-        for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
-    } else {
-        trial_scalars(G, Pr, Wk, 1, tv, sh);
-    }
-    STAMP(9);
-    if (threadIdx.x != 0) return;
-    LmState s = *stp;
+// The build's LM decision for one iteration: cost = cost at the current
+// state, tv = trial cost, |dp|^2, g_p.dp, |x|^2.  Flips the state buffers on acceptance.
+__device__ void lm_update(LmState& s, double cost, const double tv[4], int max_iter, double cost_tol,
+                          double param_tol) {
     if (s.iter == 0) s.initial_cost = cost;
     s.cost = cost;
     s.iter += 1;
@@ -1251,7 +1137,160 @@ __global__ __launch_bounds__(256) void ba_lm_decide(Geometry G, Prob Pr, Work Wk
         s.status = RSVIO_LM_MAX_ITERATIONS;
         s.done = 1;
     }
+}
+
+// LM configuration passed to the kernels that decide
+struct LmArgs {
+    int max_iter;
+    double cost_tol, param_tol;
+};
+
+// Decision by one wave (lane 0 writes the state).  pre_reduced: the trial scalars come from
+// trial4 (all-reduced over ranks); else they are this rank's.
+template <bool COHERENT = false>
+__device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced, const LmArgs& la) {
+    LmState* stp = Wk.st;
+    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
+    double tv[4];
+    if (pre_reduced) {
+        for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
+    } else {
+        trial_scalars_wave<COHERENT>(G, Pr, Wk, 1, tv);
+    }
+    if ((threadIdx.x & 63) != 0) return;
+    LmState s = *stp;
+    lm_update(s, cost, tv, la.max_iter, la.cost_tol, la.param_tol);
     *stp = s;
+}
+
+// ---------------------------------------------------------------------------------------
+// K6: one wave per landmark group: back-substitution, trial point, trial cost
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work Wk, int fuse_decide, LmArgs la) {
+    __shared__ double sht[3][64];     // W_s^T dc_f per slot
+    __shared__ double shp[3][64];     // trial point at the landmark's first lane
+    __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
+    const int w = blockIdx.x, lane = threadIdx.x;
+    const int s = 64 * w + lane;
+    const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
+    const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    if (!st->solve_ok) {  // no step: the decision (lambda up) is all there is
+        if (fuse_decide && blockIdx.x == 0) lm_decide_wave(G, Pr, Wk, 0, la);
+        return;
+    }
+    STAMP(20);
+    const bool act = h1.y > 0;
+    const int cur = st->cur, m = G.n_lm;
+    const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
+    double t3[3] = {0.0, 0.0, 0.0};
+    if (act) {
+        const int f = h1.x;
+        if (f >= 0) {
+            const double* d6 = Wk.dc + 6 * f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0.0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) acc += Wk.slotf[(size_t)s * kSlotF + SW + a * 3 + c] * d6[a];
+                t3[c] = acc;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) sht[c][lane] = t3[c];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
+    __syncthreads();
+    if (act && lane == first) {
+        double rhs[3] = {-Wk.lmd[9 * m + l], -Wk.lmd[10 * m + l], -Wk.lmd[11 * m + l]};
+        for (int k = 0; k < nk; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) rhs[c] -= sht[c][first + k];
+        const double* pc = Wk.pw[cur] + 3 * l;
+        double* pt = Wk.pw[1 - cur] + 3 * l;
+        double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double dp = (Wk.lmd[(c * 3) * m + l] * rhs[0] + Wk.lmd[(c * 3 + 1) * m + l] * rhs[1]) +
+                              Wk.lmd[(c * 3 + 2) * m + l] * rhs[2];
+            const double p = pc[c];
+            const double q = p + dp;
+            shp[c][lane] = q;
+            pt[c] = q;
+            dp2 += dp * dp;
+            gpdp += Wk.lmd[(9 + c) * m + l] * dp;
+            p2 += p * p;
+        }
+        shs[1][lane] = dp2;
+        shs[2][lane] = gpdp;
+        shs[3][lane] = p2;
+    }
+    __syncthreads();
+    double cost = 0.0;
+    if (act) {
+        const Pose P = pose_from7(Wk.pose[1 - cur] + 7 * kf);
+        double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
+        for (int o = 0; o < h1.y; ++o) {
+            double r[2], J[2][9];
+            const double uv[2] = {uvq[o].x, uvq[o].y};
+            linearize(q, P, G.TCB[(h1.z >> o) & 1].m, uv, r, J, false);
+            double rho, wt;
+            huber(r[0] * r[0] + r[1] * r[1], G.huber_delta, &rho, &wt);
+            cost += 0.5 * rho;
+        }
+    }
+    shs[0][lane] = cost;
+    __syncthreads();
+    {  // wave partials: fixed-pairing butterflies over the lanes
+        double v[kPartD];
+#pragma unroll
+        for (int i = 0; i < kPartD; ++i) v[i] = wave_sum_det(shs[i][lane]);
+        if (lane == 0) {
+            if (fuse_decide) {  // device-coherent (sc1) stores: the last wave reads them below
+#pragma unroll
+                for (int i = 0; i < kPartD; ++i)
+                    __hip_atomic_store(Wk.partD + w * kPartD + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
+            }
+        }
+    }
+    STAMP(21);
+    if (fuse_decide) {
+        // K7 folded in: the partials go out with sc1 stores, drained before the arrival counter
+        // (no L2 write-back fence); the last wave to arrive reads them with sc1 loads and takes
+        // the LM decision
+        int last = 0;
+        if (lane == 0) {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int old = __hip_atomic_fetch_add(Wk.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = old == G.n_wave - 1;
+        }
+        last = __builtin_amdgcn_readfirstlane(last);
+        if (!last) return;
+        if (lane == 0) __hip_atomic_store(Wk.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lm_decide_wave<true>(G, Pr, Wk, 0, la);
+    }
+}
+
+__global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
+    if (Wk.st->done) return;
+    double v[4];
+    trial_scalars_wave(G, Pr, Wk, include_poses, v);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; ++k) Wk.trial4[k] = v[k];
+}
+
+// ---------------------------------------------------------------------------------------
+// K7: LM decision (sharded path, or no landmark wave to fold it into).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la) {
+    if (Wk.st->done) return;
+    STAMP(8);
+    lm_decide_wave(G, Pr, Wk, pre_reduced, la);
     STAMP(10);
 }
 
@@ -1268,11 +1307,12 @@ struct BundleAdjuster {
     bool has_problem = false;
     int iter_chunk = 2;       // LM iterations enqueued per status read-back after the first chunk
     int last_iterations = 3;  // first chunk = previous solve's iteration count
-    DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_uv;
-    DevBuf<uint8_t> d_cam;
-    DevBuf<int> d_free, d_slot_kf, d_slot_lm, d_slot_obs, d_slot_first, d_slot_nk, d_wave_slot, d_chunk_pb,
+    DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_slot_uv;
+    DevBuf<int> d_slot_hdr;
+    DevBuf<int> d_free, d_chunk_pb,
         d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb;
     DevBuf<double> d_slotf, d_lmd, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
+    DevBuf<int> d_cnt;
     DevBuf<LmState> d_state;
     HostBuf<LmState> h_state;
     ncclComm_t comm = nullptr;
@@ -1312,9 +1352,9 @@ struct BundleAdjuster {
 
     Prob prob() const {
         Prob p;
-        p.free_idx = d_free.p; p.slot_kf = d_slot_kf.p; p.slot_lm = d_slot_lm.p; p.slot_obs = d_slot_obs.p;
-        p.slot_first = d_slot_first.p; p.slot_nk = d_slot_nk.p; p.wave_slot = d_wave_slot.p;
-        p.obs_cam = d_cam.p; p.obs_uv = d_uv.p;
+        p.free_idx = d_free.p;
+        p.slot_hdr = reinterpret_cast<const int4*>(d_slot_hdr.p);
+        p.slot_uv = reinterpret_cast<const double2*>(d_slot_uv.p);
         p.chunk_pb = d_chunk_pb.p; p.chunk_pair = d_chunk_pair.p; p.pb_chunk = d_pb_chunk.p;
         p.pair_a = d_pair_a.p; p.pair_b = d_pair_b.p; p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
         return p;
@@ -1324,7 +1364,7 @@ struct BundleAdjuster {
         w.pose[0] = d_pose2.p; w.pose[1] = d_pose2.p + 7 * (size_t)G.n_kf;
         w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
         w.pose_init = d_pose_init.p; w.pw_init = d_pw_init.p;
-        w.slotf = d_slotf.p; w.lmd = d_lmd.p; w.partA = d_partA.p; w.partD = d_partD.p;
+        w.slotf = d_slotf.p; w.lmd = d_lmd.p; w.partA = d_partA.p; w.partD = d_partD.p; w.cnt = d_cnt.p;
         w.cpart = d_cpart.p;
         w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p; w.st = d_state.p;
         return w;
@@ -1384,6 +1424,33 @@ struct BundleAdjuster {
         }
         if (n_slot > wave_slot.back()) wave_slot.push_back(n_slot);
         const int n_wave = (int)wave_slot.size() - 1;
+        // padded slot layout (64 per wave) with inline headers and observations (Prob::slot_hdr)
+        std::vector<int> pslot(n_slot);
+        const size_t n_pad = (size_t)64 * n_wave;
+        std::vector<int> hdr(8 * n_pad, 0);
+        std::vector<double> huv(4 * n_pad, 0.0);
+        for (int w = 0; w < n_wave; ++w)
+            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
+                const int ps = 64 * w + (sl - wave_slot[w]);
+                pslot[sl] = ps;
+                const int no = slot_obs[sl + 1] - slot_obs[sl];
+                if (no > 2)
+                    throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
+                int* h = hdr.data() + 8 * (size_t)ps;
+                h[0] = slot_kf[sl];
+                h[1] = slot_lm[sl];
+                h[2] = slot_first[sl] - wave_slot[w];
+                h[3] = slot_nk[sl];
+                h[4] = free_idx[slot_kf[sl]];
+                h[5] = no;
+                for (int q = 0; q < no; ++q) {
+                    const int o = slot_obs[sl] + q;
+                    h[6] |= cam[o] << q;
+                    huv[4 * (size_t)ps + 2 * q] = uv[2 * o];
+                    huv[4 * (size_t)ps + 2 * q + 1] = uv[2 * o + 1];
+                }
+            }
+        for (size_t ps = 0; ps < n_pad; ++ps) hdr[8 * ps + 4] = hdr[8 * ps + 5] ? hdr[8 * ps + 4] : -1;
         // camera blocks (fa <= fb) and their slot pairs (ascending landmark)
         std::vector<int> pb_fa, pb_fb, pb_of((size_t)n_free * n_free, -1);
         for (int a = 0; a < n_free; ++a)
@@ -1415,11 +1482,11 @@ struct BundleAdjuster {
             }
             pb_chunk.push_back((int)chunk_pb.size());
             for (auto& pr : pairs[b]) {
-                pa.push_back(pr.first);
-                pbv.push_back(pr.second);
+                pa.push_back(pslot[pr.first]);
+                pbv.push_back(pslot[pr.second]);
             }
         }
-        G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = n_slot;
+        G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = (int)chunk_pb.size();
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
@@ -1427,15 +1494,9 @@ struct BundleAdjuster {
         up(d_pw_init, pW, 3 * (size_t)n_lm);
         grow(d_pose2, 14 * (size_t)n_kf);
         grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
-        up(d_uv, uv);
-        up(d_cam, cam);
         up(d_free, free_idx);
-        up(d_slot_kf, slot_kf);
-        up(d_slot_lm, slot_lm);
-        up(d_slot_obs, slot_obs);
-        up(d_slot_first, slot_first);
-        up(d_slot_nk, slot_nk);
-        up(d_wave_slot, wave_slot);
+        up(d_slot_hdr, hdr);
+        up(d_slot_uv, huv);
         up(d_chunk_pb, chunk_pb);
         up(d_chunk_pair, chunk_pair);
         up(d_pb_chunk, pb_chunk);
@@ -1444,13 +1505,14 @@ struct BundleAdjuster {
         up(d_pair_b, pbv);
         up(d_pb_fa, pb_fa);
         up(d_pb_fb, pb_fb);
-        grow(d_slotf, (size_t)kSlotF * std::max(n_slot, 1));
+        grow(d_slotf, (size_t)kSlotF * std::max<size_t>(n_pad, 1));
         grow(d_lmd, (size_t)12 * std::max(n_lm, 1));
         grow(d_partA, (size_t)kPartA * std::max(n_wave, 1));
         grow(d_partD, (size_t)kPartD * std::max(n_wave, 1));
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
+        grow(d_cnt, 1);
         grow(d_state, 1);
         enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
         RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
@@ -1500,13 +1562,16 @@ struct BundleAdjuster {
         const Work wk = work();
         enqueue_linear_system();
         launch_camera_solve(pr, wk);
-        if (G.n_wave) hipLaunchKernelGGL(ba_backsub_cost, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
+        const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
+        // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
+        const int fuse = (!comm && G.n_wave) ? 1 : 0;
+        if (G.n_wave) hipLaunchKernelGGL(ba_backsub_cost, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, fuse, la);
         if (comm) {
-            hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(256), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+            hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
             allreduce(d_trial4.p, 4);
         }
-        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(256), 0, stream, G, pr, wk, comm ? 1 : 0, cfg.max_iterations,
-                           cfg.cost_tolerance, cfg.parameter_tolerance);
+        if (!fuse)
+            hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, pr, wk, comm ? 1 : 0, la);
         RSVIO_HIP(hipGetLastError());
     }
 
