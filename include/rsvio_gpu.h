@@ -178,6 +178,11 @@ int rsvio_ba_set_problem(rsvio_ba* ba, int32_t n_kf, const double* pose7, const 
                          const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                          const double* T_C_B2);
 int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
+/* rsvio_ba_run split in two so the host can overlap other work (e.g. the next frame's
+ * tracking) with the solve: _run_async enqueues the first chunk of LM iterations and returns;
+ * _wait completes the solve and fills res.  One solve in flight per handle. */
+int rsvio_ba_run_async(rsvio_ba* ba, const rsvio_lm_cfg* cfg);
+int rsvio_ba_wait(rsvio_ba* ba, rsvio_ba_result* res);
 int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W);
 /* Reduced camera system at `lambda` for the uploaded state (parity tests):
  * S is n x n row-major (n = 6 * free keyframes, ascending keyframe order), b is n. */

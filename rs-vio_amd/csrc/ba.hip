@@ -1575,33 +1575,57 @@ struct BundleAdjuster {
         RSVIO_HIP(hipGetLastError());
     }
 
-    void run(const rsvio_lm_cfg& cfg, rsvio_ba_result* res) {
+    // Pipelined solve: start() enqueues the reset and the first chunk of LM iterations and
+    // returns; finish() waits, enqueues further chunks while the LM has not terminated, and
+    // fills the result.  run() = start() + finish().  The host reads the LM state once per
+    // chunk; the first chunk is the previous solve's iteration count (consecutive windows
+    // converge alike), so the common case costs one read-back and no iteration enqueued after
+    // convergence.
+    struct Pending {
+        bool active = false, skipped = false;
+        rsvio_lm_cfg cfg{};
+        int enq = 0, max_it = 0;
+    } pend;
+
+    void enqueue_chunk(int k) {
+        for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg);
+        pend.enq += k;
+        RSVIO_HIP(hipEventRecord(ev1, stream));
+        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+    }
+
+    void start(const rsvio_lm_cfg& cfg) {
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
+        if (pend.active) throw std::logic_error("a solve is already in flight (call finish first)");
         G.huber_delta = cfg.huber_delta;
-        res->iterations = 0;
+        pend = Pending{};
+        pend.active = true;
+        pend.cfg = cfg;
         // sliding_window.rs:303-319: too few residuals / underconstrained -> skipped (Ok(false))
         if (!comm && (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm)) {
+            pend.skipped = true;
+            return;
+        }
+        pend.max_it = std::max(cfg.max_iterations, 1);
+        RSVIO_HIP(hipEventRecord(ev0, stream));
+        enqueue_reset(cfg.lambda_init);
+        enqueue_chunk(std::min(std::max(last_iterations, 1), pend.max_it));
+    }
+
+    void finish(rsvio_ba_result* res) {
+        if (!pend.active) throw std::logic_error("no solve in flight");
+        pend.active = false;
+        res->iterations = 0;
+        if (pend.skipped) {
             res->status = RSVIO_LM_SKIPPED;
             res->initial_cost = res->final_cost = 0.0;
             res->solve_ms = 0.0;
             return;
         }
-        RSVIO_HIP(hipEventRecord(ev0, stream));
-        enqueue_reset(cfg.lambda_init);
-        const int max_it = std::max(cfg.max_iterations, 1);
-        // The host reads the LM state once per chunk of iterations.  The first chunk is the
-        // previous solve's iteration count (consecutive windows converge alike), so the common
-        // case costs one read-back and no iteration enqueued after convergence.
-        int enq = 0, k = std::min(std::max(last_iterations, 1), max_it);
-        while (enq < max_it) {
-            k = std::min(k, max_it - enq);
-            for (int i = 0; i < k; ++i) enqueue_iteration(cfg);
-            enq += k;
-            RSVIO_HIP(hipEventRecord(ev1, stream));
-            RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+        while (true) {
             RSVIO_HIP(hipStreamSynchronize(stream));
-            if (h_state.p->done) break;
-            k = iter_chunk;
+            if (h_state.p->done || pend.enq >= pend.max_it) break;
+            enqueue_chunk(std::min(iter_chunk, pend.max_it - pend.enq));
         }
         last_iterations = h_state.p->iter;
         float ms = 0.0f;
@@ -1612,6 +1636,11 @@ struct BundleAdjuster {
         res->initial_cost = s.initial_cost;
         res->final_cost = s.cost;
         res->solve_ms = ms;
+    }
+
+    void run(const rsvio_lm_cfg& cfg, rsvio_ba_result* res) {
+        start(cfg);
+        finish(res);
     }
 
     void get_state(double* pose7, double* pW) {
@@ -1701,6 +1730,22 @@ int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res) {
     if (!ba || !cfg || !res) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
         ba->b.run(*cfg, res);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_run_async(rsvio_ba* ba, const rsvio_lm_cfg* cfg) {
+    if (!ba || !cfg) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        ba->b.start(*cfg);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_wait(rsvio_ba* ba, rsvio_ba_result* res) {
+    if (!ba || !res) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        ba->b.finish(res);
         return (int)RSVIO_OK;
     });
 }

@@ -88,6 +88,8 @@ SIG = {
                                  C.POINTER(LmCfg), C.POINTER(BaResult)]),
     "rsvio_ba_set_problem": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, C.c_int32, P, P, P, P, P]),
     "rsvio_ba_run": (C.c_int, [P, C.POINTER(LmCfg), C.POINTER(BaResult)]),
+    "rsvio_ba_run_async": (C.c_int, [P, C.POINTER(LmCfg)]),
+    "rsvio_ba_wait": (C.c_int, [P, C.POINTER(BaResult)]),
     "rsvio_ba_get_state": (C.c_int, [P, P, P]),
     "rsvio_ba_build_system": (C.c_int, [P, C.c_double, C.c_double, P, P, C.POINTER(C.c_double)]),
     "rsvio_rccl_unique_id": (C.c_int, [P, C.c_size_t]),

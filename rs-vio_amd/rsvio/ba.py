@@ -79,6 +79,16 @@ class BundleAdjuster:
         check(_lib.load().rsvio_ba_run(self._h, C.byref(cfg or lm_cfg()), C.byref(res)))
         return res
 
+    def run_async(self, cfg=None) -> None:
+        """Enqueue the solve and return (rsvio_ba_run_async); wait() completes it."""
+        self._cfg = cfg or lm_cfg()  # kept alive until wait()
+        check(_lib.load().rsvio_ba_run_async(self._h, C.byref(self._cfg)))
+
+    def wait(self) -> _lib.BaResult:
+        res = _lib.BaResult()
+        check(_lib.load().rsvio_ba_wait(self._h, C.byref(res)))
+        return res
+
     def state(self):
         pose = np.zeros((self.n_kf, 7))
         pw = np.zeros((self.n_lm, 3))

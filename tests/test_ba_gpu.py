@@ -195,3 +195,18 @@ def test_sharded_code_path_single_rank(gpu, cfg3):
     assert np.array_equal(pa, pb) and np.array_equal(wa, wb)
     a.close()
     b.close()
+
+
+def test_async_solve_equals_run(gpu, cfg3):
+    """rsvio_ba_run_async + rsvio_ba_wait is the same solve as rsvio_ba_run."""
+    a = _adjuster(gpu, cfg3)
+    ra = a.run()
+    pa, wa = a.state()
+    a.run_async()
+    rb = a.wait()
+    pb, wb = a.state()
+    assert (ra.status, ra.iterations, ra.final_cost) == (rb.status, rb.iterations, rb.final_cost)
+    assert np.array_equal(pa, pb) and np.array_equal(wa, wb)
+    with pytest.raises(Exception):
+        a.wait()  # nothing in flight
+    a.close()
