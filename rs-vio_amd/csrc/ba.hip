@@ -8,21 +8,25 @@
 // Layout (landmark-major, built once per problem on the host):
 //   obs   sorted by (landmark, keyframe, camera)
 //   slot  = (landmark, keyframe) group of 1-2 observations, sorted like obs
-//   wave  = a run of whole landmarks with <= 64 slots: one lane per slot
+//   wave  = a run of whole landmarks with <= 64 slots: one lane per slot (padded to 64 per wave)
 //   chunk = <= 64 (slot_a, slot_b) pairs of one upper-triangular 6x6 camera block (fa <= fb)
-// Per LM iteration (one HIP stream; the host reads the LM state once per chunk of iterations):
-//   K4  ba_linearize_eliminate  wave / landmark group: residual + Jacobian + Huber per slot,
-//                               V, g_p summed over the landmark's lanes, (V + lambda I)^-1,
-//                               Y = W V^-1, Y g_p -- per-slot Schur factors to HBM
-//   K4c ba_schur_chunks         wave / 64 pairs: -Y_a W_b^T (+ U on the diagonal), lane-ordered chunk sums
-//   K4d ba_schur_combine        wave / camera block: chunk partials in chunk order -> S, b, g_c; cost
+// A linearisation (lambda-independent) of a state is stored per slot -- W, U, g_c -- and per
+// landmark -- V, g_p -- in the raw buffers of that state (double-buffered like the state).
+// Per solve: K0 ba_reset, K4 ba_linearize (the initial state), then per LM iteration (one HIP
+// stream; the host reads the LM state once per chunk of iterations):
+//   K4c ba_schur_chunks         wave / 64 pairs: (V + lambda I)^-1, Y = W V^-1 on the fly,
+//                               -Y_a W_b^T (+ U, Y g_p - g_c on the diagonal), lane-ordered sums
+//   K4d ba_schur_combine        wave / camera block: chunk partials in chunk order -> S, b, g_c
 //   [RCCL all-reduce of the per-rank reduced system when sharded]
 //   K5  ba_camera_solve         1 workgroup: S, b in LDS; pipelined 4-wave LDL^T (n <= 60) or
 //                               blocked Cholesky; substitutions, SE3 (+) trial poses
-//   K6  ba_backsub_cost         wave / landmark group: dp = V^-1 (-g_p - W^T dc), trial point,
-//                               trial cost
-//   [RCCL all-reduce of 4 trial scalars when sharded]
-//   K7  ba_lm_decide            gain ratio, accept / reject (buffer flip), lambda, termination
+//   K6  ba_backsub_relinearize  wave / landmark group: dp = V^-1 (-g_p - W^T dc), trial point,
+//                               and the speculative linearisation of the trial state (residual,
+//                               Jacobian, Huber) into the other raw buffers -- its cost is the
+//                               trial cost; an accepted step needs no further linearisation
+//   [sharded: K6r per-rank trial scalars + RCCL all-reduce, K7 ba_lm_decide]
+//   single rank: the last K6 wave to arrive takes the LM decision (gain ratio, accept / reject
+//   = buffer flip, lambda, termination)
 // Every reduction has a fixed order (no floating-point atomics): results are run-to-run identical.
 #include <rccl/rccl.h>
 
@@ -43,10 +47,12 @@ RSVIO_DBG_DECL
 constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
 constexpr int kMaxN = 6 * kMaxFree;
 constexpr int kLdA = kMaxN + 1;         // odd stride
-// per-slot Schur factors, one contiguous 576-B record per slot (AoS): Y, W, U (packed), b, g_c
-enum { SY = 0, SW = 18, SU = 36, SB = 57, SG = 63, kSlotF = 72 };
+// raw linearisation per slot, one contiguous 384-B record (AoS): W (6x3), U (6x6 packed upper),
+// g_c (6), pad; and per landmark (96 B): V (3x3 packed upper), g_p (3), pad
+enum { RW = 0, RU = 18, RG = 39, kRawF = 48 };
+enum { LV = 0, LG = 6, kLmF = 12 };
 constexpr int kBlockF = 48;             // 36 S + 6 b + 6 g_c per camera block workgroup
-constexpr int kPartA = 2;               // cost, singular-landmark count per wave
+constexpr int kPartA = 2;               // cost of the initial linearisation, 0 (per wave)
 constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per wave
 
 struct Mat4 {
@@ -239,6 +245,7 @@ struct Prob {
     const int* pb_chunk;     // n_pb + 1: chunk range of each camera block
     const int* pair_a;
     const int* pair_b;
+    const int* pair_l;       // landmark of each pair
     const int* pb_fa;
     const int* pb_fb;
 };
@@ -248,8 +255,9 @@ struct Work {
     double* pw[2];           // n_lm x 3
     const double* pose_init;
     const double* pw_init;
-    double* slotf;           // n_slot x kSlotF
-    double* lmd;             // 12 x n_lm : V*^-1 (9), g_p (3)
+    double* raws[2];         // n_slot x kRawF per state buffer
+    double* rawl[2];         // n_lm x kLmF per state buffer
+    int* singular;           // set by K4c when a landmark block (V + lambda I) is singular
     double* partA;           // n_wave x kPartA
     double* partD;           // n_wave x kPartD
     int* cnt;                // K6 arrival counter (fused LM decision)
@@ -275,6 +283,7 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
     }
     if (i == 0) {
         *Wk.cnt = 0;
+        *Wk.singular = 0;
         LmState s{};
         s.lambda = lambda0;
         s.nu = 2.0;
@@ -310,147 +319,143 @@ __device__ __forceinline__ double wave_sum_det(double v) {
 }
 
 // ---------------------------------------------------------------------------------------
-// K4: one wave per landmark group, one lane per (landmark, keyframe) slot
+// Linearisation of one slot (lane) and of the wave's landmarks, shared by K4 (initial state)
+// and K6 (the trial state): factors.rs:350-447 residual + 2x9 Jacobian per observation,
+// Huber IRLS weight, and the slot's contributions V, g_p (landmark block), W, U, g_c
+// (camera blocks, free keyframes only), cost.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_linearize_eliminate(Geometry G, Prob Pr, Work Wk) {
-    __shared__ double shv[10][64];   // V (6), g_p (3), cost of each slot
-    __shared__ double shl[12][64];   // V*^-1 (9), g_p (3) at the landmark's first lane
-    __shared__ double shc[2][64];    // landmark cost, singular flag at the first lane
+struct SlotLin {
+    double V[6], gp[3], W[18], U[21], gc[6], cost;
+};
+
+__device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P, const double p[3], int nobs,
+                                               int cams, const double2 (&uvq)[2], bool fr, SlotLin& L) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) L.V[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) L.gp[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 18; ++i) L.W[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 21; ++i) L.U[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) L.gc[i] = 0.0;
+    L.cost = 0.0;
+    for (int o = 0; o < nobs; ++o) {
+        double r[2], J[2][9];
+        const double uv[2] = {uvq[o].x, uvq[o].y};
+        linearize(p, P, G.TCB[(cams >> o) & 1].m, uv, r, J, true);
+        double sq = r[0] * r[0] + r[1] * r[1], rho, wt;
+        huber(sq, G.huber_delta, &rho, &wt);
+        L.cost += 0.5 * rho;
+        const double wr0 = wt * r[0], wr1 = wt * r[1];
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+            for (int c = a; c < 3; ++c) L.V[k++] += wt * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
+            L.gp[a] += J[0][a] * wr0 + J[1][a] * wr1;
+        }
+        if (fr) {
+            int u = 0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) L.W[a * 3 + c] += wt * (J[0][3 + a] * J[0][c] + J[1][3 + a] * J[1][c]);
+#pragma unroll
+                for (int c = a; c < 6; ++c) L.U[u++] += wt * (J[0][3 + a] * J[0][3 + c] + J[1][3 + a] * J[1][3 + c]);
+                L.gc[a] += J[0][3 + a] * wr0 + J[1][3 + a] * wr1;
+            }
+        }
+    }
+}
+
+// Store one wave's linearisation into raw buffer `buf`: the slot records (free keyframes), then
+// the landmark sums V, g_p in slot order by each landmark's first lane.  Called by the whole
+// wave (contains barriers); sh is a [10][64] LDS scratch.
+__device__ void store_linearization(const Work& Wk, int buf, int s, int lane, bool act, bool fr, int first, int nk,
+                                    int l, const SlotLin& L, double (*sh)[64]) {
+    if (act && fr) {
+        double rec[kRawF];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) rec[RW + i] = L.W[i];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) rec[RU + i] = L.U[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) rec[RG + i] = L.gc[i];
+        rec[45] = rec[46] = rec[47] = 0.0;
+        double2* dst = reinterpret_cast<double2*>(Wk.raws[buf] + (size_t)s * kRawF);
+#pragma unroll
+        for (int i = 0; i < kRawF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sh[i][lane] = L.V[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sh[6 + i][lane] = L.gp[i];
+    __syncthreads();
+    if (act && lane == first) {  // landmark sums in slot order
+        double Vl[6] = {0, 0, 0, 0, 0, 0}, gl[3] = {0, 0, 0};
+        for (int k = 0; k < nk; ++k) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) Vl[i] += sh[i][first + k];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) gl[i] += sh[6 + i][first + k];
+        }
+        double rec[kLmF] = {Vl[0], Vl[1], Vl[2], Vl[3], Vl[4], Vl[5], gl[0], gl[1], gl[2], 0.0, 0.0, 0.0};
+        double2* dst = reinterpret_cast<double2*>(Wk.rawl[buf] + (size_t)l * kLmF);
+#pragma unroll
+        for (int i = 0; i < kLmF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+    }
+}
+
+// (V + lambda I)^-1 of a landmark from its raw record; the same f64 operations wherever it is
+// needed (K4c lanes, K6 first lanes), so every user sees identical bits.  false if singular
+// (then Vi = 0).
+__device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda, double Vi[3][3]) {
+    double A[3][3] = {{Vp[0] + lambda, Vp[1], Vp[2]}, {Vp[1], Vp[3] + lambda, Vp[4]}, {Vp[2], Vp[4], Vp[5] + lambda}};
+    const bool ok = inv3(A, Vi);
+    if (!ok)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Vi[a][c] = 0.0;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------------------
+// K4: linearisation of the initial state (buffer 0) -- one wave per landmark group, one lane
+// per (landmark, keyframe) slot.  Its cost partials (partA) give the initial cost.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk) {
+    __shared__ double sh[10][64];
     const int w = blockIdx.x, lane = threadIdx.x;
     const int s = 64 * w + lane;
     const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
     const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
-    const LmState* st = Wk.st;
-    if (st->done) return;
     STAMP(11);
     const bool act = h1.y > 0;
-    const int cur = st->cur;
-    double V[6] = {0, 0, 0, 0, 0, 0}, gp[3] = {0, 0, 0}, W[18], U[21], gc[6], cost = 0.0;
-#pragma unroll
-    for (int i = 0; i < 18; ++i) W[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < 21; ++i) U[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) gc[i] = 0.0;
     const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
     const bool fr = h1.x >= 0;
+    SlotLin L;
     if (act) {
-        const Pose P = pose_from7(Wk.pose[cur] + 7 * kf);
-        const double* pwp = Wk.pw[cur] + 3 * l;
-        double p[3] = {pwp[0], pwp[1], pwp[2]};
-        for (int o = 0; o < h1.y; ++o) {
-            double r[2], J[2][9];
-            const double uv[2] = {uvq[o].x, uvq[o].y};
-            linearize(p, P, G.TCB[(h1.z >> o) & 1].m, uv, r, J, true);
-            double sq = r[0] * r[0] + r[1] * r[1], rho, wt;
-            huber(sq, G.huber_delta, &rho, &wt);
-            cost += 0.5 * rho;
-            const double wr0 = wt * r[0], wr1 = wt * r[1];
-            int k = 0;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                for (int c = a; c < 3; ++c) V[k++] += wt * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
-                gp[a] += J[0][a] * wr0 + J[1][a] * wr1;
-            }
-            if (fr) {
-                int u = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) W[a * 3 + c] += wt * (J[0][3 + a] * J[0][c] + J[1][3 + a] * J[1][c]);
-#pragma unroll
-                    for (int c = a; c < 6; ++c) U[u++] += wt * (J[0][3 + a] * J[0][3 + c] + J[1][3 + a] * J[1][3 + c]);
-                    gc[a] += J[0][3 + a] * wr0 + J[1][3 + a] * wr1;
-                }
-            }
-        }
+        const Pose P = pose_from7(Wk.pose[0] + 7 * kf);
+        const double* pwp = Wk.pw[0] + 3 * l;
+        const double p[3] = {pwp[0], pwp[1], pwp[2]};
+        slot_linearize(G, P, p, h1.y, h1.z, uvq, fr, L);
+    } else {
+        const Pose P{};
+        const double p[3] = {0.0, 0.0, 1.0};
+        slot_linearize(G, P, p, 0, 0, uvq, false, L);
     }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) shv[i][lane] = V[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) shv[6 + i][lane] = gp[i];
-    shv[9][lane] = cost;
-    shc[0][lane] = 0.0;
-    shc[1][lane] = 0.0;
-    __syncthreads();
     STAMP(12);
-    if (act && lane == first) {  // landmark-level sums in slot order, then the 3x3 elimination
-        double Vl[6] = {0, 0, 0, 0, 0, 0}, gl[3] = {0, 0, 0}, cl = 0.0;
-        for (int k = 0; k < nk; ++k) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) Vl[i] += shv[i][first + k];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] += shv[6 + i][first + k];
-            cl += shv[9][first + k];
-        }
-        const double lambda = st->lambda;
-        double A[3][3] = {{Vl[0] + lambda, Vl[1], Vl[2]}, {Vl[1], Vl[3] + lambda, Vl[4]}, {Vl[2], Vl[4], Vl[5] + lambda}};
-        double Vi[3][3];
-        const bool ok = inv3(A, Vi);
-        if (!ok)
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) Vi[a][c] = 0.0;
-        const int m = G.n_lm;
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                shl[a * 3 + c][lane] = Vi[a][c];
-                Wk.lmd[(a * 3 + c) * m + l] = Vi[a][c];
-            }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            shl[9 + a][lane] = gl[a];
-            Wk.lmd[(9 + a) * m + l] = gl[a];
-        }
-        shc[0][lane] = cl;
-        shc[1][lane] = ok ? 0.0 : 1.0;
-    }
-    __syncthreads();
-    STAMP(13);
-    if (act && fr) {
-        double Vi[9], g3[3];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Vi[i] = shl[i][first];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) g3[i] = shl[9 + i][first];
-        double rec[kSlotF];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            double y[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) y[c] = (W[a * 3] * Vi[c] + W[a * 3 + 1] * Vi[3 + c]) + W[a * 3 + 2] * Vi[6 + c];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                rec[SY + a * 3 + c] = y[c];
-                rec[SW + a * 3 + c] = W[a * 3 + c];
-            }
-            const double yg = (y[0] * g3[0] + y[1] * g3[1]) + y[2] * g3[2];
-            rec[SB + a] = yg - gc[a];  // b = -g_c + sum Y g_p
-            rec[SG + a] = gc[a];
-        }
-#pragma unroll
-        for (int i = 0; i < 21; ++i) rec[SU + i] = U[i];
-        rec[69] = rec[70] = rec[71] = 0.0;
-        double2* dst = reinterpret_cast<double2*>(Wk.slotf + (size_t)s * kSlotF);
-#pragma unroll
-        for (int i = 0; i < kSlotF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
-    }
-    {  // wave partials: fixed-pairing butterflies over the lanes (first lanes hold the values)
-        const double c = wave_sum_det(shc[0][lane]);
-        const double b = wave_sum_det(shc[1][lane]);
-        if (lane == 0) {
-            Wk.partA[w * kPartA] = c;
-            Wk.partA[w * kPartA + 1] = b;
-        }
+    store_linearization(Wk, 0, s, lane, act, fr, first, nk, l, L, sh);
+    const double c = wave_sum_det(L.cost);
+    if (lane == 0) {
+        Wk.partA[w * kPartA] = c;
+        Wk.partA[w * kPartA + 1] = 0.0;
     }
     STAMP(14);
 }
-
-
 
 // Deterministic sum of n values in global memory: thread t adds elements t, t + T, t + 2T, ...
 // (independent loads, all in flight), then thread 0 adds the T per-thread sums in thread order.
@@ -479,40 +484,62 @@ __device__ double block_ordered_sum(const double* __restrict__ v, int n, int str
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk) {
     __shared__ double sh[kBlockF * 65];
-    if (Wk.st->done) return;
-    STAMP(16);
     const int c = blockIdx.x, lane = threadIdx.x;
     const int pb = Pr.chunk_pb[c];
     const bool diag = Pr.pb_fa[pb] == Pr.pb_fb[pb];
     const int p0 = Pr.chunk_pair[c], np = Pr.chunk_pair[c + 1] - p0;
-    const double* sf = Wk.slotf;
+    const bool act = lane < np;
+    int sa = 0, sb = 0, l = 0;
+    if (act) {
+        const int p = p0 + lane;
+        sa = Pr.pair_a[p];
+        sb = Pr.pair_b[p];
+        l = Pr.pair_l[p];
+    }
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    STAMP(16);
+    const int cur = st->cur;
+    const double lambda = st->lambda;
     double acc[36], bg[12];
 #pragma unroll
     for (int i = 0; i < 36; ++i) acc[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < 12; ++i) bg[i] = 0.0;
-    if (lane < np) {
-        const int p = p0 + lane;
-        const int sa = Pr.pair_a[p], sb = Pr.pair_b[p];
-        const double2* ra = reinterpret_cast<const double2*>(sf + (size_t)sa * kSlotF);
-        const double2* rb = reinterpret_cast<const double2*>(sf + (size_t)sb * kSlotF);
-        double Ya[18], Wb[18];
+    if (act) {
+        const double2* ra = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sa * kRawF);
+        const double2* rb = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sb * kRawF);
+        const double2* rl = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)l * kLmF);
+        double Wa[18], Wb[18], Lm[10];
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const double2 y = ra[SY / 2 + i], w = rb[SW / 2 + i];
-            Ya[2 * i] = y.x; Ya[2 * i + 1] = y.y;
-            Wb[2 * i] = w.x; Wb[2 * i + 1] = w.y;
+            const double2 x = ra[RW / 2 + i], y = rb[RW / 2 + i];
+            Wa[2 * i] = x.x; Wa[2 * i + 1] = x.y;
+            Wb[2 * i] = y.x; Wb[2 * i + 1] = y.y;
         }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double2 x = rl[i];
+            Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
+        }
+        double Vi[3][3];
+        if (!landmark_inverse(Lm + LV, lambda, Vi)) *Wk.singular = 1;
+        double Ya[18];  // Y_a = W_a (V + lambda I)^-1
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                Ya[a * 3 + k] = (Wa[a * 3] * Vi[0][k] + Wa[a * 3 + 1] * Vi[1][k]) + Wa[a * 3 + 2] * Vi[2][k];
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
             for (int k = 0; k < 6; ++k)
                 acc[a * 6 + k] = -((Ya[a * 3] * Wb[k * 3] + Ya[a * 3 + 1] * Wb[k * 3 + 1]) + Ya[a * 3 + 2] * Wb[k * 3 + 2]);
         if (diag) {
-            double r[34];  // record entries 36..69: U (21), b (6), g_c (6), pad
+            double r[28];  // record entries 18..45: U (21), g_c (6), pad
 #pragma unroll
-            for (int i = 0; i < 17; ++i) {
-                const double2 v = ra[SU / 2 + i];
+            for (int i = 0; i < 14; ++i) {
+                const double2 v = ra[RU / 2 + i];
                 r[2 * i] = v.x; r[2 * i + 1] = v.y;
             }
             int u = 0;
@@ -526,8 +553,10 @@ __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work 
                 }
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-                bg[a] = r[SB - SU + a];
-                bg[6 + a] = r[SG - SU + a];
+                const double gca = r[RG - RU + a];
+                const double yg = (Ya[a * 3] * Lm[LG] + Ya[a * 3 + 1] * Lm[LG + 1]) + Ya[a * 3 + 2] * Lm[LG + 2];
+                bg[a] = yg - gca;  // b = -g_c + sum Y g_p
+                bg[6 + a] = gca;
             }
         }
     }
@@ -548,21 +577,18 @@ __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work 
     STAMP(18);
 }
 
-// Cost and singular-landmark count of this rank from the K4 wave partials (one wave, fixed
-// order); written to sys[SC0], sys[SC0 + 1].  Returns the singular count on every lane.
-__device__ double cost_partials(const Geometry& G, const Work& Wk, int lane, int SC0) {
-    double c = 0.0, b = 0.0;
-    for (int w = lane; w < G.n_wave; w += 64) {
-        c += Wk.partA[w * kPartA];
-        b += Wk.partA[w * kPartA + 1];
-    }
+// Cost of the initial linearisation of this rank (K4 wave partials, one wave, fixed order) and
+// the singular-landmark flag of this iteration's K4c (consumed and cleared here): written to
+// sys[SC0], sys[SC0 + 1].
+__device__ void cost_partials(const Geometry& G, const Work& Wk, int lane, int SC0) {
+    double c = 0.0;
+    for (int w = lane; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
     c = wave_sum_det(c);
-    b = wave_sum_det(b);
     if (lane == 0) {
         Wk.sys[SC0] = c;
-        Wk.sys[SC0 + 1] = b;
+        Wk.sys[SC0 + 1] = *Wk.singular ? 1.0 : 0.0;
+        *Wk.singular = 0;
     }
-    return b;
 }
 
 // Entry k (< 48) of camera block pb: its chunk partials in chunk order (+ lambda on the
@@ -1150,7 +1176,7 @@ struct LmArgs {
 template <bool COHERENT = false>
 __device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced, const LmArgs& la) {
     LmState* stp = Wk.st;
-    const double cost = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost at the current state
+    const double cost0 = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost of the initial state
     double tv[4];
     if (pre_reduced) {
         for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
@@ -1159,15 +1185,22 @@ __device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk
     }
     if ((threadIdx.x & 63) != 0) return;
     LmState s = *stp;
+    // cost at the current state: the initial linearisation's at the first iteration, then the
+    // cost of the last accepted trial state (K6 evaluated it while linearising it)
+    const double cost = s.iter == 0 ? cost0 : s.cost;
     lm_update(s, cost, tv, la.max_iter, la.cost_tol, la.param_tol);
     *stp = s;
 }
 
 // ---------------------------------------------------------------------------------------
-// K6: one wave per landmark group: back-substitution, trial point, trial cost
+// K6: one wave per landmark group: back-substitution dp = V^-1 (-g_p - W^T dc), the trial
+// point, and the linearisation of the trial state into the other raw buffers (its cost is
+// the trial cost).  Accepted: the next iteration starts from that linearisation; rejected:
+// from the current one, untouched.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work Wk, int fuse_decide, LmArgs la) {
-    __shared__ double sht[3][64];     // W_s^T dc_f per slot
+__global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr, Work Wk, int fuse_decide,
+                                                             LmArgs la) {
+    __shared__ double sh[10][64];     // W_s^T dc_f per slot; then the linearisation scratch
     __shared__ double shp[3][64];     // trial point at the landmark's first lane
     __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int w = blockIdx.x, lane = threadIdx.x;
@@ -1182,45 +1215,46 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
     }
     STAMP(20);
     const bool act = h1.y > 0;
-    const int cur = st->cur, m = G.n_lm;
+    const int cur = st->cur;
     const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
+    const bool fr = h1.x >= 0;
     double t3[3] = {0.0, 0.0, 0.0};
-    if (act) {
-        const int f = h1.x;
-        if (f >= 0) {
-            const double* d6 = Wk.dc + 6 * f;
+    if (act && fr) {
+        const double* d6 = Wk.dc + 6 * h1.x;
+        const double* Wr = Wk.raws[cur] + (size_t)s * kRawF + RW;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double acc = 0.0;
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0.0;
 #pragma unroll
-                for (int a = 0; a < 6; ++a) acc += Wk.slotf[(size_t)s * kSlotF + SW + a * 3 + c] * d6[a];
-                t3[c] = acc;
-            }
+            for (int a = 0; a < 6; ++a) acc += Wr[a * 3 + c] * d6[a];
+            t3[c] = acc;
         }
     }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) sht[c][lane] = t3[c];
+    for (int c = 0; c < 3; ++c) sh[c][lane] = t3[c];
 #pragma unroll
     for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
     __syncthreads();
     if (act && lane == first) {
-        double rhs[3] = {-Wk.lmd[9 * m + l], -Wk.lmd[10 * m + l], -Wk.lmd[11 * m + l]};
+        const double* Lm = Wk.rawl[cur] + (size_t)l * kLmF;
+        double Vi[3][3];
+        landmark_inverse(Lm + LV, st->lambda, Vi);
+        double rhs[3] = {-Lm[LG], -Lm[LG + 1], -Lm[LG + 2]};
         for (int k = 0; k < nk; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) rhs[c] -= sht[c][first + k];
+            for (int c = 0; c < 3; ++c) rhs[c] -= sh[c][first + k];
         const double* pc = Wk.pw[cur] + 3 * l;
         double* pt = Wk.pw[1 - cur] + 3 * l;
         double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double dp = (Wk.lmd[(c * 3) * m + l] * rhs[0] + Wk.lmd[(c * 3 + 1) * m + l] * rhs[1]) +
-                              Wk.lmd[(c * 3 + 2) * m + l] * rhs[2];
+            const double dp = (Vi[c][0] * rhs[0] + Vi[c][1] * rhs[1]) + Vi[c][2] * rhs[2];
             const double p = pc[c];
             const double q = p + dp;
             shp[c][lane] = q;
             pt[c] = q;
             dp2 += dp * dp;
-            gpdp += Wk.lmd[(9 + c) * m + l] * dp;
+            gpdp += Lm[LG + c] * dp;
             p2 += p * p;
         }
         shs[1][lane] = dp2;
@@ -1228,21 +1262,20 @@ __global__ __launch_bounds__(64) void ba_backsub_cost(Geometry G, Prob Pr, Work 
         shs[3][lane] = p2;
     }
     __syncthreads();
-    double cost = 0.0;
+    // linearisation of the trial state
+    SlotLin L;
     if (act) {
         const Pose P = pose_from7(Wk.pose[1 - cur] + 7 * kf);
-        double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
-        for (int o = 0; o < h1.y; ++o) {
-            double r[2], J[2][9];
-            const double uv[2] = {uvq[o].x, uvq[o].y};
-            linearize(q, P, G.TCB[(h1.z >> o) & 1].m, uv, r, J, false);
-            double rho, wt;
-            huber(r[0] * r[0] + r[1] * r[1], G.huber_delta, &rho, &wt);
-            cost += 0.5 * rho;
-        }
+        const double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
+        slot_linearize(G, P, q, h1.y, h1.z, uvq, fr, L);
+    } else {
+        const Pose P{};
+        const double q[3] = {0.0, 0.0, 1.0};
+        slot_linearize(G, P, q, 0, 0, uvq, false, L);
     }
-    shs[0][lane] = cost;
-    __syncthreads();
+    shs[0][lane] = L.cost;
+    __syncthreads();  // sh is reused below
+    store_linearization(Wk, 1 - cur, s, lane, act, fr, first, nk, l, L, sh);
     {  // wave partials: fixed-pairing butterflies over the lanes
         double v[kPartD];
 #pragma unroll
@@ -1311,7 +1344,9 @@ struct BundleAdjuster {
     DevBuf<int> d_slot_hdr;
     DevBuf<int> d_free, d_chunk_pb,
         d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb;
-    DevBuf<double> d_slotf, d_lmd, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
+    DevBuf<double> d_raws, d_rawl, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
+    DevBuf<int> d_pair_l, d_singular;
+    size_t n_pad = 0;
     DevBuf<int> d_cnt;
     DevBuf<LmState> d_state;
     HostBuf<LmState> h_state;
@@ -1356,7 +1391,7 @@ struct BundleAdjuster {
         p.slot_hdr = reinterpret_cast<const int4*>(d_slot_hdr.p);
         p.slot_uv = reinterpret_cast<const double2*>(d_slot_uv.p);
         p.chunk_pb = d_chunk_pb.p; p.chunk_pair = d_chunk_pair.p; p.pb_chunk = d_pb_chunk.p;
-        p.pair_a = d_pair_a.p; p.pair_b = d_pair_b.p; p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
+        p.pair_a = d_pair_a.p; p.pair_b = d_pair_b.p; p.pair_l = d_pair_l.p; p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
         return p;
     }
     Work work() const {
@@ -1364,7 +1399,10 @@ struct BundleAdjuster {
         w.pose[0] = d_pose2.p; w.pose[1] = d_pose2.p + 7 * (size_t)G.n_kf;
         w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
         w.pose_init = d_pose_init.p; w.pw_init = d_pw_init.p;
-        w.slotf = d_slotf.p; w.lmd = d_lmd.p; w.partA = d_partA.p; w.partD = d_partD.p; w.cnt = d_cnt.p;
+        w.raws[0] = d_raws.p; w.raws[1] = d_raws.p + (size_t)kRawF * std::max<size_t>(n_pad, 1);
+        w.rawl[0] = d_rawl.p; w.rawl[1] = d_rawl.p + (size_t)kLmF * std::max(G.n_lm, 1);
+        w.singular = d_singular.p;
+        w.partA = d_partA.p; w.partD = d_partD.p; w.cnt = d_cnt.p;
         w.cpart = d_cpart.p;
         w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p; w.st = d_state.p;
         return w;
@@ -1426,7 +1464,7 @@ struct BundleAdjuster {
         const int n_wave = (int)wave_slot.size() - 1;
         // padded slot layout (64 per wave) with inline headers and observations (Prob::slot_hdr)
         std::vector<int> pslot(n_slot);
-        const size_t n_pad = (size_t)64 * n_wave;
+        n_pad = (size_t)64 * n_wave;
         std::vector<int> hdr(8 * n_pad, 0);
         std::vector<double> huv(4 * n_pad, 0.0);
         for (int w = 0; w < n_wave; ++w)
@@ -1473,7 +1511,7 @@ struct BundleAdjuster {
             }
         // chunks of <= 64 pairs; a block with no pair still gets one (empty) chunk so that its
         // entries are written
-        std::vector<int> pa, pbv, chunk_pb, chunk_pair{0}, pb_chunk{0};
+        std::vector<int> pa, pbv, pl, chunk_pb, chunk_pair{0}, pb_chunk{0};
         for (int b = 0; b < n_pb; ++b) {
             const int np = (int)pairs[b].size();
             for (int c0 = 0; c0 < std::max(np, 1); c0 += 64) {
@@ -1484,6 +1522,7 @@ struct BundleAdjuster {
             for (auto& pr : pairs[b]) {
                 pa.push_back(pslot[pr.first]);
                 pbv.push_back(pslot[pr.second]);
+                pl.push_back(slot_lm[pr.first]);
             }
         }
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
@@ -1503,10 +1542,12 @@ struct BundleAdjuster {
         grow(d_cpart, (size_t)kBlockF * G.n_chunk);
         up(d_pair_a, pa);
         up(d_pair_b, pbv);
+        up(d_pair_l, pl);
         up(d_pb_fa, pb_fa);
         up(d_pb_fb, pb_fb);
-        grow(d_slotf, (size_t)kSlotF * std::max<size_t>(n_pad, 1));
-        grow(d_lmd, (size_t)12 * std::max(n_lm, 1));
+        grow(d_raws, (size_t)2 * kRawF * std::max<size_t>(n_pad, 1));
+        grow(d_rawl, (size_t)2 * kLmF * std::max(n_lm, 1));
+        grow(d_singular, 1);
         grow(d_partA, (size_t)kPartA * std::max(n_wave, 1));
         grow(d_partD, (size_t)kPartD * std::max(n_wave, 1));
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
@@ -1532,11 +1573,18 @@ struct BundleAdjuster {
         RSVIO_HIP(hipGetLastError());
     }
 
-    // K4 + K4c + K4d: this rank's reduced camera system in d_sys, summed over ranks when sharded
+    // K0 + K4: initial state and its linearisation (buffer 0)
+    void enqueue_start(double lambda0) {
+        enqueue_reset(lambda0);
+        if (G.n_wave) hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work());
+        RSVIO_HIP(hipGetLastError());
+    }
+
+    // K4c + K4d: this rank's reduced camera system (current linearisation, current lambda) in
+    // d_sys, summed over ranks when sharded
     void enqueue_linear_system() {
         const Prob pr = prob();
         const Work wk = work();
-        if (G.n_wave) hipLaunchKernelGGL(ba_linearize_eliminate, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
         hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(64), 0, stream, G, pr, wk);
         RSVIO_HIP(hipGetLastError());
         hipLaunchKernelGGL(ba_schur_combine, dim3(G.n_pb + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
@@ -1565,7 +1613,8 @@ struct BundleAdjuster {
         const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
         // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
         const int fuse = (!comm && G.n_wave) ? 1 : 0;
-        if (G.n_wave) hipLaunchKernelGGL(ba_backsub_cost, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, fuse, la);
+        if (G.n_wave)
+            hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, fuse, la);
         if (comm) {
             hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
             allreduce(d_trial4.p, 4);
@@ -1608,7 +1657,7 @@ struct BundleAdjuster {
         }
         pend.max_it = std::max(cfg.max_iterations, 1);
         RSVIO_HIP(hipEventRecord(ev0, stream));
-        enqueue_reset(cfg.lambda_init);
+        enqueue_start(cfg.lambda_init);
         enqueue_chunk(std::min(std::max(last_iterations, 1), pend.max_it));
     }
 
@@ -1655,7 +1704,7 @@ struct BundleAdjuster {
     void build_system(double lambda, double huber_delta, double* S, double* b, double* cost) {
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
-        enqueue_reset(lambda);
+        enqueue_start(lambda);
         enqueue_linear_system();
         std::vector<double> sys((size_t)36 * G.n_pb + 12 * G.n_free + 2);
         RSVIO_HIP(hipMemcpyAsync(sys.data(), d_sys.p, sizeof(double) * sys.size(), hipMemcpyDeviceToHost, stream));

@@ -52,6 +52,6 @@ def report(name, cols, labels):
         print(f"   {labels[i - 1]:>22s}: median {int(np.median(d)):7d}  max {int(d.max()):7d}")
 
 
-report("linearize_eliminate", [11, 12, 13, 14], ["obs linearize", "landmark inverse", "Y/record + partials"])
+report("linearize (initial)", [11, 12, 14], ["obs linearize", "store + partials"])
 report("schur_chunks", [16, 17, 18], ["pair products", "lane-ordered chunk sum"])
 report("backsub_cost", [20, 21], ["whole block"])
