@@ -67,6 +67,19 @@ def ba_flops_per_iter(n_obs: int, n_lm: int, k_per_lm: int, n_free: int) -> floa
 
 
 # ---------------------------------------------------------------------------------------
+def pmc_traffic(kernel: str):
+    """HBM bytes per dispatch of `kernel` (FETCH_SIZE + WRITE_SIZE) from the newest committed
+    PMC summary profiles/*_pmc_traffic.json (separate rocprofv3 --pmc passes of this same
+    bench command, tools/gpu_bench.sh + tools/pmc_summary.py), or None."""
+    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return k["fetch_size_bytes_per_dispatch"] + k["write_size_bytes_per_dispatch"], files[-1].name
+
+
 def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -295,6 +308,7 @@ def main():
     achieved = lk_bytes / (lk_ms * 1e-3) / 1e9
     prob = ba.prob
     flops = ba_flops_per_iter(prob.n_obs, prob.n_lm, 6, int((prob.kf_fixed == 0).sum()))
+    traffic, traffic_src = pmc_traffic("lk_track_kernel")
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -321,7 +335,8 @@ def main():
         "tracker_lk_ms_per_frame": round(lk_ms, 4),
         "roofline": {"kernel": "lk_track_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None,
+                     "traffic": None if traffic is None else round(traffic),
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": lk_bytes, "launch_ms": round(lk_ms, 4),
                      "note": "latency-bound: 900 one-wave workgroups (fwd+bwd chains) on 256 CUs"},
         "ba_roofline": {"bound": "fp64", "flop_per_iter": flops,
