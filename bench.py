@@ -112,10 +112,30 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def cu_partition(device: int, frac: float, layout: str):
+    """CU sets for the tracker and the BA streams (hipExtStreamCreateWithCUMask): the tracker's
+    900 latency-bound one-wave workgroups otherwise share SIMDs with the BA's serial kernels.
+    layout "stride": the tracker takes every k-th CU (all XCDs); "block": a contiguous range."""
+    import ctypes as C
+
+    from rsvio import _lib
+    n = C.c_int(0)
+    _lib.check(_lib.load().rsvio_device_info(device, None, 0, C.byref(n)))
+    n = n.value
+    k = max(1, min(n - 1, int(round(frac * n))))
+    if layout == "block":
+        trk = list(range(k))
+    else:
+        step = n / k
+        trk = sorted({int(i * step) for i in range(k)})
+    ba = [c for c in range(n) if c not in set(trk)]
+    return trk, ba
+
+
 class TrackerWorkload:
     """Config 2 on device: per-frame pyramids (left, right) + 3 track_points batches."""
 
-    def __init__(self, device: int):
+    def __init__(self, device: int, stream_ptr=None):
         import ctypes as C
 
         import torch
@@ -153,7 +173,8 @@ class TrackerWorkload:
         self.seq = [0, 1, 2, 3, 2, 1]
         self.k = 0
         self.slot = 0
-        self.stream = torch.cuda.current_stream(dev)
+        self.stream = (torch.cuda.ExternalStream(stream_ptr, device=dev) if stream_ptr
+                       else torch.cuda.current_stream(dev))
         self.ev = []
         # prime: pyramids of the first frame
         self._pyramids(self.seq[0], self.slot)
@@ -195,7 +216,7 @@ class TrackerWorkload:
 
 
 class BAWorkload:
-    def __init__(self, device: int, world: int, rank: int):
+    def __init__(self, device: int, world: int, rank: int, stream_ptr=None):
         from rsvio import synthetic as S
         from rsvio.ba import BundleAdjuster
         t0 = time.time()
@@ -211,6 +232,8 @@ class BAWorkload:
             obj = [BundleAdjuster.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             self.ba.attach_comm(world, rank, obj[0])
+        if stream_ptr:
+            self.ba.set_stream(stream_ptr)
         self.ba.set_problem_from(self.prob)
         self.iters = []
         self.solve_ms = []
@@ -268,6 +291,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cu-split", type=float, default=0.5,
+                    help="fraction of CUs given to the tracker stream (0: no CU partition)")
+    ap.add_argument("--cu-layout", default="stride", choices=["stride", "block"])
     args = ap.parse_args()
 
     world, rank, local = setup_dist()
@@ -278,8 +304,14 @@ def main():
     import rsvio
     arch = rsvio.require_device(local)
     log(f"[bench] rank {rank}/{world} on cuda:{local} ({arch})")
-    trk = TrackerWorkload(local)
-    ba = BAWorkload(local, world, rank)
+    streams = []
+    if args.cu_split > 0:
+        from rsvio._lib import CuStream
+        cu_trk, cu_ba = cu_partition(local, args.cu_split, args.cu_layout)
+        streams = [CuStream(local, cu_trk), CuStream(local, cu_ba)]
+        log(f"[bench] CU partition ({args.cu_layout}): tracker {len(cu_trk)} CUs, BA {len(cu_ba)} CUs")
+    trk = TrackerWorkload(local, streams[0].ptr if streams else None)
+    ba = BAWorkload(local, world, rank, streams[1].ptr if streams else None)
 
     # one step: the BA solve is enqueued first (its stream), the frame's tracking is enqueued on
     # the tracker stream while it runs, then the host completes the solve
@@ -328,7 +360,9 @@ def main():
                                "(24,000 obs/GPU), Schur LM <= 20 it; every frame a keyframe",
                    "image": "752x480", "features": NFEAT, "levels": LEVELS, "keyframes": 10,
                    "landmarks_per_gpu": prob.n_lm, "observations_per_gpu": prob.n_obs,
-                   "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s) (RCCL)"},
+                   "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s) (RCCL)",
+                   "cu_partition": (f"{args.cu_layout} {args.cu_split:g} of CUs to the tracker stream"
+                                    if args.cu_split > 0 else "none")},
         "ba_ms_per_iter": round(ba_ms_iter, 4),
         "ba_iterations": ba_iters,
         "ba_ms_per_solve": round(ba_solve_ms, 4),

@@ -44,6 +44,13 @@ const char* rsvio_last_error(void);
 /* Library / device identification; returns RSVIO_ERR_NO_DEVICE if no gfx950 is visible. */
 int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus);
 
+/* HIP stream (hipStream_t) for the device-pointer entry points and rsvio_ba_set_stream.
+ * cu_mask (mask_words x 32 bits, bit i = CU i; NULL = all CUs) restricts the stream's kernels
+ * to a CU subset, so the tracker and the BA of one process can run side by side on disjoint
+ * CUs (hipExtStreamCreateWithCUMask).  No reference counterpart (the reference is CPU-only). */
+int rsvio_stream_create(int32_t device, const uint32_t* cu_mask, uint32_t mask_words, void** out);
+int rsvio_stream_destroy(void* stream);
+
 /* =============================== HP-T: patch tracker =============================== */
 
 typedef struct {
@@ -182,6 +189,8 @@ int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
  * tracking) with the solve: _run_async enqueues the first chunk of LM iterations and returns;
  * _wait completes the solve and fills res.  One solve in flight per handle. */
 int rsvio_ba_run_async(rsvio_ba* ba, const rsvio_lm_cfg* cfg);
+/* Enqueue the handle's work on a caller-owned stream (NULL: back to the handle's own stream). */
+int rsvio_ba_set_stream(rsvio_ba* ba, void* stream);
 int rsvio_ba_wait(rsvio_ba* ba, rsvio_ba_result* res);
 int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W);
 /* Reduced camera system at `lambda` for the uploaded state (parity tests):

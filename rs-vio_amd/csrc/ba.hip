@@ -281,8 +281,8 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[0][i] = Wk.pw_init[i];
         Wk.pw[1][i] = Wk.pw_init[i];
     }
+    if (i < G.n_pb + 1) Wk.cnt[i] = 0;
     if (i == 0) {
-        *Wk.cnt = 0;
         *Wk.singular = 0;
         LmState s{};
         s.lambda = lambda0;
@@ -482,9 +482,21 @@ __device__ double block_ordered_sum(const double* __restrict__ v, int n, int str
 // The lane partials are transposed through LDS and summed in lane order; the chunk partial
 // (48 values) goes to cpart.  No atomics: K4d combines the chunks of each block in order.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk) {
+__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, int fused) {
     __shared__ double sh[kBlockF * 65];
     const int c = blockIdx.x, lane = threadIdx.x;
+    if (c == G.n_chunk) {  // fused: the initial cost of this rank for the first decision
+        if (Wk.st->done) return;
+        const int SC0 = G.n_pb * 36 + 12 * G.n_free;
+        double v = 0.0;
+        for (int w = lane; w < G.n_wave; w += 64) v += Wk.partA[w * kPartA];
+        v = wave_sum_det(v);
+        if (lane == 0) {
+            Wk.sys[SC0] = v;
+            Wk.sys[SC0 + 1] = 0.0;  // the singular flag stays in Wk.singular (read by K5)
+        }
+        return;
+    }
     const int pb = Pr.chunk_pb[c];
     const bool diag = Pr.pb_fa[pb] == Pr.pb_fb[pb];
     const int p0 = Pr.chunk_pair[c], np = Pr.chunk_pair[c + 1] - p0;
@@ -572,9 +584,42 @@ __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work 
         double s = 0.0;
 #pragma unroll 16
         for (int k = 0; k < 64; ++k) s += row[k];  // lanes >= np hold zeros
-        Wk.cpart[(size_t)c * kBlockF + lane] = s;
+        if (fused)  // device-coherent (sc1): the block's last chunk reads it in this launch
+            __hip_atomic_store(Wk.cpart + (size_t)c * kBlockF + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            Wk.cpart[(size_t)c * kBlockF + lane] = s;
     }
     STAMP(18);
+    if (!fused) return;
+    // K4d folded in (single rank): drain the sc1 partials, count the block's arrivals; the last
+    // chunk of the block sums the block's chunk partials in chunk order (+ lambda on the
+    // diagonal) and writes the block of S, b, g_c for K5
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
+    int last = 0;
+    if (lane == 0) {
+        const int old = __hip_atomic_fetch_add(Wk.cnt + 1 + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == c1 - c0 - 1;
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    if (lane == 0) __hip_atomic_store(Wk.cnt + 1 + pb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < nf) {
+        double v = 0.0;
+#pragma unroll 8
+        for (int cc = c0; cc < c1; ++cc)
+            v += __hip_atomic_load(Wk.cpart + (size_t)cc * kBlockF + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int fa = Pr.pb_fa[pb];
+        const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free;
+        if (lane < 36) {
+            if (diag && lane / 6 == lane % 6) v += lambda;
+            Wk.sys[pb * 36 + lane] = v;
+        } else if (lane < 42) {
+            Wk.sys[SB0 + 6 * fa + (lane - 36)] = v;   // b = -g_c + sum Y g_p
+        } else {
+            Wk.sys[SG0 + 6 * fa + (lane - 42)] = v;   // g_c
+        }
+    }
 }
 
 // Cost of the initial linearisation of this rank (K4 wave partials, one wave, fixed order) and
@@ -865,7 +910,10 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     }
     STAMP(0);
     if (tid == 0) {
-        fail = (sys[SC0 + 1] != 0.0) ? 1 : 0;  // a landmark block was singular
+        // a landmark block was singular (sharded: summed over ranks by K4d + all-reduce;
+        // single rank: K4c's flag, cleared here for the next iteration)
+        fail = (sys[SC0 + 1] != 0.0 || *Wk.singular) ? 1 : 0;
+        *Wk.singular = 0;
         progress = 0;
     }
     // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
@@ -1335,9 +1383,11 @@ RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 struct BundleAdjuster {
     rsvio_ba_params P{};
     hipStream_t stream = nullptr;
+    bool own_stream = true;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Geometry G{};
     bool has_problem = false;
+    bool fuse_combine = true;  // single rank: K4d folded into K4c
     int iter_chunk = 2;       // LM iterations enqueued per status read-back after the first chunk
     int last_iterations = 3;  // first chunk = previous solve's iteration count
     DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_slot_uv;
@@ -1367,7 +1417,7 @@ struct BundleAdjuster {
         if (comm) ncclCommDestroy(comm);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
-        if (stream) (void)hipStreamDestroy(stream);
+        if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
     template <class T>
@@ -1553,7 +1603,7 @@ struct BundleAdjuster {
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
-        grow(d_cnt, 1);
+        grow(d_cnt, (size_t)n_pb + 1);
         grow(d_state, 1);
         enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
         RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
@@ -1568,7 +1618,7 @@ struct BundleAdjuster {
     }
 
     void enqueue_reset(double lambda0) {
-        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb);
+        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb + 1);
         hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work(), lambda0);
         RSVIO_HIP(hipGetLastError());
     }
@@ -1585,7 +1635,12 @@ struct BundleAdjuster {
     void enqueue_linear_system() {
         const Prob pr = prob();
         const Work wk = work();
-        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(64), 0, stream, G, pr, wk);
+        if (!comm && fuse_combine) {  // K4d folded into K4c (last chunk of each block)
+            hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk + 1), dim3(64), 0, stream, G, pr, wk, 1);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
+        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(64), 0, stream, G, pr, wk, 0);
         RSVIO_HIP(hipGetLastError());
         hipLaunchKernelGGL(ba_schur_combine, dim3(G.n_pb + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
@@ -1687,6 +1742,20 @@ struct BundleAdjuster {
         res->solve_ms = ms;
     }
 
+    // run on a caller-owned stream (e.g. one restricted to a CU subset); nullptr = own stream
+    void set_stream(hipStream_t s) {
+        if (pend.active) throw std::logic_error("a solve is in flight");
+        RSVIO_HIP(hipStreamSynchronize(stream));
+        if (s) {
+            if (own_stream) RSVIO_HIP(hipStreamDestroy(stream));
+            stream = s;
+            own_stream = false;
+        } else if (!own_stream) {
+            RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+            own_stream = true;
+        }
+    }
+
     void run(const rsvio_lm_cfg& cfg, rsvio_ba_result* res) {
         start(cfg);
         finish(res);
@@ -1779,6 +1848,14 @@ int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res) {
     if (!ba || !cfg || !res) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
         ba->b.run(*cfg, res);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_set_stream(rsvio_ba* ba, void* stream) {
+    if (!ba) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        ba->b.set_stream(static_cast<hipStream_t>(stream));
         return (int)RSVIO_OK;
     });
 }

@@ -517,6 +517,28 @@ int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus) {
     });
 }
 
+int rsvio_stream_create(int32_t device, const uint32_t* cu_mask, uint32_t mask_words, void** out) {
+    if (!out || (cu_mask && mask_words == 0)) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        RSVIO_HIP(hipSetDevice(device));
+        hipStream_t s = nullptr;
+        if (cu_mask)
+            RSVIO_HIP(hipExtStreamCreateWithCUMask(&s, mask_words, cu_mask));
+        else
+            RSVIO_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *out = s;
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_stream_destroy(void* stream) {
+    if (!stream) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        RSVIO_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+        return (int)RSVIO_OK;
+    });
+}
+
 int rsvio_tracker_create(const rsvio_tracker_params* params, rsvio_tracker** out) {
     if (!params || !out) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {

@@ -89,6 +89,9 @@ SIG = {
     "rsvio_ba_set_problem": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, C.c_int32, P, P, P, P, P]),
     "rsvio_ba_run": (C.c_int, [P, C.POINTER(LmCfg), C.POINTER(BaResult)]),
     "rsvio_ba_run_async": (C.c_int, [P, C.POINTER(LmCfg)]),
+    "rsvio_ba_set_stream": (C.c_int, [P, P]),
+    "rsvio_stream_create": (C.c_int, [C.c_int32, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(P)]),
+    "rsvio_stream_destroy": (C.c_int, [P]),
     "rsvio_ba_wait": (C.c_int, [P, C.POINTER(BaResult)]),
     "rsvio_ba_get_state": (C.c_int, [P, P, P]),
     "rsvio_ba_build_system": (C.c_int, [P, C.c_double, C.c_double, P, P, C.POINTER(C.c_double)]),
@@ -142,3 +145,26 @@ def require_device(device: int = 0) -> str:
     ncu = C.c_int(0)
     check(lib.rsvio_device_info(device, name, 64, C.byref(ncu)))
     return name.value.decode()
+
+
+class CuStream:
+    """A HIP stream restricted to a set of CUs (rsvio_stream_create); .ptr is the hipStream_t."""
+
+    def __init__(self, device: int, cus=None):
+        lib = load()
+        out = C.c_void_p()
+        if cus is None:
+            check(lib.rsvio_stream_create(device, None, 0, C.byref(out)))
+        else:
+            n = max(cus) + 1
+            words = (n + 31) // 32
+            mask = (C.c_uint32 * words)()
+            for c in cus:
+                mask[c // 32] |= 1 << (c % 32)
+            check(lib.rsvio_stream_create(device, mask, words, C.byref(out)))
+        self.ptr = out.value
+
+    def close(self):
+        if self.ptr:
+            check(load().rsvio_stream_destroy(self.ptr))
+            self.ptr = None

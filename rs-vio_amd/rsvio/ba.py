@@ -79,6 +79,10 @@ class BundleAdjuster:
         check(_lib.load().rsvio_ba_run(self._h, C.byref(cfg or lm_cfg()), C.byref(res)))
         return res
 
+    def set_stream(self, stream_ptr) -> None:
+        """Enqueue on a caller-owned HIP stream (rsvio.cu_stream), None = the handle's own."""
+        check(_lib.load().rsvio_ba_set_stream(self._h, stream_ptr))
+
     def run_async(self, cfg=None) -> None:
         """Enqueue the solve and return (rsvio_ba_run_async); wait() completes it."""
         self._cfg = cfg or lm_cfg()  # kept alive until wait()
