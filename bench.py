@@ -293,7 +293,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cu-split", type=float, default=0.5,
                     help="fraction of CUs given to the tracker stream (0: no CU partition)")
-    ap.add_argument("--cu-layout", default="stride", choices=["stride", "block"])
+    ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
     args = ap.parse_args()
 
     world, rank, local = setup_dist()
