@@ -33,35 +33,34 @@ __constant__ int8_t kPattern[64][2] = {
     {1, -5},  {3, -5},  {5, -5},  {-3, -7}, {-1, -7}, {1, -7},  {3, -7}};
 
 // N independent sequential f32 sums over lanes 0..51, in lane order (the reference's loop order):
-// every lane stages its N values in LDS, then every lane reads them back with broadcast
-// ds_read_b128 and runs the N dependent add chains interleaved.  FROM_ZERO: acc = 0; acc += v_k
-// (Rust `sum += x` loops); otherwise acc = v_0; acc = v_k + acc (nalgebra gemv / gemm column
-// accumulation).  All lanes end with the same sums.  sh: N * 64 floats of this wave's LDS.
+// every lane stages its N values in LDS (row i = value i, padded stride), lane i then runs chain
+// i alone -- 52 dependent adds, the N chains side by side in N lanes -- and the sums are
+// broadcast back by readlane.  FROM_ZERO: acc = 0; acc += v_k (Rust `sum += x` loops); otherwise
+// acc = v_0; acc = v_k + acc (nalgebra gemv / gemm column accumulation).  All lanes end with
+// the same sums.  sh: N * kChainLd floats of this wave's LDS.
+constexpr int kChainLd = 68;  // row stride (floats): 16-B aligned rows on distinct banks
+
 template <int N, bool FROM_ZERO>
 __device__ __forceinline__ void lane_chains(const float (&v)[N], float (&out)[N], float* sh, int lane) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) sh[i * 64 + lane] = v[i];
+    for (int i = 0; i < N; ++i) sh[i * kChainLd + lane] = v[i];
     __builtin_amdgcn_wave_barrier();
-    float acc[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = 0.0f;
+    const float4* row = reinterpret_cast<const float4*>(sh + (lane < N ? lane : 0) * kChainLd);
+    float acc = 0.0f;
 #pragma unroll
     for (int q = 0; q < NP / 4; ++q) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            const float4 x = reinterpret_cast<const float4*>(sh + i * 64)[q];
-            if (!FROM_ZERO && q == 0)
-                acc[i] = x.x;
-            else
-                acc[i] = acc[i] + x.x;
-            acc[i] = acc[i] + x.y;
-            acc[i] = acc[i] + x.z;
-            acc[i] = acc[i] + x.w;
-        }
+        const float4 x = row[q];
+        if (!FROM_ZERO && q == 0)
+            acc = x.x;
+        else
+            acc = acc + x.x;
+        acc = acc + x.y;
+        acc = acc + x.z;
+        acc = acc + x.w;
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = acc[i];
+    for (int i = 0; i < N; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), i));
 }
 
 __device__ __forceinline__ uint32_t sat_u32(float v) {
@@ -364,7 +363,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
     const int idx = job - L.start[b];
     if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
-    __shared__ float sh[6 * 64];
+    __shared__ __attribute__((aligned(16))) float sh[6 * kChainLd];
     const int lane = threadIdx.x;
     const float patx = lane < NP ? (float)kPattern[lane][0] / 2.0f : 0.0f;
     const float paty = lane < NP ? (float)kPattern[lane][1] / 2.0f : 0.0f;
