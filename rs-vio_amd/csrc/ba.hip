@@ -1264,17 +1264,40 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
     STAMP(20);
     const bool act = h1.y > 0;
     const int cur = st->cur;
+    const double lambda = st->lambda;
     const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
     const bool fr = h1.x >= 0;
+    // every global input of this lane in one round trip (indices clamped on padding lanes):
+    // the slot's W, the camera step, the landmark's raw record and point, the trial pose
+    const int kfc = act ? kf : 0, lc = act ? l : 0, fc = (act && fr) ? h1.x : 0;
+    double Wv[18], d6[6], Lm[10], pc[3], p7[7];
+    {
+        const double2* wr = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)s * kRawF + RW);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double2 x = wr[i];
+            Wv[2 * i] = x.x; Wv[2 * i + 1] = x.y;
+        }
+        const double2* lr = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)lc * kLmF);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double2 x = lr[i];
+            Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) d6[i] = Wk.dc[6 * fc + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pc[i] = Wk.pw[cur][3 * lc + i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[1 - cur][7 * kfc + i];
+    }
     double t3[3] = {0.0, 0.0, 0.0};
     if (act && fr) {
-        const double* d6 = Wk.dc + 6 * h1.x;
-        const double* Wr = Wk.raws[cur] + (size_t)s * kRawF + RW;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             double acc = 0.0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) acc += Wr[a * 3 + c] * d6[a];
+            for (int a = 0; a < 6; ++a) acc += Wv[a * 3 + c] * d6[a];
             t3[c] = acc;
         }
     }
@@ -1283,15 +1306,14 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
 #pragma unroll
     for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
     __syncthreads();
+    STAMP(22);
     if (act && lane == first) {
-        const double* Lm = Wk.rawl[cur] + (size_t)l * kLmF;
         double Vi[3][3];
-        landmark_inverse(Lm + LV, st->lambda, Vi);
+        landmark_inverse(Lm + LV, lambda, Vi);
         double rhs[3] = {-Lm[LG], -Lm[LG + 1], -Lm[LG + 2]};
         for (int k = 0; k < nk; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) rhs[c] -= sh[c][first + k];
-        const double* pc = Wk.pw[cur] + 3 * l;
         double* pt = Wk.pw[1 - cur] + 3 * l;
         double dp2 = 0.0, gpdp = 0.0, p2 = 0.0;
 #pragma unroll
@@ -1310,10 +1332,11 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
         shs[3][lane] = p2;
     }
     __syncthreads();
+    STAMP(23);
     // linearisation of the trial state
     SlotLin L;
     if (act) {
-        const Pose P = pose_from7(Wk.pose[1 - cur] + 7 * kf);
+        const Pose P = pose_from7(p7);
         const double q[3] = {shp[0][first], shp[1][first], shp[2][first]};
         slot_linearize(G, P, q, h1.y, h1.z, uvq, fr, L);
     } else {
@@ -1323,7 +1346,9 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
     }
     shs[0][lane] = L.cost;
     __syncthreads();  // sh is reused below
+    STAMP(24);
     store_linearization(Wk, 1 - cur, s, lane, act, fr, first, nk, l, L, sh);
+    STAMP(25);
     {  // wave partials: fixed-pairing butterflies over the lanes
         double v[kPartD];
 #pragma unroll

@@ -54,4 +54,5 @@ def report(name, cols, labels):
 
 report("linearize (initial)", [11, 12, 14], ["obs linearize", "store + partials"])
 report("schur_chunks", [16, 17, 18], ["pair products", "lane-ordered chunk sum"])
-report("backsub_cost", [20, 21], ["whole block"])
+report("backsub_relinearize", [20, 22, 23, 24, 25, 21],
+       ["W^T dc", "dp (first lanes)", "trial linearise", "store linearisation", "partials"])
