@@ -783,20 +783,30 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
     if constexpr (KNEXT < c1) chol_pipe_step<NP, CW, WV, KNEXT>(a, lane, Lc, Uc, progress, seen, bad, inv);
 }
 
+// Element (r, c), c <= r < n, of the lower triangle of S in the packed block layout of sys
+// (upper camera blocks fa <= fb, block-major a-then-b; a diagonal block keeps its own lower
+// triangle, an off-diagonal one is read transposed).  row == n: b.
+template <int NF>
+__device__ __forceinline__ const double* sys_lower(const double* sys, int r, int c) {
+    constexpr int n = 6 * NF;
+    if (r == n) return sys + (NF * (NF + 1) / 2) * 36 + c;
+    const int a = c / 6, b = r / 6;
+    const int pb = a * NF - a * (a - 1) / 2 + (b - a);
+    const int k = (a == b) ? (r % 6) * 6 + (c % 6) : (c % 6) * 6 + (r % 6);
+    return sys + pb * 36 + k;
+}
+
 template <int NP, int CW, int WV>
-__device__ void chol_pipe(const double* A, double* Lc, double* Uc, int* progress, int* badw, int n, int lane) {
+__device__ void chol_pipe(const double* sys, double* Lc, double* Uc, int* progress, int* badw, int lane) {
     constexpr int c0 = WV * CW;
     double a[CW];
-    const int src = lane < n ? lane : (lane == NP ? n : -1);
+    // this wave's columns of every row straight from sys (one round trip): row lane < NP of S,
+    // row NP = b, the rest zero
 #pragma unroll
     for (int jj = 0; jj < CW; ++jj) {
         const int c = c0 + jj;
-        double v = 0.0;
-        if (src >= 0 && c < n && (c <= lane || lane == NP)) v = A[src * kLdA + c];
-        if (lane >= n && lane < NP && c == lane) v = 1.0;
-        a[jj] = v;
+        a[jj] = (c < NP && lane <= NP && (c <= lane || lane == NP)) ? *sys_lower<NP / 6>(sys, lane, c) : 0.0;
     }
-    __syncthreads();  // every wave holds its columns: A may now be overwritten by Lc / Uc
     bool bad = false;
     if constexpr (c0 < NP) {
         double inv = 0.0;
@@ -820,14 +830,15 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
     constexpr int NP = 6 * NF, CW = (NP + 3) / 4;
     const int lane = tid & 63, wave = tid >> 6;
     LmState* st = Wk.st;
-    // Lc / Uc overwrite A once every wave has loaded its columns (A[0..n) is reused for dc later)
+    const double gcl_v = (wave == 0 && lane < n) ? Wk.sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
+    // Lc / Uc in A's LDS past its first 128 doubles (A[0..n) holds dc for the pose updates)
     double* Lc = A + 128;
     double* Uc = Lc + NP * kLcLd;
     switch (wave) {
-        case 0: chol_pipe<NP, CW, 0>(A, Lc, Uc, progress, badw, n, lane); break;
-        case 1: chol_pipe<NP, CW, 1>(A, Lc, Uc, progress, badw, n, lane); break;
-        case 2: chol_pipe<NP, CW, 2>(A, Lc, Uc, progress, badw, n, lane); break;
-        default: chol_pipe<NP, CW, 3>(A, Lc, Uc, progress, badw, n, lane); break;
+        case 0: chol_pipe<NP, CW, 0>(Wk.sys, Lc, Uc, progress, badw, lane); break;
+        case 1: chol_pipe<NP, CW, 1>(Wk.sys, Lc, Uc, progress, badw, lane); break;
+        case 2: chol_pipe<NP, CW, 2>(Wk.sys, Lc, Uc, progress, badw, lane); break;
+        default: chol_pipe<NP, CW, 3>(Wk.sys, Lc, Uc, progress, badw, lane); break;
     }
     __syncthreads();
     if (wave != 0) return;
@@ -855,11 +866,11 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
     STAMP(3);
     const double x = lane < n ? yv : 0.0;
     const double d2 = wave_sum_det(x * x);
-    const double gd = wave_sum_det(lane < n ? gcl[lane] * x : 0.0);
+    const double gd = wave_sum_det(lane < n ? gcl_v * x : 0.0);
     __builtin_amdgcn_wave_barrier();
     if (lane < n) {
         Wk.dc[lane] = x;
-        A[lane] = x;  // row 0 of A reused as dc for the pose updates (Lc lies past row NP)
+        A[lane] = x;  // A[0..n) holds dc for the pose updates (Lc lies past A[128])
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -919,7 +930,7 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
     // blocks (fa < fb, upper) are transposed into the lower triangle; b as row n, g_c in gcl.
     // Each element's value and its block's keyframe pair are loaded together (one round trip).
-    const int nel = SB0 + 12 * nF;
+    const int nel = NF > 0 ? 0 : SB0 + 12 * nF;  // the register path reads sys itself
     auto place = [&](int e, double v, int fa, int fb) {
         if (e >= SB0) {  // b, g_c
             const int i = e - SB0;
