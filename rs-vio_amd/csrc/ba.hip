@@ -756,6 +756,9 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
 #ifdef RSVIO_STAMPS
         if (K == c0 && lane == 0) g_dbg[28 + WV] = (unsigned long long)clock64();
 #endif
+        // publish column K-1 now: its LDS writes have long landed, so the release does not
+        // stall this column's pivot chain (the last column is published at the end)
+        if constexpr (K > c0) __hip_atomic_store(progress, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         const double uk = a[j];
         const double l = uk * inv;
         a[j] = l;
@@ -775,12 +778,14 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
             bad |= !(piv > 0.0) || !isfinite(piv);
             inv = rcp_f64(piv);
         }
-        __hip_atomic_store(progress, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (K + 1 == c1) __hip_atomic_store(progress, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // materialise this step's updates here (keeps the compiler from sinking the FMAs past the
-    // next wait loop, which would keep every loaded column alive)
+    // consume steps: materialise the updates here (keeps the compiler from sinking the FMAs
+    // past the next wait loop, which would keep every loaded column alive)
+    if constexpr (K < c0) {
 #pragma unroll
-    for (int jj = 0; jj < CW; ++jj) __asm__ volatile("" : "+v"(a[jj]));
+        for (int jj = 0; jj < CW; ++jj) __asm__ volatile("" : "+v"(a[jj]));
+    }
     constexpr int KNEXT = (K < c0) ? KN : K + 1;
     if constexpr (KNEXT < c1) chol_pipe_step<NP, CW, WV, KNEXT>(a, lane, Lc, Uc, progress, seen, bad, inv);
 }
