@@ -209,6 +209,11 @@ class TrackerWorkload:
         self.slot = cur
         self.k += 1
 
+    def close(self):
+        if self.ctx:
+            self.lib.rsvio_track_ctx_destroy(self.ctx)
+            self.ctx = None
+
     def lk_ms(self):
         if not self.ev:
             return float("nan")
@@ -388,7 +393,12 @@ def main():
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
+    # release device objects before interpreter teardown (the CU-mask streams last)
+    torch.cuda.synchronize()
     ba.ba.close()
+    trk.close()
+    for st in streams:
+        st.close()
 
 
 if __name__ == "__main__":
