@@ -202,6 +202,14 @@ int rsvio_ba_build_system(rsvio_ba* ba, double lambda, double huber_delta, doubl
  * landmarks/observations; the reduced system and costs are summed with RCCL over xGMI. */
 int rsvio_rccl_unique_id(uint8_t* out, size_t cap);   /* cap >= 128 */
 int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* unique_id);
+/* Peer-to-peer one-shot all-reduce for the same exchanges (latency-bound small messages over
+ * xGMI): each rank exports its exchange buffer (64-byte IPC handle), the handles of all ranks
+ * are exchanged by the caller, then every rank attaches; attach runs a self-test and fails
+ * (the handle keeps RCCL / its previous collective) if any peer is unreachable.  All ranks
+ * must end in the same mode: on any rank's failure every rank calls rsvio_ba_detach_p2p. */
+int rsvio_ba_p2p_export(rsvio_ba* ba, int32_t nranks, uint8_t* handle_out, size_t cap);
+int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* handles);
+int rsvio_ba_detach_p2p(rsvio_ba* ba);
 
 #ifdef __cplusplus
 }

@@ -1418,6 +1418,60 @@ __global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk,
     STAMP(10);
 }
 
+// ---------------------------------------------------------------------------------------
+// One-shot peer-to-peer all-reduce over xGMI for the sharded BA's small per-iteration
+// messages (the reduced system, ~14 KB at W=10; 4 trial scalars).  Every rank exports an
+// uncached exchange buffer (IPC); a call pushes the message into slot [parity][rank] of every
+// peer's buffer, raises its flag there (system-scope release), waits for every peer's flag in
+// its own buffer (bounded), then sums the slots in rank order -- one kernel, one xGMI
+// round trip, identical bits on every rank.  Generations alternate two parities, so a rank
+// that runs ahead can never overwrite a slot its slower peer is still reading.
+// ---------------------------------------------------------------------------------------
+constexpr int kP2PMax = 8;       // ranks
+constexpr int kP2PMsg = 8192;    // doubles per slot (>= 36 * 210 + 12 * 20 + 2)
+
+struct P2P {
+    double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
+    int nranks, rank;
+};
+
+__device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
+    return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
+}
+
+__global__ __launch_bounds__(256) void ba_p2p_allreduce(double* buf, int n, P2P P, unsigned long long gen,
+                                                        int* err) {
+    const int tid = threadIdx.x, nr = P.nranks, me = P.rank, par = (int)(gen & 1);
+    for (int r = 0; r < nr; ++r) {
+        double* dst = P.peer[r] + (size_t)(par * kP2PMax + me) * kP2PMsg;
+        for (int i = tid; i < n; i += 256) dst[i] = buf[i];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nr)
+        __hip_atomic_store(p2p_flags(P.peer[tid]) + par * kP2PMax + me, gen, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < nr) {
+        const unsigned long long* f = p2p_flags(P.peer[me]) + par * kP2PMax + tid;
+        long long spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1ll << 25)) {  // a peer never arrived: report, do not hang
+                atomicExch(err, 1);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const double* mine = P.peer[me] + (size_t)(par * kP2PMax) * kP2PMsg;
+    for (int i = tid; i < n; i += 256) {
+        double v = 0.0;
+        for (int r = 0; r < nr; ++r)
+            v += __hip_atomic_load(mine + (size_t)r * kP2PMsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        buf[i] = v;
+    }
+}
+
 }  // namespace
 
 RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
@@ -1445,6 +1499,14 @@ struct BundleAdjuster {
     HostBuf<LmState> h_state;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // collective of the sharded path: 0 none (single rank), 1 RCCL, 2 peer-to-peer one-shot
+    int coll = 0;
+    bool sharded() const { return coll != 0; }
+    double* xbuf = nullptr;               // P2P exchange buffer (uncached, IPC-exported)
+    P2P p2p{};
+    bool p2p_opened[kP2PMax] = {};
+    unsigned long long p2p_gen = 0;
+    DevBuf<int> d_p2p_err;
 
     void init(const rsvio_ba_params& p) {
         P = p;
@@ -1458,6 +1520,9 @@ struct BundleAdjuster {
     }
     ~BundleAdjuster() {
         if (comm) ncclCommDestroy(comm);
+        for (int r = 0; r < kP2PMax; ++r)
+            if (p2p_opened[r]) (void)hipIpcCloseMemHandle(p2p.peer[r]);
+        if (xbuf) (void)hipFree(xbuf);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
@@ -1655,7 +1720,14 @@ struct BundleAdjuster {
     }
 
     void allreduce(double* buf, size_t n) {
-        if (!comm || n == 0) return;
+        if (!sharded() || n == 0) return;
+        if (coll == 2) {
+            if (n > kP2PMsg) throw std::runtime_error("message exceeds the P2P slot");
+            hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, buf, (int)n, p2p, ++p2p_gen,
+                               d_p2p_err.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
         if (ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm, stream) != ncclSuccess)
             throw std::runtime_error("RCCL all-reduce failed");
     }
@@ -1678,7 +1750,7 @@ struct BundleAdjuster {
     void enqueue_linear_system() {
         const Prob pr = prob();
         const Work wk = work();
-        if (!comm && fuse_combine) {  // K4d folded into K4c (last chunk of each block)
+        if (!sharded() && fuse_combine) {  // K4d folded into K4c (last chunk of each block)
             hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk + 1), dim3(64), 0, stream, G, pr, wk, 1);
             RSVIO_HIP(hipGetLastError());
             return;
@@ -1710,15 +1782,15 @@ struct BundleAdjuster {
         launch_camera_solve(pr, wk);
         const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
         // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
-        const int fuse = (!comm && G.n_wave) ? 1 : 0;
+        const int fuse = (!sharded() && G.n_wave) ? 1 : 0;
         if (G.n_wave)
             hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, fuse, la);
-        if (comm) {
+        if (sharded()) {
             hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
             allreduce(d_trial4.p, 4);
         }
         if (!fuse)
-            hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, pr, wk, comm ? 1 : 0, la);
+            hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, pr, wk, sharded() ? 1 : 0, la);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -1749,7 +1821,7 @@ struct BundleAdjuster {
         pend.active = true;
         pend.cfg = cfg;
         // sliding_window.rs:303-319: too few residuals / underconstrained -> skipped (Ok(false))
-        if (!comm && (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm)) {
+        if (!sharded() && (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm)) {
             pend.skipped = true;
             return;
         }
@@ -1775,6 +1847,7 @@ struct BundleAdjuster {
             enqueue_chunk(std::min(iter_chunk, pend.max_it - pend.enq));
         }
         last_iterations = h_state.p->iter;
+        if (coll == 2) p2p_check();
         float ms = 0.0f;
         RSVIO_HIP(hipEventElapsedTime(&ms, ev0, ev1));
         const LmState& s = *h_state.p;
@@ -1783,6 +1856,65 @@ struct BundleAdjuster {
         res->initial_cost = s.initial_cost;
         res->final_cost = s.cost;
         res->solve_ms = ms;
+    }
+
+    // ---- peer-to-peer collective (sharded path) ----
+    void p2p_export(int nr, hipIpcMemHandle_t* h) {
+        if (nr < 1 || nr > kP2PMax) throw std::invalid_argument("P2P: 1..8 ranks");
+        if (!xbuf) {
+            const size_t bytes = sizeof(double) * 2 * kP2PMax * kP2PMsg + sizeof(unsigned long long) * 2 * kP2PMax;
+            RSVIO_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&xbuf), bytes, hipDeviceMallocUncached));
+            RSVIO_HIP(hipMemset(xbuf, 0, bytes));
+            d_p2p_err.alloc(1);
+            RSVIO_HIP(hipMemset(d_p2p_err.p, 0, sizeof(int)));
+        }
+        RSVIO_HIP(hipIpcGetMemHandle(h, xbuf));
+    }
+
+    void p2p_check() {
+        int err = 0;
+        RSVIO_HIP(hipMemcpy(&err, d_p2p_err.p, sizeof(int), hipMemcpyDeviceToHost));
+        if (err) throw std::runtime_error("P2P all-reduce: a peer did not arrive");
+    }
+
+    // open the peers' exchange buffers and self-test one all-reduce; on any failure the
+    // handle keeps its previous collective
+    void p2p_attach(int nr, int rk, const hipIpcMemHandle_t* hs) {
+        if (nr < 1 || nr > kP2PMax || rk < 0 || rk >= nr) throw std::invalid_argument("P2P: bad rank layout");
+        if (!xbuf) throw std::logic_error("P2P: export the buffer first");
+        P2P P{};
+        P.nranks = nr;
+        P.rank = rk;
+        for (int r = 0; r < nr; ++r) {
+            if (r == rk) {
+                P.peer[r] = xbuf;
+                continue;
+            }
+            void* ptr = nullptr;
+            RSVIO_HIP(hipIpcOpenMemHandle(&ptr, hs[r], hipIpcMemLazyEnablePeerAccess));
+            P.peer[r] = static_cast<double*>(ptr);
+            p2p_opened[r] = true;
+        }
+        // self-test: rank r contributes r + 1 (and 1); every rank must read nr (nr + 1) / 2, nr
+        DevBuf<double> t(2);
+        const double tv[2] = {(double)(rk + 1), 1.0};
+        RSVIO_HIP(hipMemcpy(t.p, tv, sizeof tv, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, 2, P, ++p2p_gen, d_p2p_err.p);
+        RSVIO_HIP(hipGetLastError());
+        double out[2] = {0.0, 0.0};
+        RSVIO_HIP(hipMemcpyAsync(out, t.p, sizeof out, hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+        p2p_check();
+        if (out[0] != nr * (nr + 1) / 2.0 || out[1] != (double)nr)
+            throw std::runtime_error("P2P all-reduce self-test returned wrong sums");
+        p2p = P;
+        nranks = nr;
+        rank = rk;
+        coll = 2;
+    }
+
+    void p2p_detach() {
+        if (coll == 2) coll = comm ? 1 : 0;
     }
 
     // run on a caller-owned stream (e.g. one restricted to a CU subset); nullptr = own stream
@@ -1976,8 +2108,40 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
         }
         B.nranks = nranks;
         B.rank = rank;
+        B.coll = 1;
         return (int)RSVIO_OK;
     });
+}
+
+int rsvio_ba_p2p_export(rsvio_ba* ba, int32_t nranks, uint8_t* handle_out, size_t cap) {
+    if (!ba || !handle_out || cap < sizeof(hipIpcMemHandle_t)) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        hipIpcMemHandle_t h;
+        ba->b.p2p_export(nranks, &h);
+        __builtin_memcpy(handle_out, &h, sizeof h);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* handles) {
+    if (!ba || !handles) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        std::vector<hipIpcMemHandle_t> hs(nranks > 0 ? nranks : 1);
+        for (int r = 0; r < nranks; ++r) __builtin_memcpy(&hs[r], handles + (size_t)r * sizeof(hipIpcMemHandle_t), sizeof(hipIpcMemHandle_t));
+        try {
+            ba->b.p2p_attach(nranks, rank, hs.data());
+        } catch (const std::exception& e) {
+            rsvio::set_last_error(std::string("P2P attach failed: ") + e.what());
+            return (int)RSVIO_ERR_RCCL;
+        }
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_detach_p2p(rsvio_ba* ba) {
+    if (!ba) return RSVIO_ERR_INVALID_ARG;
+    ba->b.p2p_detach();
+    return RSVIO_OK;
 }
 
 }  // extern "C"

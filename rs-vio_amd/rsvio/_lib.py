@@ -90,6 +90,9 @@ SIG = {
     "rsvio_ba_run": (C.c_int, [P, C.POINTER(LmCfg), C.POINTER(BaResult)]),
     "rsvio_ba_run_async": (C.c_int, [P, C.POINTER(LmCfg)]),
     "rsvio_ba_set_stream": (C.c_int, [P, P]),
+    "rsvio_ba_p2p_export": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint8), C.c_size_t]),
+    "rsvio_ba_attach_p2p": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
+    "rsvio_ba_detach_p2p": (C.c_int, [P]),
     "rsvio_stream_create": (C.c_int, [C.c_int32, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(P)]),
     "rsvio_stream_destroy": (C.c_int, [P]),
     "rsvio_ba_wait": (C.c_int, [P, C.POINTER(BaResult)]),

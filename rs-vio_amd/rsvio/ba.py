@@ -55,6 +55,22 @@ class BundleAdjuster:
         buf = (C.c_uint8 * len(unique_id)).from_buffer_copy(unique_id)
         check(_lib.load().rsvio_ba_attach_comm(self._h, nranks, rank, buf))
 
+    def p2p_export(self, nranks: int) -> bytes:
+        """IPC handle (64 bytes) of this handle's P2P exchange buffer (rsvio_ba_p2p_export)."""
+        buf = (C.c_uint8 * 64)()
+        check(_lib.load().rsvio_ba_p2p_export(self._h, nranks, buf, 64))
+        return bytes(buf)
+
+    def attach_p2p(self, nranks: int, rank: int, handles) -> None:
+        """Switch the sharded exchanges to the P2P one-shot all-reduce (self-tested; raises
+        RsvioError and keeps the previous collective on failure)."""
+        blob = b"".join(handles)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(_lib.load().rsvio_ba_attach_p2p(self._h, nranks, rank, buf))
+
+    def detach_p2p(self) -> None:
+        check(_lib.load().rsvio_ba_detach_p2p(self._h))
+
     @staticmethod
     def rccl_unique_id() -> bytes:
         buf = (C.c_uint8 * 128)()

@@ -210,3 +210,53 @@ def test_async_solve_equals_run(gpu, cfg3):
     with pytest.raises(Exception):
         a.wait()  # nothing in flight
     a.close()
+
+
+def _p2p_worker(rank, world, port, out_dir):
+    import os
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rsvio import synthetic as S
+        from rsvio.ba import BundleAdjuster
+        full = S.ba_problem()
+        shard = full.shard(rank, world)
+        ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
+        mine = ba.p2p_export(world)
+        handles = [None] * world
+        dist.all_gather_object(handles, mine)
+        ba.attach_p2p(world, rank, handles)
+        ba.set_problem_from(shard)
+        r = ba.run()
+        pose, pw = ba.state()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), pose=pose, pw=pw,
+                 res=np.array([r.status, r.iterations, r.final_cost, r.initial_cost]))
+        ba.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
+    """The landmark-sharded BA with the P2P one-shot all-reduce, 2 ranks (2 processes on one
+    GPU: the exchange buffers are IPC-shared): both ranks end with the same poses, and the
+    gathered solution matches the oracle's single-problem solve within the config-3 tolerances."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_p2p_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = np.load(tmp_path / "r0.npz"), np.load(tmp_path / "r1.npz")
+    assert np.array_equal(r0["pose"], r1["pose"]) and np.array_equal(r0["res"], r1["res"])
+    po, pwo, ro = oracle.ba_solve(cfg3)
+    status, iters = int(r0["res"][0]), int(r0["res"][1])
+    assert status == ro.status and iters == ro.iterations
+    assert abs(r0["res"][2] - ro.final_cost) <= 1e-8 * ro.initial_cost
+    assert np.abs(r0["pose"] - po).max() < 1e-7
+    pw = np.concatenate([r0["pw"], r1["pw"]])
+    assert np.abs(pw - pwo).max() < 1e-6
