@@ -80,15 +80,20 @@ def pmc_traffic(kernel: str):
     return k["fetch_size_bytes_per_dispatch"] + k["write_size_bytes_per_dispatch"], files[-1].name
 
 
-def setup_dist():
+def setup_dist(same_device: bool = False):
+    """One process per GPU over RCCL.  `same_device` is a rehearsal mode for a one-GPU box: every
+    rank on cuda:0 with a gloo control group (RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if same_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -102,14 +107,19 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def max_over_ranks(x: float, world: int) -> float:
+def reduce_scalar(x: float, world: int, op: str = "max") -> float:
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
     return float(t.item())
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    return reduce_scalar(x, world, "max")
 
 
 def cu_partition(device: int, frac: float, layout: str):
@@ -221,7 +231,8 @@ class TrackerWorkload:
 
 
 class BAWorkload:
-    def __init__(self, device: int, world: int, rank: int, stream_ptr=None):
+    def __init__(self, device: int, world: int, rank: int, stream_ptr=None, collective: str = "auto",
+                 rccl_ok: bool = True):
         from rsvio import synthetic as S
         from rsvio.ba import BundleAdjuster
         t0 = time.time()
@@ -232,16 +243,51 @@ class BAWorkload:
             f"(global {full.n_lm}/{full.n_obs}) built in {time.time() - t0:.1f}s")
         self.ba = BundleAdjuster(max_keyframes=full.n_kf, max_landmarks=self.prob.n_lm,
                                  max_observations=self.prob.n_obs, device=device)
+        self.collective = "none"
         if world > 1:
-            import torch.distributed as dist
-            obj = [BundleAdjuster.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            self.ba.attach_comm(world, rank, obj[0])
+            self.collective = self._attach(world, rank, collective, rccl_ok)
+            log(f"[bench] rank {rank}: BA exchange = {self.collective}")
         if stream_ptr:
             self.ba.set_stream(stream_ptr)
         self.ba.set_problem_from(self.prob)
         self.iters = []
         self.solve_ms = []
+
+    def _attach(self, world, rank, collective, rccl_ok):
+        """RCCL communicator first (the fallback), then the P2P one-shot all-reduce when every rank
+        can map every peer's exchange buffer; all ranks agree on the outcome."""
+        import torch.distributed as dist
+        from rsvio.ba import BundleAdjuster
+        have_rccl = False
+        if collective in ("auto", "rccl") and rccl_ok:
+            obj = [BundleAdjuster.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            self.ba.attach_comm(world, rank, obj[0])
+            have_rccl = True
+        if collective == "rccl":
+            return "rccl"
+        mine = None
+        try:
+            mine = self.ba.p2p_export(world)
+        except Exception as e:  # noqa: BLE001 - reported, then agreed on below
+            log(f"[bench] rank {rank}: p2p export failed: {e}")
+        handles = [None] * world
+        dist.all_gather_object(handles, mine)
+        ok = all(h is not None for h in handles)
+        if ok:
+            try:
+                self.ba.attach_p2p(world, rank, handles)
+            except Exception as e:  # noqa: BLE001
+                log(f"[bench] rank {rank}: p2p attach failed: {e}")
+                ok = False
+        all_ok = reduce_scalar(1.0 if ok else 0.0, world, "min") > 0.5
+        if all_ok:
+            return "p2p"
+        if ok:
+            self.ba.detach_p2p()
+        if not have_rccl:
+            raise RuntimeError("P2P exchange unavailable and no RCCL communicator attached")
+        return "rccl"
 
     def start(self):
         self.ba.run_async()
@@ -299,9 +345,15 @@ def main():
     ap.add_argument("--cu-split", type=float, default=0.5,
                     help="fraction of CUs given to the tracker stream (0: no CU partition)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
+    ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "p2p"],
+                    help="BA exchange for N>1: P2P one-shot all-reduce (auto: if every rank attaches) or RCCL")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: all ranks on cuda:0, gloo control group, P2P exchange")
     args = ap.parse_args()
+    if args.same_device:
+        args.collective = "p2p"
 
-    world, rank, local = setup_dist()
+    world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     import torch
@@ -316,8 +368,10 @@ def main():
         streams = [CuStream(local, cu_trk), CuStream(local, cu_ba)]
         log(f"[bench] CU partition ({args.cu_layout}): tracker {len(cu_trk)} CUs, BA {len(cu_ba)} CUs")
     trk = TrackerWorkload(local, streams[0].ptr if streams else None)
-    ba = BAWorkload(local, world, rank, streams[1].ptr if streams else None)
+    ba = BAWorkload(local, world, rank, streams[1].ptr if streams else None, args.collective,
+                    rccl_ok=not args.same_device)
 
+    barrier(world)
     # one step: the BA solve is enqueued first (its stream), the frame's tracking is enqueued on
     # the tracker stream while it runs, then the host completes the solve
     for _ in range(args.warmup):
@@ -365,7 +419,8 @@ def main():
                                "(24,000 obs/GPU), Schur LM <= 20 it; every frame a keyframe",
                    "image": "752x480", "features": NFEAT, "levels": LEVELS, "keyframes": 10,
                    "landmarks_per_gpu": prob.n_lm, "observations_per_gpu": prob.n_obs,
-                   "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s) (RCCL)",
+                   "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s)"
+                                   + (f" ({ba.collective} all-reduce)" if world > 1 else ""),
                    "cu_partition": (f"{args.cu_layout} {args.cu_split:g} of CUs to the tracker stream"
                                     if args.cu_split > 0 else "none")},
         "ba_ms_per_iter": round(ba_ms_iter, 4),
