@@ -129,6 +129,41 @@ typedef struct {
 int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, int32_t n_batches,
                          int32_t max_iterations, float thresh, void* stream);
 
+/* ================= T12: camera unprojection (Frame::add_*_feature) ================= */
+
+/* Camera models of src/datasets/mod.rs:93-163 (camera-intrinsic-model 0.7.2):
+ *   RSVIO_CAM_OPENCV5  OpenCVModel5, params {fx, fy, cx, cy, k1, k2, p1, p2, k3} (pinhole-radtan)
+ *   RSVIO_CAM_EUCM     EUCM,         params {fx, fy, cx, cy, alpha, beta}
+ * unproject_one's return convention is not verifiable offline, so it is
+ * a parameter: RSVIO_UNPROJ_PLANE gives (x/z, y/z), RSVIO_UNPROJ_RAY the first two components
+ * of the unit ray.  frame.rs:118-119,131-132 keep components [0..2] as f32. */
+enum { RSVIO_CAM_OPENCV5 = 0, RSVIO_CAM_EUCM = 1 };
+enum { RSVIO_UNPROJ_PLANE = 0, RSVIO_UNPROJ_RAY = 1 };
+
+typedef struct {
+    int32_t model;           /* RSVIO_CAM_* */
+    int32_t convention;      /* RSVIO_UNPROJ_* */
+    int32_t max_iterations;  /* radtan Newton cap; <= 0 means 20 */
+    int32_t reserved;
+    double params[9];
+} rsvio_camera;              /* 88 bytes */
+
+/* Batched unproject_one (frame.rs:107-134): pixels (n x 2 f32, cast to f64 as frame.rs:118)
+ * -> undistorted (n x 2 f32).  Failure of one point (EUCM outside its valid cone, radtan
+ * Newton not converging, non-finite) gives NaN coordinates and valid_out = 0 (valid_out may be
+ * NULL).  Host buffers, current device. */
+int rsvio_unproject(const rsvio_camera* cam, const float* px, size_t n, float* out_xy,
+                    uint8_t* valid_out);
+/* Same on device pointers, enqueued on `stream` (hipStream_t; NULL = legacy stream). */
+int rsvio_unproject_d(const rsvio_camera* cam, const float* d_px, size_t n, float* d_out_xy,
+                      uint8_t* d_valid_out, void* stream);
+/* Frame::add_left_feature / add_right_feature on the tracker's output: after this call every
+ * process_frame also unprojects both cameras' features on device (fused into the output
+ * packing) and rsvio_tracker_undistorted returns them in feature order.  NULL, NULL turns it
+ * off. */
+int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const rsvio_camera* right);
+int rsvio_tracker_undistorted(rsvio_tracker* t, float* out_l, size_t cap_l, float* out_r, size_t cap_r);
+
 /* =========================== HP-B: sliding-window BA =========================== */
 
 enum {

@@ -32,7 +32,14 @@ class OrcFeature(C.Structure):
     _fields_ = [("id", C.c_uint64), ("x", C.c_float), ("y", C.c_float), ("aff", C.c_float * 6)]
 
 
+class OrcCamera(C.Structure):
+    _fields_ = [("model", C.c_int32), ("convention", C.c_int32), ("max_iterations", C.c_int32),
+                ("reserved", C.c_int32), ("params", C.c_double * 9)]
+
+
 _SIG = {
+    "orc_unproject": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
+    "orc_project": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
     "orc_set_trig_mode": (None, [C.c_int]),
     "orc_se2_exp": (None, [P, P]),
     "orc_pyramid_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
@@ -183,6 +190,31 @@ class StereoTracker:
             load().orc_tracker_destroy(self.h)
         except Exception:
             pass
+
+
+def camera(model: int, params, convention: int = 0, max_iterations: int = 20) -> OrcCamera:
+    c = OrcCamera()
+    c.model, c.convention, c.max_iterations = model, convention, max_iterations
+    for i, v in enumerate(params):
+        c.params[i] = float(v)
+    return c
+
+
+def unproject(cam: OrcCamera, px):
+    """frame.rs:118-119 restated: n x 2 f32 pixels -> (n x 2 f32 undistorted, valid bool)."""
+    px = np.ascontiguousarray(px, np.float32).reshape(-1, 2)
+    out = np.zeros_like(px)
+    valid = np.zeros(len(px), np.uint8)
+    load().orc_unproject(C.byref(cam), _p(px), len(px), _p(out), _p(valid))
+    return out, valid.astype(bool)
+
+
+def project(cam: OrcCamera, pts):
+    pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+    out = np.zeros((len(pts), 2), np.float64)
+    valid = np.zeros(len(pts), np.uint8)
+    load().orc_project(C.byref(cam), _p(pts), len(pts), _p(out), _p(valid))
+    return out, valid.astype(bool)
 
 
 def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):

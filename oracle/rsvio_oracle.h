@@ -93,6 +93,24 @@ int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t
                               orc_feature* out_r, int cap_r, int* n_r);
 void orc_tracker_remove_ids(orc_tracker* t, const uint64_t* ids, int n);
 
+/* ---------------- camera unprojection (src/estimator/frame.rs:107-134) ---------------- */
+
+/* Same layout as rsvio_camera (include/rsvio_gpu.h): model 0 = OpenCVModel5
+ * {fx,fy,cx,cy,k1,k2,p1,p2,k3}, 1 = EUCM {fx,fy,cx,cy,alpha,beta}; convention 0 = (x/z, y/z),
+ * 1 = unit-ray components.  Parity unpinned (camera_oracle.cpp header). */
+typedef struct {
+    int32_t model;
+    int32_t convention;
+    int32_t max_iterations;
+    int32_t reserved;
+    double params[9];
+} orc_camera;
+
+/* px: n x 2 f32 pixels -> out_xy n x 2 f32 (NaN + valid 0 on failure); returns #valid */
+int orc_unproject(const orc_camera* cam, const float* px, size_t n, float* out_xy, uint8_t* valid);
+/* pts: n x 3 f64 camera-frame points -> out_uv n x 2 f64 pixels; returns #valid */
+int orc_project(const orc_camera* cam, const double* pts, size_t n, double* out_uv, uint8_t* valid);
+
 /* ---------------- bundle adjustment (src/optimization/factors.rs, sliding_window.rs) ---------------- */
 
 typedef struct {

@@ -15,6 +15,7 @@
 // Canonical order: track maps are kept sorted by id; new ids are assigned in detection scan
 // order (the reference's HashMap iteration order is random, feature_tracker.rs:162-170).
 #include <cmath>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -22,6 +23,7 @@
 
 #include "lk_track.hpp"
 #include "pyramid.hpp"
+#include "camera.hpp"
 
 namespace rsvio {
 
@@ -238,13 +240,19 @@ __global__ __launch_bounds__(1024) void gather_new_kernel(const int4* __restrict
     if (threadIdx.x == 0) *new_count = total;
 }
 
+struct CamPair {
+    rsvio_camera cam[2];
+    int on;
+};
+
 // feature_tracker.rs:162-170 in canonical order, then get_track_points packing.
 __global__ __launch_bounds__(1024) void append_pack_kernel(
     const float* __restrict__ new_aff0, const float* __restrict__ new_aff1,
     const uint8_t* __restrict__ new_valid, const int* __restrict__ new_count, float* __restrict__ map_aff0,
     float* __restrict__ map_aff1, uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
     int* __restrict__ counts, unsigned long long* __restrict__ last_id, int capacity,
-    rsvio_feature* __restrict__ out0, rsvio_feature* __restrict__ out1, int* __restrict__ overflow) {
+    rsvio_feature* __restrict__ out0, rsvio_feature* __restrict__ out1, int* __restrict__ overflow,
+    CamPair cams, float2* __restrict__ und0, float2* __restrict__ und1) {
     __shared__ int sh[1024];
     const int m = *new_count;
     const int per = (m + blockDim.x - 1) / blockDim.x;
@@ -281,17 +289,20 @@ __global__ __launch_bounds__(1024) void append_pack_kernel(
         counts[1] = n1;
         *last_id = base + (unsigned long long)total;
     }
-    for (int i = threadIdx.x; i < n0; i += blockDim.x) {
-        const float* a = map_aff0 + 6 * i;
+    // get_track_points packing, both cameras spread over the block; with cameras attached the
+    // Frame::add_{left,right}_feature unprojection (frame.rs:118-119,131-132) is fused here
+    for (int j = threadIdx.x; j < n0 + n1; j += blockDim.x) {
+        const int c = j < n0 ? 0 : 1;
+        const int i = c == 0 ? j : j - n0;
+        const float* a = (c == 0 ? map_aff0 : map_aff1) + 6 * i;
         rsvio_feature f;
-        f.id = ids0[i]; f.x = a[4]; f.y = a[5]; f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
-        out0[i] = f;
-    }
-    for (int i = threadIdx.x; i < n1; i += blockDim.x) {
-        const float* a = map_aff1 + 6 * i;
-        rsvio_feature f;
-        f.id = ids1[i]; f.x = a[4]; f.y = a[5]; f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
-        out1[i] = f;
+        f.id = (c == 0 ? ids0 : ids1)[i]; f.x = a[4]; f.y = a[5];
+        f.r[0] = a[0]; f.r[1] = a[1]; f.r[2] = a[2]; f.r[3] = a[3];
+        (c == 0 ? out0 : out1)[i] = f;
+        if (cams.on) {
+            const Undist u = unproject_one(cams.cam[c], f.x, f.y);
+            (c == 0 ? und0 : und1)[i] = make_float2(u.x, u.y);
+        }
     }
 }
 
@@ -363,6 +374,10 @@ struct Tracker {
     DevBuf<unsigned long long> last_id;
     DevBuf<rsvio_feature> out;
     HostBuf<int> h_counts;
+    CamPair cams{};                 // T12 unprojection fused into append_pack_kernel when on
+    DevBuf<float2> undist;          // 2 x cap
+    HostBuf<float2> h_undist;       // last process_frame's undistorted coordinates
+    size_t last_n[2] = {0, 0};
 
     uint8_t* pyr(int slot, int cam) { return d_pyr.p + (size_t)(2 * slot + cam) * pyr_bytes; }
 
@@ -456,7 +471,7 @@ struct Tracker {
         }
         hipLaunchKernelGGL(append_pack_kernel, dim3(1), dim3(1024), 0, stream, new_aff.p, new_aff1.p, new_valid.p,
                            new_count.p, maff(0), maff(1), mid(0), mid(1), counts.p, last_id.p, cap, out.p,
-                           out.p + cap, overflow.p);
+                           out.p + cap, overflow.p, cams, undist.p, undist.p + (cams.on ? cap : 0));
         RSVIO_HIP(hipGetLastError());
         cur = nxt;
         has_prev = true;
@@ -471,7 +486,15 @@ struct Tracker {
         const size_t nl = std::min((size_t)host_count[0], cap_l), nr = std::min((size_t)host_count[1], cap_r);
         if (nl) RSVIO_HIP(hipMemcpyAsync(out_l, out.p, nl * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
         if (nr) RSVIO_HIP(hipMemcpyAsync(out_r, out.p + cap, nr * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
+        if (cams.on) {
+            if (nl) RSVIO_HIP(hipMemcpyAsync(h_undist.p, undist.p, nl * sizeof(float2), hipMemcpyDeviceToHost, stream));
+            if (nr)
+                RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap, undist.p + cap, nr * sizeof(float2), hipMemcpyDeviceToHost,
+                                         stream));
+        }
         RSVIO_HIP(hipStreamSynchronize(stream));
+        last_n[0] = cams.on ? nl : 0;
+        last_n[1] = cams.on ? nr : 0;
         *n_l = nl;
         *n_r = nr;
     }
@@ -584,6 +607,44 @@ int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left, 
         t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
         return (int)RSVIO_OK;
     });
+}
+
+int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const rsvio_camera* right) {
+    if (!t || (!left) != (!right)) return RSVIO_ERR_INVALID_ARG;
+    if (left && (!rsvio::camera_ok(left) || !rsvio::camera_ok(right))) {
+        rsvio::set_last_error("rsvio_tracker_set_cameras: invalid camera");
+        return RSVIO_ERR_INVALID_ARG;
+    }
+    return guarded([&] {
+        auto& T = t->t;
+        RSVIO_HIP(hipStreamSynchronize(T.stream));
+        if (!left) {
+            T.cams.on = 0;
+            T.last_n[0] = T.last_n[1] = 0;
+            return (int)RSVIO_OK;
+        }
+        if (!T.undist.p) {
+            T.undist.alloc((size_t)2 * T.cap);
+            T.h_undist.alloc((size_t)2 * T.cap);
+        }
+        T.cams.cam[0] = *left;
+        T.cams.cam[1] = *right;
+        T.cams.on = 1;
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_undistorted(rsvio_tracker* t, float* out_l, size_t cap_l, float* out_r, size_t cap_r) {
+    if (!t || (cap_l && !out_l) || (cap_r && !out_r)) return RSVIO_ERR_INVALID_ARG;
+    auto& T = t->t;
+    if (!T.cams.on) {
+        rsvio::set_last_error("rsvio_tracker_undistorted: no cameras attached");
+        return RSVIO_ERR_INVALID_ARG;
+    }
+    if (cap_l < T.last_n[0] || cap_r < T.last_n[1]) return RSVIO_ERR_CAPACITY;
+    std::memcpy(out_l, T.h_undist.p, T.last_n[0] * sizeof(float2));
+    std::memcpy(out_r, T.h_undist.p + T.cap, T.last_n[1] * sizeof(float2));
+    return RSVIO_OK;
 }
 
 int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n) {

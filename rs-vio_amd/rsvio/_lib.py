@@ -55,6 +55,11 @@ class BaResult(C.Structure):
                 ("final_cost", C.c_double), ("solve_ms", C.c_double)]
 
 
+class Camera(C.Structure):
+    _fields_ = [("model", C.c_int32), ("convention", C.c_int32), ("max_iterations", C.c_int32),
+                ("reserved", C.c_int32), ("params", C.c_double * 9)]
+
+
 class BaParams(C.Structure):
     _fields_ = [("max_keyframes", C.c_int32), ("max_landmarks", C.c_int32),
                 ("max_observations", C.c_int32), ("device", C.c_int32)]
@@ -72,6 +77,10 @@ SIG = {
                                                      C.c_size_t, C.POINTER(C.c_size_t)]),
     "rsvio_tracker_remove_ids": (C.c_int, [P, P, C.c_size_t]),
     "rsvio_tracker_stream": (P, [P]),
+    "rsvio_unproject": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P]),
+    "rsvio_unproject_d": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P, P]),
+    "rsvio_tracker_set_cameras": (C.c_int, [P, C.POINTER(Camera), C.POINTER(Camera)]),
+    "rsvio_tracker_undistorted": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
     "rsvio_pyramid_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
     "rsvio_build_pyramid": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, P]),
     "rsvio_track_points": (C.c_int, [P, P, C.c_int32, C.c_int32, C.c_int32, P, C.c_int32, C.c_int32, C.c_float,

@@ -121,6 +121,24 @@ class StereoPatchTracker:
         return [{int(f["id"]): (float(f["x"]), float(f["y"])) for f in l},
                 {int(f["id"]): (float(f["x"]), float(f["y"])) for f in r}]
 
+    def set_cameras(self, left, right):
+        """Attach the frame's camera models (rsvio.camera.Camera); every process_frame then also
+        computes Frame::add_{left,right}_feature's undistorted coordinates on device."""
+        if left is None:
+            check(_lib.load().rsvio_tracker_set_cameras(self._h, None, None))
+            self._cams = False
+            return
+        self._cl, self._cr = left.struct(), right.struct()
+        check(_lib.load().rsvio_tracker_set_cameras(self._h, C.byref(self._cl), C.byref(self._cr)))
+        self._cams = True
+
+    def undistorted(self):
+        """(n_l x 2, n_r x 2) f32 undistorted coordinates of the last process_frame's features."""
+        ul = np.zeros((self._n[0], 2), np.float32)
+        ur = np.zeros((self._n[1], 2), np.float32)
+        check(_lib.load().rsvio_tracker_undistorted(self._h, ptr(ul), self._n[0], ptr(ur), self._n[1]))
+        return ul, ur
+
     def remove_id(self, ids):
         ids = np.ascontiguousarray(ids, np.uint64)
         check(_lib.load().rsvio_tracker_remove_ids(self._h, ptr(ids), len(ids)))

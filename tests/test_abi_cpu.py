@@ -45,6 +45,15 @@ def test_struct_layouts():
     assert C.sizeof(_lib.Feature) == 32
     assert C.sizeof(_lib.TrackerParams) == 32
     assert C.sizeof(_lib.TrackBatch) == 48
+    assert C.sizeof(_lib.Camera) == 88
+
+
+def test_camera_struct_matches_oracle_layout():
+    from oracle import oracle as O
+    from rsvio import _lib
+    assert C.sizeof(O.OrcCamera) == C.sizeof(_lib.Camera)
+    for (a, ta), (b, tb) in zip(O.OrcCamera._fields_, _lib.Camera._fields_):
+        assert a == b and C.sizeof(ta) == C.sizeof(tb)
 
 
 def test_invalid_arguments_rejected_without_device():
@@ -57,3 +66,9 @@ def test_invalid_arguments_rejected_without_device():
     assert lib.rsvio_detect_keypoints(img.ctypes.data, 10, 10, 4, None, 0, None, None, 0, C.byref(n)) == -1
     assert lib.rsvio_pyramid_bytes(752, 480, 3) == 752 * 480 + 376 * 240 + 188 * 120
     assert lib.rsvio_ba_solve(None, 0, None, None, 0, None, 0, None, None, None, None, None, None, None) == -1
+    cam = _lib.Camera()
+    cam.model = 7
+    assert lib.rsvio_unproject(C.byref(cam), None, 0, None, None) == -1      # unknown model
+    cam.model, cam.params[0], cam.params[1] = 0, 0.0, 1.0
+    assert lib.rsvio_unproject(C.byref(cam), None, 0, None, None) == -1      # fx == 0
+    assert lib.rsvio_tracker_set_cameras(None, None, None) == -1
