@@ -246,6 +246,51 @@ int rsvio_ba_p2p_export(rsvio_ba* ba, int32_t nranks, uint8_t* handle_out, size_
 int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* handles);
 int rsvio_ba_detach_p2p(rsvio_ba* ba);
 
+/* ===== B8: motion tracking (PnP) + keyframe rule (SlidingWindow::track_motion) ===== */
+
+/* One SE3 pose (T_B_W) against the fixed map: PnPFactor (src/optimization/factors.rs:455-583,
+ * no cheirality guard, J = [dt | dw]) with Huber(2.0), the build's LM with
+ * max 10 iterations (sliding_window.rs:494-501), initialised from the last keyframe
+ * (:506-517); then the keyframe rule of estimator.rs:195-226.  The whole sequence -- map join,
+ * LM, T_W_B = inverse(SE3), T_rel, euler angles, thresholds -- is one single-workgroup kernel. */
+typedef struct rsvio_pnp rsvio_pnp;
+
+typedef struct {
+    double translation_threshold;  /* keyframe_management.translation_threshold (euroc 0.05) */
+    double rotation_threshold;     /* keyframe_management.rotation_threshold    (euroc 0.05) */
+} rsvio_keyframe_rule;
+
+typedef struct {
+    int32_t status;            /* RSVIO_LM_*; > 0 or TRUST_REGION is success (:384-395) */
+    int32_t iterations;
+    int32_t is_keyframe;       /* estimator.rs:216-225; 1 on failure (frame keeps is_keyframe) */
+    int32_t n_observations;    /* features with a map point (:521-547) */
+    double initial_cost;
+    double final_cost;
+    double translation_norm;   /* ||t_rel|| (estimator.rs:206) */
+    double rotation_norm;      /* ||euler(R_rel)|| (:207-212) */
+    double T_W_B[16];          /* row-major; identity on failure (frame.rs:95, state.rs:26) */
+} rsvio_motion_result;        /* 176 bytes */
+
+int rsvio_pnp_create(int32_t device, rsvio_pnp** out);
+void rsvio_pnp_destroy(rsvio_pnp* p);
+/* SlidingWindow::map_points after optimize (sliding_window.rs:466-475): feature ids strictly
+ * ascending, p_W as f32 triples. */
+int rsvio_pnp_set_map(rsvio_pnp* p, const uint64_t* ids, const float* p_W, int32_t n);
+/* track_motion(&Frame) + keyframe rule for a frame given as host arrays (feature ids and
+ * undistorted coordinates per camera, frame.rs:107-134).  T_W_B_last_kf: keyframes.back()
+ * (:506); T_C_B2: T_Cl_B, T_Cr_B of keyframes.front() (:520-521), row-major 4x4 each. */
+int rsvio_track_motion(rsvio_pnp* p, const uint64_t* ids_l, const float* uv_l, size_t n_l,
+                       const uint64_t* ids_r, const float* uv_r, size_t n_r,
+                       const double* T_W_B_last_kf, const double* T_C_B2, const rsvio_lm_cfg* cfg,
+                       const rsvio_keyframe_rule* rule, rsvio_motion_result* res);
+/* Same for the tracker's last frame, read in place on the device (ids, counts and the fused
+ * undistorted coordinates; needs rsvio_tracker_set_cameras): no host round trip between
+ * tracking and motion tracking.  Runs on the tracker's stream. */
+int rsvio_track_motion_tracker(rsvio_pnp* p, rsvio_tracker* t, const double* T_W_B_last_kf,
+                               const double* T_C_B2, const rsvio_lm_cfg* cfg,
+                               const rsvio_keyframe_rule* rule, rsvio_motion_result* res);
+
 #ifdef __cplusplus
 }
 #endif

@@ -517,3 +517,220 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// B8: SlidingWindow::track_motion (sliding_window.rs:490-587) + keyframe rule
+// (estimator.rs:195-234).  PnPFactor::linearize (factors.rs:527-578): no cheirality guard.
+static void pnp_linearize(const double* pW, const Pose& P, const double* TCB, const double* uv, double r[2],
+                          double J[2][6]) {
+    double RCB[3][3] = {{TCB[0], TCB[1], TCB[2]}, {TCB[4], TCB[5], TCB[6]}, {TCB[8], TCB[9], TCB[10]}};
+    double pB[3], pC[3], tmp[3];
+    mat3vec(P.R, pW, tmp);
+    for (int i = 0; i < 3; ++i) pB[i] = tmp[i] + P.t[i];
+    mat3vec(RCB, pB, tmp);
+    pC[0] = tmp[0] + TCB[3];
+    pC[1] = tmp[1] + TCB[7];
+    pC[2] = tmp[2] + TCB[11];
+    r[0] = pC[0] / pC[2] - uv[0];
+    r[1] = pC[1] / pC[2] - uv[1];
+    double iz = 1.0 / pC[2];
+    double iz2 = iz * iz;
+    double Jp[2][3] = {{iz, 0.0, -pC[0] * iz2}, {0.0, iz, -pC[1] * iz2}};
+    double A[2][3], M[3][3];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j) A[i][j] = (Jp[i][0] * RCB[0][j] + Jp[i][1] * RCB[1][j]) + Jp[i][2] * RCB[2][j];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j) J[i][j] = (A[i][0] * P.R[0][j] + A[i][1] * P.R[1][j]) + A[i][2] * P.R[2][j];
+    double S[3][3] = {{0.0, -pW[2], pW[1]}, {pW[2], 0.0, -pW[0]}, {-pW[1], pW[0], 0.0}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            M[i][j] = ((-P.R[i][0]) * S[0][j] + (-P.R[i][1]) * S[1][j]) + (-P.R[i][2]) * S[2][j];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 3; ++j) J[i][3 + j] = (A[i][0] * M[0][j] + A[i][1] * M[1][j]) + A[i][2] * M[2][j];
+}
+
+struct PnpObs {
+    double pW[3], uv[2];
+    int cam;
+};
+
+// H (6x6), g, cost over the factor list, sequentially in factor order
+static void pnp_system(const std::vector<PnpObs>& obs, const Pose& P, const double* TCB2, double delta, double H[36],
+                       double g[6], double* cost) {
+    for (int k = 0; k < 36; ++k) H[k] = 0.0;
+    for (int k = 0; k < 6; ++k) g[k] = 0.0;
+    *cost = 0.0;
+    for (const PnpObs& o : obs) {
+        double r[2], J[2][6];
+        pnp_linearize(o.pW, P, TCB2 + 16 * o.cam, o.uv, r, J);
+        double s = r[0] * r[0] + r[1] * r[1], rho, w;
+        huber(s, delta, &rho, &w);
+        *cost += 0.5 * rho;
+        double wr[2] = {w * r[0], w * r[1]};
+        for (int a = 0; a < 6; ++a) {
+            for (int c = 0; c < 6; ++c) H[a * 6 + c] += w * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
+            g[a] += J[0][a] * wr[0] + J[1][a] * wr[1];
+        }
+    }
+}
+
+static void rigid_inverse(const double* T, double* Ti) {
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) Ti[4 * i + j] = T[4 * j + i];
+        Ti[4 * i + 3] = -((T[i] * T[3] + T[4 + i] * T[7]) + T[8 + i] * T[11]);
+    }
+    Ti[12] = 0.0; Ti[13] = 0.0; Ti[14] = 0.0; Ti[15] = 1.0;
+}
+
+// nalgebra Rotation3::euler_angles -> (roll, pitch, yaw), returned as its Euclidean norm
+static double euler_norm(const double R[3][3]) {
+    double roll, pitch, yaw;
+    if (std::fabs(R[2][0]) < 1.0) {
+        pitch = -std::asin(R[2][0]);
+        double c = std::cos(pitch);
+        roll = std::atan2(R[2][1] / c, R[2][2] / c);
+        yaw = std::atan2(R[1][0] / c, R[0][0] / c);
+    } else if (R[2][0] <= -1.0) {
+        roll = std::atan2(R[0][1], R[0][2]);
+        pitch = M_PI_2;
+        yaw = 0.0;
+    } else {
+        roll = -std::atan2(-R[0][1], -R[0][2]);
+        pitch = -M_PI_2;
+        yaw = 0.0;
+    }
+    return std::sqrt((roll * roll + pitch * pitch) + yaw * yaw);
+}
+
+extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_l, const uint64_t* ids_r,
+                                const float* uv_r, int n_r, const uint64_t* map_ids, const float* map_pw, int n_map,
+                                const double* T_last, const double* TCB2, const orc_lm_cfg* cfg, double thr_t,
+                                double thr_r, orc_motion_result* res) {
+    // the factor list (sliding_window.rs:519-547): left then right, features with a map point;
+    // map_points.get(id) restated as a search of the ascending id list
+    std::vector<PnpObs> obs;
+    for (int c = 0; c < 2; ++c) {
+        const uint64_t* ids = c == 0 ? ids_l : ids_r;
+        const float* uv = c == 0 ? uv_l : uv_r;
+        int n = c == 0 ? n_l : n_r;
+        for (int i = 0; i < n; ++i) {
+            const uint64_t* it = std::lower_bound(map_ids, map_ids + n_map, ids[i]);
+            if (it == map_ids + n_map || *it != ids[i]) continue;
+            size_t k = (size_t)(it - map_ids);
+            PnpObs o;
+            for (int a = 0; a < 3; ++a) o.pW[a] = (double)map_pw[3 * k + a];  // point[a] as f64 (:530-535)
+            o.uv[0] = (double)uv[2 * i];                                       // undistorted_coord cast (:529)
+            o.uv[1] = (double)uv[2 * i + 1];
+            o.cam = c;
+            obs.push_back(o);
+        }
+    }
+    res->n_observations = (int)obs.size();
+    res->iterations = 0;
+    res->initial_cost = res->final_cost = 0.0;
+    res->translation_norm = res->rotation_norm = 0.0;
+    // initial pose: the last keyframe's T_B_W (:506-517)
+    double TBW0[16], x[7], xt[7];
+    rigid_inverse(T_last, TBW0);
+    double R0[9] = {TBW0[0], TBW0[1], TBW0[2], TBW0[4], TBW0[5], TBW0[6], TBW0[8], TBW0[9], TBW0[10]};
+    x[0] = TBW0[3]; x[1] = TBW0[7]; x[2] = TBW0[11];
+    orc_quat_from_rotation(R0, x + 3);
+    int status = LM_MAX_ITERS;
+    if (obs.empty()) {
+        status = LM_SKIPPED;
+    } else {
+        double H[36], g[6], cost;
+        pnp_system(obs, pose_from7(x), TCB2, cfg->huber_delta, H, g, &cost);
+        res->initial_cost = cost;
+        double lambda = cfg->lambda_init, nu = 2.0;
+        for (int it = 0; it < cfg->max_iterations; ++it) {
+            res->iterations = it + 1;
+            if (!std::isfinite(cost)) {
+                status = LM_NUMERICAL_FAILURE;
+                break;
+            }
+            std::vector<double> A(H, H + 36), b(6), dx;
+            for (int a = 0; a < 6; ++a) {
+                A[a * 6 + a] += lambda;
+                b[a] = -g[a];
+            }
+            if (!chol_solve(A, 6, b, dx)) {
+                lambda *= nu;
+                nu *= 2.0;
+                if (lambda > 1e32) {
+                    status = LM_TRUST_REGION;
+                    break;
+                }
+                continue;
+            }
+            double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
+            for (int a = 0; a < 6; ++a) {
+                dx2 += dx[a] * dx[a];
+                gdx += g[a] * dx[a];
+            }
+            for (int a = 0; a < 7; ++a) x2 += x[a] * x[a];
+            if (std::sqrt(dx2) <= cfg->parameter_tolerance * (std::sqrt(x2) + cfg->parameter_tolerance)) {
+                status = LM_PARAM_TOL;
+                break;
+            }
+            orc_se3_plus(x, dx.data(), xt);
+            double Ht[36], gt[6], new_cost;
+            pnp_system(obs, pose_from7(xt), TCB2, cfg->huber_delta, Ht, gt, &new_cost);
+            double pred = 0.5 * (lambda * dx2 - gdx);
+            double rho = (cost - new_cost) / pred;
+            if (std::isfinite(new_cost) && rho > 0.0) {
+                double dcost = cost - new_cost;
+                memcpy(x, xt, sizeof(x));
+                memcpy(H, Ht, sizeof(H));
+                memcpy(g, gt, sizeof(g));
+                double f = 2.0 * rho - 1.0;
+                lambda *= std::max(1.0 / 3.0, 1.0 - f * f * f);
+                nu = 2.0;
+                cost = new_cost;
+                if (dcost <= cfg->cost_tolerance * (cost + dcost)) {
+                    status = LM_COST_TOL;
+                    break;
+                }
+            } else {
+                lambda *= nu;
+                nu *= 2.0;
+                if (lambda > 1e32) {
+                    status = LM_TRUST_REGION;
+                    break;
+                }
+            }
+        }
+        res->final_cost = cost;
+    }
+    res->status = status;
+    memcpy(res->pose7, x, sizeof(x));
+    if (status > 0) {  // is_optimization_successful (:384-395)
+        Pose P = pose_from7(x);
+        double TBW[16], Tl_inv[16], Tr[16];
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) TBW[4 * i + j] = P.R[i][j];
+            TBW[4 * i + 3] = P.t[i];
+        }
+        TBW[12] = 0.0; TBW[13] = 0.0; TBW[14] = 0.0; TBW[15] = 1.0;
+        rigid_inverse(TBW, res->T_W_B);
+        rigid_inverse(T_last, Tl_inv);
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < 4; ++k) s += res->T_W_B[4 * i + k] * Tl_inv[4 * k + j];
+                Tr[4 * i + j] = s;
+            }
+        res->translation_norm = std::sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+        double Rr[9] = {Tr[0], Tr[1], Tr[2], Tr[4], Tr[5], Tr[6], Tr[8], Tr[9], Tr[10]};
+        double q7[7] = {0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
+        orc_quat_from_rotation(Rr, q7 + 3);
+        Pose Q = pose_from7(q7);
+        res->rotation_norm = euler_norm(Q.R);
+        res->is_keyframe = (res->translation_norm > thr_t || res->rotation_norm > thr_r) ? 1 : 0;
+    } else {  // estimator.rs:228-234: the frame stays a keyframe with T_W_B = I
+        for (int k = 0; k < 16; ++k) res->T_W_B[k] = (k % 5 == 0) ? 1.0 : 0.0;
+        res->is_keyframe = 1;
+    }
+    return 0;
+}
+

@@ -37,7 +37,15 @@ class OrcCamera(C.Structure):
                 ("reserved", C.c_int32), ("params", C.c_double * 9)]
 
 
+class OrcMotionResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("iterations", C.c_int), ("is_keyframe", C.c_int), ("n_observations", C.c_int),
+                ("initial_cost", C.c_double), ("final_cost", C.c_double), ("translation_norm", C.c_double),
+                ("rotation_norm", C.c_double), ("T_W_B", C.c_double * 16), ("pose7", C.c_double * 7)]
+
+
 _SIG = {
+    "orc_track_motion": (C.c_int, [P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P, P, C.POINTER(LmCfg),
+                                   C.c_double, C.c_double, C.POINTER(OrcMotionResult)]),
     "orc_unproject": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
     "orc_project": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
     "orc_set_trig_mode": (None, [C.c_int]),
@@ -215,6 +223,23 @@ def project(cam: OrcCamera, pts):
     valid = np.zeros(len(pts), np.uint8)
     load().orc_project(C.byref(cam), _p(pts), len(pts), _p(out), _p(valid))
     return out, valid.astype(bool)
+
+
+def track_motion(ids_l, uv_l, ids_r, uv_r, map_ids, map_pw, T_W_B_last_kf, T_C_B2, cfg=None,
+                 thr_t=0.05, thr_r=0.05) -> OrcMotionResult:
+    """sliding_window.rs:490-587 + estimator.rs:195-234 restated (map ids ascending)."""
+    a = [np.ascontiguousarray(ids_l, np.uint64).reshape(-1), np.ascontiguousarray(uv_l, np.float32).reshape(-1, 2),
+         np.ascontiguousarray(ids_r, np.uint64).reshape(-1), np.ascontiguousarray(uv_r, np.float32).reshape(-1, 2),
+         np.ascontiguousarray(map_ids, np.uint64).reshape(-1), np.ascontiguousarray(map_pw, np.float32).reshape(-1, 3),
+         np.ascontiguousarray(T_W_B_last_kf, np.float64).reshape(16),
+         np.ascontiguousarray(T_C_B2, np.float64).reshape(32)]
+    cfg = cfg or lm_cfg(max_iterations=10)
+    r = OrcMotionResult()
+    load().orc_track_motion(_p(a[0]) if len(a[0]) else None, _p(a[1]) if len(a[0]) else None, len(a[0]),
+                            _p(a[2]) if len(a[2]) else None, _p(a[3]) if len(a[2]) else None, len(a[2]),
+                            _p(a[4]) if len(a[4]) else None, _p(a[5]) if len(a[4]) else None, len(a[4]),
+                            _p(a[6]), _p(a[7]), C.byref(cfg), thr_t, thr_r, C.byref(r))
+    return r
 
 
 def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):

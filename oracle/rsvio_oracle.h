@@ -151,6 +151,20 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed,
 /* SE3 right-plus used by the LM update: pose7 <- pose7 (+) delta ([rho; theta]) */
 void orc_se3_plus(const double* pose7, const double* delta, double* out7);
 
+/* SlidingWindow::track_motion (sliding_window.rs:490-587) + keyframe rule (estimator.rs:195-234):
+ * PnP LM on one pose from the last keyframe, T_W_B = inv(SE3), keyframe iff ||t_rel|| > thr_t or
+ * ||euler(R_rel)|| > thr_r; failure -> T_W_B = I, keyframe.  Map ids strictly ascending. */
+typedef struct {
+    int status, iterations, is_keyframe, n_observations;
+    double initial_cost, final_cost, translation_norm, rotation_norm;
+    double T_W_B[16];
+    double pose7[7];
+} orc_motion_result;
+int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_l, const uint64_t* ids_r,
+                     const float* uv_r, int n_r, const uint64_t* map_ids, const float* map_pw, int n_map,
+                     const double* T_W_B_last_kf, const double* T_C_B2, const orc_lm_cfg* cfg,
+                     double thr_t, double thr_r, orc_motion_result* res);
+
 /* nalgebra UnitQuaternion::from_matrix restatement (sliding_window.rs:221) */
 void orc_quat_from_rotation(const double* R, double* qwxyz);
 

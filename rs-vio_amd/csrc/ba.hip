@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "se3.hpp"
 
 namespace rsvio {
 
@@ -58,32 +59,6 @@ constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per
 struct Mat4 {
     double m[16];
 };
-
-struct Pose {
-    double R[3][3];
-    double t[3];
-};
-
-// nalgebra UnitQuaternion::to_rotation_matrix after normalisation (apex SE3::from)
-__device__ __forceinline__ Pose pose_from7(const double* p7) {
-    double w = p7[3], x = p7[4], y = p7[5], z = p7[6];
-    const double in = 1.0 / sqrt(w * w + x * x + y * y + z * z);  // one division, 4 products
-    w *= in; x *= in; y *= in; z *= in;
-    double ww = w * w, xx = x * x, yy = y * y, zz = z * z;
-    double xy = x * y * 2.0, wz = w * z * 2.0, wy = w * y * 2.0;
-    double xz = x * z * 2.0, yz = y * z * 2.0, wx = w * x * 2.0;
-    Pose P;
-    P.R[0][0] = ww + xx - yy - zz; P.R[0][1] = xy - wz;           P.R[0][2] = wy + xz;
-    P.R[1][0] = wz + xy;           P.R[1][1] = ww - xx + yy - zz; P.R[1][2] = yz - wx;
-    P.R[2][0] = xz - wy;           P.R[2][1] = wx + yz;           P.R[2][2] = ww - xx - yy + zz;
-    P.t[0] = p7[0]; P.t[1] = p7[1]; P.t[2] = p7[2];
-    return P;
-}
-
-__device__ __forceinline__ void mat3vec(const double R[3][3], const double* v, double* out) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) out[i] = (R[i][0] * v[0] + R[i][1] * v[1]) + R[i][2] * v[2];
-}
 
 // factors.rs:350-447 -- residual and the 2x9 Jacobian [dp_W | dt | dw]; false on cheirality failure
 __device__ __forceinline__ bool linearize(const double* pW, const Pose& P, const double* TCB, const double* uv,
@@ -139,18 +114,6 @@ __device__ __forceinline__ bool linearize(const double* pW, const Pose& P, const
     return true;
 }
 
-__device__ __forceinline__ void huber(double s, double d, double* rho, double* w) {
-    double d2 = d * d;
-    if (s <= d2) {
-        *rho = s;
-        *w = 1.0;
-    } else {
-        double rs = sqrt(s);
-        *rho = 2.0 * d * rs - d2;
-        *w = d / rs;
-    }
-}
-
 __device__ __forceinline__ bool inv3(const double A[3][3], double X[3][3]) {
     double c00 = A[1][1] * A[2][2] - A[1][2] * A[2][1];
     double c01 = A[1][2] * A[2][0] - A[1][0] * A[2][2];
@@ -168,46 +131,6 @@ __device__ __forceinline__ bool inv3(const double A[3][3], double X[3][3]) {
     X[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) * id;
     X[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) * id;
     return true;
-}
-
-// T (+) delta = T * Exp([rho; theta]) (same formula as oracle orc_se3_plus)
-__device__ void se3_plus(const double* p7, const double* d, double* out) {
-    const double* rho = d;
-    const double* om = d + 3;
-    double th2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
-    double th = sqrt(th2);
-    double qd[4], A, Bc;
-    if (th < 1e-8) {
-        qd[0] = 1.0; qd[1] = 0.5 * om[0]; qd[2] = 0.5 * om[1]; qd[3] = 0.5 * om[2];
-        A = 0.5 - th2 / 24.0;
-        Bc = 1.0 / 6.0 - th2 / 120.0;
-    } else {
-        // one sincos of theta/2: sin(th) = 2 s c, 1 - cos(th) = 2 s^2 (same values as the
-        // oracle's libm calls to within an ulp; tolerance parity)
-        double sh, ch;
-        sincos(0.5 * th, &sh, &ch);
-        const double ith = 1.0 / th;
-        const double s = sh * ith;
-        qd[0] = ch; qd[1] = s * om[0]; qd[2] = s * om[1]; qd[3] = s * om[2];
-        const double ith2 = ith * ith;
-        A = 2.0 * sh * sh * ith2;
-        Bc = (th - 2.0 * sh * ch) * ith2 * ith;
-    }
-    double wx[3] = {om[1] * rho[2] - om[2] * rho[1], om[2] * rho[0] - om[0] * rho[2], om[0] * rho[1] - om[1] * rho[0]};
-    double wwx[3] = {om[1] * wx[2] - om[2] * wx[1], om[2] * wx[0] - om[0] * wx[2], om[0] * wx[1] - om[1] * wx[0]};
-    double td[3];
-    for (int i = 0; i < 3; ++i) td[i] = rho[i] + A * wx[i] + Bc * wwx[i];
-    Pose P = pose_from7(p7);
-    double Rt[3];
-    mat3vec(P.R, td, Rt);
-    out[0] = p7[0] + Rt[0];
-    out[1] = p7[1] + Rt[1];
-    out[2] = p7[2] + Rt[2];
-    double w0 = p7[3], x0 = p7[4], y0 = p7[5], z0 = p7[6];
-    double qn[4] = {w0 * qd[0] - x0 * qd[1] - y0 * qd[2] - z0 * qd[3], w0 * qd[1] + x0 * qd[0] + y0 * qd[3] - z0 * qd[2],
-                    w0 * qd[2] - x0 * qd[3] + y0 * qd[0] + z0 * qd[1], w0 * qd[3] + x0 * qd[2] - y0 * qd[1] + z0 * qd[0]};
-    const double inn = 1.0 / sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
-    for (int i = 0; i < 4; ++i) out[3 + i] = qn[i] * inn;
 }
 
 __device__ __forceinline__ int utri(int a, int c) {  // index of (min, max) in a packed 6x6 upper triangle
@@ -289,33 +212,6 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         s.nu = 2.0;
         *Wk.st = s;
     }
-}
-
-__device__ __forceinline__ double rl64(double v, int lane) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Row-local DPP move of a double (both halves through the same lane permutation).
-template <int CTRL>
-__device__ __forceinline__ double dpp64(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-
-// Deterministic sum over the 64 lanes (all lanes active), returned to every lane: a fixed
-// pairing inside each row of 16 (quad_perm xor 1, xor 2, half-row mirror, row mirror -- each
-// step adds the same two values on both partners, so all 16 lanes agree bitwise), then the four
-// row totals in row order.
-__device__ __forceinline__ double wave_sum_det(double v) {
-    v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
-    v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
-    v += dpp64<0x141>(v);  // row_half_mirror
-    v += dpp64<0x140>(v);  // row_mirror
-    return ((rl64(v, 0) + rl64(v, 16)) + rl64(v, 32)) + rl64(v, 48);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -67,6 +67,17 @@ int guarded(F&& f) {
 #define RSVIO_DBG_READER(name)
 #endif
 
+// The tracker's device-resident output of the last frame (tracker.hip), for consumers on the
+// device (pnp.hip): features (AoS rsvio_feature), fused undistorted coordinates, counts.
+struct TrackerView {
+    hipStream_t stream;
+    const rsvio_feature* out[2];
+    const float2* undist[2];   // null unless cameras are attached
+    const int* counts;         // device (n_l, n_r)
+    int device;
+};
+TrackerView tracker_view(rsvio_tracker* t);
+
 // Pyramid level geometry: level i = (w / 2^i) x (h / 2^i), packed back to back
 // (feature_tracker.rs:215-216).
 __host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }

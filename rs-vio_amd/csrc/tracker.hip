@@ -515,6 +515,21 @@ struct rsvio_track_ctx {
     rsvio::TrackCtx c;
 };
 
+namespace rsvio {
+TrackerView tracker_view(rsvio_tracker* h) {
+    Tracker& T = h->t;
+    TrackerView v{};
+    v.stream = T.stream;
+    v.out[0] = T.out.p;
+    v.out[1] = T.out.p + T.cap;
+    v.undist[0] = T.cams.on ? T.undist.p : nullptr;
+    v.undist[1] = T.cams.on ? T.undist.p + T.cap : nullptr;
+    v.counts = T.counts.p;
+    v.device = T.P.device;
+    return v;
+}
+}  // namespace rsvio
+
 using rsvio::guarded;
 
 extern "C" {

@@ -60,6 +60,16 @@ class Camera(C.Structure):
                 ("reserved", C.c_int32), ("params", C.c_double * 9)]
 
 
+class KeyframeRule(C.Structure):
+    _fields_ = [("translation_threshold", C.c_double), ("rotation_threshold", C.c_double)]
+
+
+class MotionResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("iterations", C.c_int32), ("is_keyframe", C.c_int32),
+                ("n_observations", C.c_int32), ("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("translation_norm", C.c_double), ("rotation_norm", C.c_double), ("T_W_B", C.c_double * 16)]
+
+
 class BaParams(C.Structure):
     _fields_ = [("max_keyframes", C.c_int32), ("max_landmarks", C.c_int32),
                 ("max_observations", C.c_int32), ("device", C.c_int32)]
@@ -81,6 +91,13 @@ SIG = {
     "rsvio_unproject_d": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P, P]),
     "rsvio_tracker_set_cameras": (C.c_int, [P, C.POINTER(Camera), C.POINTER(Camera)]),
     "rsvio_tracker_undistorted": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
+    "rsvio_pnp_create": (C.c_int, [C.c_int32, C.POINTER(P)]),
+    "rsvio_pnp_destroy": (None, [P]),
+    "rsvio_pnp_set_map": (C.c_int, [P, P, P, C.c_int32]),
+    "rsvio_track_motion": (C.c_int, [P, P, P, C.c_size_t, P, P, C.c_size_t, P, P, C.POINTER(LmCfg),
+                                     C.POINTER(KeyframeRule), C.POINTER(MotionResult)]),
+    "rsvio_track_motion_tracker": (C.c_int, [P, P, P, P, C.POINTER(LmCfg), C.POINTER(KeyframeRule),
+                                             C.POINTER(MotionResult)]),
     "rsvio_pyramid_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
     "rsvio_build_pyramid": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, P]),
     "rsvio_track_points": (C.c_int, [P, P, C.c_int32, C.c_int32, C.c_int32, P, C.c_int32, C.c_int32, C.c_float,
@@ -123,6 +140,14 @@ def load() -> C.CDLL:
     if not path.exists():
         raise RuntimeError(f"{path} not found: build it with `make -C rs-vio_amd` (hipcc, gfx950); "
                            "rsvio has no CPU fallback")
+    # One HIP runtime per process: torch's wheel bundles its own libamdhip64 (loaded under the
+    # file name libamdhip64.so, SONAME libamdhip64.so.7).  If librsvio_gpu.so were loaded first
+    # it would pull /opt/rocm's copy and a later torch import would bring a second runtime that
+    # sees no device.  Importing torch first makes the library bind to the already-loaded one.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(str(path))
     for name, (res, args) in SIG.items():
         try:

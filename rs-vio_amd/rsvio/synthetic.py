@@ -290,3 +290,75 @@ def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int =
                      obs_cam=np.asarray(obs_cam, np.uint8), obs_uv=np.asarray(obs_uv, np.float64),
                      T_C_B2=np.stack([T_C_B[0].reshape(16), T_C_B[1].reshape(16)]),
                      true_pose7=true_pose7, true_p_W=p_W)
+
+
+@dataclass
+class MotionFrame:
+    """One frame for track_motion: the map (ids ascending, p_W f32), the frame's features per
+    camera (ids, undistorted coordinates f32), the last keyframe's T_W_B, the true T_W_B and
+    T_C_B2 (T_Cl_B, T_Cr_B)."""
+    map_ids: np.ndarray
+    map_pw: np.ndarray
+    ids_l: np.ndarray
+    uv_l: np.ndarray
+    ids_r: np.ndarray
+    uv_r: np.ndarray
+    T_W_B_last_kf: np.ndarray
+    T_W_B_true: np.ndarray
+    T_C_B2: np.ndarray
+
+
+def motion_frame(n_map: int = 2000, n_feat: int = 300, seed: int = 3, step=(0.03, math.radians(1.0)),
+                 noise_px: float = 0.5, map_noise: float = 0.01, outlier_frac: float = 0.0,
+                 unmapped: int = 40) -> MotionFrame:
+    """Config-4-like motion tracking input: map points in front of the
+    last keyframe's left camera, a frame moved by `step` (translation m, rotation rad), the
+    features the frame sees (left ids + right ids, some unmapped), normalised observations
+    with pixel noise, and map points perturbed by `map_noise` m and stored as f32."""
+    rng = np.random.default_rng(seed)
+    T_last = np.eye(4)
+    T_last[:3, :3] = rot_z(0.1)
+    T_last[:3, 3] = [0.5, -0.2, 0.1]
+    T_true = T_last.copy()
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    a = step[1]
+    dR = np.eye(3) + math.sin(a) * K + (1 - math.cos(a)) * (K @ K)
+    dt = rng.normal(size=3)
+    dt *= step[0] / np.linalg.norm(dt)
+    T_true[:3, :3] = T_last[:3, :3] @ dR
+    T_true[:3, 3] = T_last[:3, 3] + T_last[:3, :3] @ dt
+    T_C_B = [np.linalg.inv(T_B_CL), np.linalg.inv(T_B_CR)]
+    p_c0 = np.stack([rng.uniform(-3, 3, n_map), rng.uniform(-2, 2, n_map), rng.uniform(2, 8, n_map)], 1)
+    T_W_C0 = T_last @ T_B_CL
+    p_W = (T_W_C0[:3, :3] @ p_c0.T).T + T_W_C0[:3, 3]
+    map_ids = np.sort(rng.choice(np.arange(10, 10 * n_map + 10), n_map, replace=False)).astype(np.uint64)
+    map_pw = (p_W + rng.normal(0.0, map_noise, p_W.shape)).astype(np.float32)
+    sig = noise_px / FX_LEFT
+    seen = np.sort(rng.choice(n_map, min(n_feat, n_map), replace=False))
+    T_B_W = np.linalg.inv(T_true)
+    feats = []
+    for c in range(2):
+        T = T_C_B[c] @ T_B_W
+        ids, uv = [], []
+        for l in seen:
+            pc = T[:3, :3] @ p_W[l] + T[:3, 3]
+            if pc[2] <= 0.1:
+                continue
+            o = pc[:2] / pc[2] + rng.normal(0.0, sig, 2)
+            if rng.uniform() < outlier_frac:
+                o = o + rng.uniform(-6.0, 6.0, 2)   # beyond the Huber knee (delta 2)
+            ids.append(map_ids[l])
+            uv.append(o)
+        # features without a map point (new tracks): ids not in the map
+        for u in range(unmapped):
+            ids.append(np.uint64(10 * n_map + 100 + 7 * u + c))
+            uv.append(rng.uniform(-0.5, 0.5, 2))
+        ids = np.asarray(ids, np.uint64)
+        uv = np.asarray(uv, np.float64).astype(np.float32)
+        order = np.argsort(ids, kind="stable")   # the tracker returns features sorted by id
+        feats.append((ids[order], uv[order]))
+    return MotionFrame(map_ids=map_ids, map_pw=map_pw, ids_l=feats[0][0], uv_l=feats[0][1], ids_r=feats[1][0],
+                       uv_r=feats[1][1], T_W_B_last_kf=T_last, T_W_B_true=T_true,
+                       T_C_B2=np.stack([T_C_B[0].reshape(16), T_C_B[1].reshape(16)]))
