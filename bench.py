@@ -67,6 +67,106 @@ def ba_flops_per_iter(n_obs: int, n_lm: int, k_per_lm: int, n_free: int) -> floa
 
 
 # ---------------------------------------------------------------------------------------
+PNP_FLOP_PER_OBS_PASS = 318   # pnp_linearize (~183) + Huber + 21+6 H/g accumulations (~135), per observation
+UNPROJ_BYTES_PER_POINT = 17    # 8 B pixel in, 8 B undistorted out, 1 B valid
+
+
+def measure_rows(device: int, cpu: bool, reps: int = 200):
+    """The §8 rows beside the headline path, each on its own config-shaped input, timed with HIP
+    events on the stream its kernel runs on (inputs resident on the device):
+      * T12 unprojection: config 5's batch, 80,000 EUCM (TUM-VI cam0) observations;
+      * B8 track_motion + keyframe rule: one frame of 300 features per camera (600 mapped
+        observations, 40 unmapped per camera) against a 2,000-point map, EuRoC extrinsics.
+    The oracle's time on the same inputs (1 host thread) is reported beside each."""
+    import torch
+
+    from rsvio import synthetic as S
+    from rsvio.camera import TUM_VI
+    from rsvio.motion import MotionTracker
+    out = {}
+    st = torch.cuda.Stream(device)
+    # --- T12
+    n = 80000
+    rng = np.random.default_rng(5)
+    px = np.stack([rng.uniform(0, 512, n), rng.uniform(0, 512, n)], 1).astype(np.float32)
+    d_px = torch.from_numpy(px).to(f"cuda:{device}")
+    d_out = torch.empty_like(d_px)
+    d_ok = torch.empty(n, dtype=torch.uint8, device=d_px.device)
+    torch.cuda.synchronize()
+    cam = TUM_VI[0]
+    for _ in range(10):
+        cam.unproject_device(d_px.data_ptr(), n, d_out.data_ptr(), d_ok.data_ptr(), st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        cam.unproject_device(d_px.data_ptr(), n, d_out.data_ptr(), d_ok.data_ptr(), st.cuda_stream)
+    e1.record(st)
+    st.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    gbs = n * UNPROJ_BYTES_PER_POINT / (ms * 1e-3) / 1e9
+    row = {"workload": "80,000 EUCM observations (config 5 batch), plane convention",
+           "value": round(n / (ms * 1e-3), 1), "unit": "points/s", "kernel": "unproject_kernel",
+           "launch_ms": round(ms, 5),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 6),
+                        "algorithmic_bytes_per_launch": n * UNPROJ_BYTES_PER_POINT,
+                        "note": "launch-latency bound at this size (1.36 MB)"}}
+    if cpu:
+        from oracle import oracle as O
+        oc = O.camera(cam.model, cam.params, 0, cam.max_iterations)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 1.0 or k < 3:
+            O.unproject(oc, px)
+            k += 1
+        cms = 1e3 * (time.perf_counter() - t0) / k
+        row["cpu_baseline"] = {"value": round(n / (cms * 1e-3), 1), "unit": "points/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} x 80,000 points, oracle/camera_oracle.cpp"}
+    out["unproject"] = row
+    # --- B8
+    m = S.motion_frame(seed=3)
+    mt = MotionTracker(device)
+    mt.set_stream(st.cuda_stream)
+    mt.set_map(m.map_ids, m.map_pw)
+    for _ in range(5):
+        r = mt.track_motion(m.ids_l, m.uv_l, m.ids_r, m.uv_r, m.T_W_B_last_kf, m.T_C_B2)
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        r = mt.track_motion(m.ids_l, m.uv_l, m.ids_r, m.uv_r, m.T_W_B_last_kf, m.T_C_B2)
+        b.record(st)
+        evs.append((a, b))
+    host_ms = 1e3 * (time.perf_counter() - t0) / reps
+    st.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    passes = 1 + r.iterations
+    flops = PNP_FLOP_PER_OBS_PASS * r.n_observations * passes
+    tf = flops / (ms * 1e-3) / 1e12
+    row = {"workload": "1 frame: 300 features/camera (600 mapped observations) vs a 2,000-point map, "
+                       "PnP LM <= 10 it + keyframe rule",
+           "value": round(1e3 / ms, 1), "unit": "frames/s", "kernel": "pnp_track_motion_kernel",
+           "launch_ms": round(ms, 5), "host_inclusive_ms": round(host_ms, 4),
+           "lm_iterations": r.iterations, "status": r.status, "observations": r.n_observations,
+           "roofline": {"bound": "fp64", "achieved": round(tf, 5), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tf / FP64_PEAK_TFLOPS, 8), "flop_per_launch": flops,
+                        "note": "one workgroup by design (a serial LM of <= 10 dependent 6x6 solves)"}}
+    if cpu:
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 1.0 or k < 3:
+            O.track_motion(m.ids_l, m.uv_l, m.ids_r, m.uv_r, m.map_ids, m.map_pw, m.T_W_B_last_kf, m.T_C_B2)
+            k += 1
+        cms = 1e3 * (time.perf_counter() - t0) / k
+        row["cpu_baseline"] = {"value": round(1e3 / cms, 1), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} frames, oracle orc_track_motion"}
+    out["track_motion"] = row
+    mt.close()
+    return out
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per dispatch of `kernel` (FETCH_SIZE + WRITE_SIZE) from the newest committed
     PMC summary profiles/*_pmc_traffic.json (separate rocprofv3 --pmc passes of this same
@@ -342,6 +442,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-rows", action="store_true", help="skip the unprojection / track_motion row measurements")
     ap.add_argument("--cu-split", type=float, default=0.5,
                     help="fraction of CUs given to the tracker stream (0: no CU partition)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
@@ -437,6 +538,8 @@ def main():
                         "achieved_tflops": round(flops / (ba_ms_iter * 1e-3) / 1e12, 4),
                         "peak_tflops": FP64_PEAK_TFLOPS},
     }
+    if rank == 0 and not args.no_rows:
+        out["rows"] = measure_rows(local, cpu=(world == 1 and not args.no_cpu))
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(args.cpu_seconds)
         cb["cores"] = 1

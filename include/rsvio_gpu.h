@@ -274,6 +274,8 @@ typedef struct {
 
 int rsvio_pnp_create(int32_t device, rsvio_pnp** out);
 void rsvio_pnp_destroy(rsvio_pnp* p);
+/* Launch rsvio_track_motion on a caller-owned stream (hipStream_t; NULL: the handle's own). */
+int rsvio_pnp_set_stream(rsvio_pnp* p, void* stream);
 /* SlidingWindow::map_points after optimize (sliding_window.rs:466-475): feature ids strictly
  * ascending, p_W as f32 triples. */
 int rsvio_pnp_set_map(rsvio_pnp* p, const uint64_t* ids, const float* p_W, int32_t n);

@@ -585,16 +585,6 @@ constexpr int kNB = 8;  // Cholesky panel width (blocked path, n > 60)
 
 
 
-// 1/d, f64: hardware estimate (v_rcp_f64, ~2^-23 relative) + two Newton steps, the second
-// folded into the correction: y1 = y0 + y0 e, e = 1 - d y0; y2 = y1 + y1 (1 - d y1) with
-// 1 - d y1 = e^2 exactly up to rounding, so y2 = y0 (1 + e + e^2) -- full f64 precision with
-// one fewer dependent step.
-__device__ __forceinline__ double rcp_f64(double d) {
-    const double y = __builtin_amdgcn_rcp(d);
-    const double e = fma(-d, y, 1.0);
-    return fma(y, fma(e, e, e), y);
-}
-
 // Pipelined 4-wave LDL^T of the augmented system [S; b^T]: wave WV owns the contiguous columns
 // [WV*CW, WV*CW + CW) of every row (lane = row; lane NP = b).  A wave first consumes the
 // columns of the waves before it (waits on an LDS progress counter, then rank-1 updates its own

@@ -111,6 +111,24 @@ __device__ __forceinline__ double wave_sum_det(double v) {
     return ((rl64(v, 0) + rl64(v, 16)) + rl64(v, 32)) + rl64(v, 48);
 }
 
+// 1/d, f64: hardware estimate (v_rcp_f64, ~2^-23 relative) + two Newton steps, the second
+// folded into the correction: y1 = y0 + y0 e, e = 1 - d y0; y2 = y1 + y1 (1 - d y1) with
+// 1 - d y1 = e^2 exactly up to rounding, so y2 = y0 (1 + e + e^2) -- full f64 precision with
+// one fewer dependent step.
+__device__ __forceinline__ double rcp_f64(double d) {
+    const double y = __builtin_amdgcn_rcp(d);
+    const double e = fma(-d, y, 1.0);
+    return fma(y, fma(e, e, e), y);
+}
+
+// 1/sqrt(d), f64: hardware estimate + two Newton steps (y <- y (3 - d y^2) / 2)
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    y = y * fma(-0.5 * d, y * y, 1.5);
+    y = y * fma(-0.5 * d, y * y, 1.5);
+    return y;
+}
+
 // Rigid inverse [R^T | -R^T t] of a row-major 4x4 transform (nalgebra try_inverse of a rigid
 // T up to rounding; the oracle uses the same formula).
 __device__ __forceinline__ void rigid_inverse(const double* T, double* Ti) {

@@ -93,6 +93,7 @@ SIG = {
     "rsvio_tracker_undistorted": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
     "rsvio_pnp_create": (C.c_int, [C.c_int32, C.POINTER(P)]),
     "rsvio_pnp_destroy": (None, [P]),
+    "rsvio_pnp_set_stream": (C.c_int, [P, P]),
     "rsvio_pnp_set_map": (C.c_int, [P, P, P, C.c_int32]),
     "rsvio_track_motion": (C.c_int, [P, P, P, C.c_size_t, P, P, C.c_size_t, P, P, C.POINTER(LmCfg),
                                      C.POINTER(KeyframeRule), C.POINTER(MotionResult)]),

@@ -65,6 +65,10 @@ class MotionTracker:
         except Exception:
             pass
 
+    def set_stream(self, stream_ptr):
+        """Launch on a caller-owned HIP stream (None: the handle's own)."""
+        check(_lib.load().rsvio_pnp_set_stream(self._h, stream_ptr))
+
     def set_map(self, ids, p_W):
         """map_points (sliding_window.rs:466-475); sorted here if the caller's ids are not."""
         ids = np.asarray(ids, np.uint64).reshape(-1)
