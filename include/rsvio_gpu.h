@@ -129,6 +129,71 @@ typedef struct {
 int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, int32_t n_batches,
                          int32_t max_iterations, float thresh, void* stream);
 
+/* ====== T-sec: the feature_tracker/ crate (FeatureTracker, bicubic LK + Shi-Tomasi) ====== */
+
+/* FeatureTrackingConfig (feature_tracker/src/feature_tracker.rs:25-38; defaults
+ * feature_tracker/config/config.yaml) + image size, matching cost, device and capacity. */
+enum { RSVIO_FT_SSD = 0, RSVIO_FT_LSSD = 1 };   /* MatchingCost (patch.rs:6-9) */
+typedef struct {
+    int32_t width, height;
+    int32_t nlevels;                  /* 5 */
+    int32_t preprocessing_blur;       /* 1 */
+    double ratio;                     /* 2.0 */
+    float preprocessing_blur_sigma;   /* 2.0 */
+    float detection_threshold;        /* 2.5 */
+    uint32_t detection_min_dist;      /* 15 */
+    float detection_blur;             /* 6.0 */
+    int32_t optical_flow_max_iter;    /* 25 */
+    float optical_flow_lm_lambda;     /* 0.1 */
+    int32_t matching_cost;            /* RSVIO_FT_SSD: what process_frame uses (feature_tracker.rs:125) */
+    int32_t device;
+    int32_t max_features;             /* capacity of the frame's feature list (0 -> 8192) */
+    int32_t reserved;
+} rsvio_ft_config;                    /* 64 bytes */
+
+/* Feature (feature_tracker.rs:41-48): id + central point */
+typedef struct {
+    uint64_t feature_id;
+    float x, y;
+} rsvio_ft_feature;                   /* 16 bytes */
+
+typedef struct rsvio_ft rsvio_ft;
+
+/* FeatureTracker::new(config, None) (feature_tracker.rs:59-69) */
+int rsvio_ft_create(const rsvio_ft_config* cfg, rsvio_ft** out);
+void rsvio_ft_destroy(rsvio_ft* t);
+/* FeatureTracker::process_frame(&FloatGrayImage, Frame) (:77-185): img is f32 luma in [0, 1]
+ * (to_luma32f), row stride in floats (0 = width).  out receives frame.features: the previous
+ * frame's features that track (previous order, positions transform * centre), then the new
+ * Shi-Tomasi corners in (y, x) order with consecutive ids.  RSVIO_ERR_CAPACITY when the list
+ * exceeds max_features (the list is truncated). */
+int rsvio_ft_process_frame(rsvio_ft* t, const float* img, size_t stride, rsvio_ft_feature* out, size_t cap,
+                           size_t* n);
+/* Same with the image already in device memory (tightly packed). */
+int rsvio_ft_process_frame_device(rsvio_ft* t, const float* d_img, rsvio_ft_feature* out, size_t cap, size_t* n);
+/* FeatureTracker::get_pyramid (:190-193): the last frame's packed pyramid (rsvio_ft_pyramid_floats) */
+int rsvio_ft_get_pyramid(rsvio_ft* t, float* out, size_t cap_floats);
+void* rsvio_ft_stream(rsvio_ft* t);
+
+/* ---- parity-level entry points (host buffers in/out, current device) ---- */
+/* packed size of build_image_pyramid's output: level l = round(w / ratio^l) x round(h / ratio^l) */
+size_t rsvio_ft_pyramid_floats(int32_t w, int32_t h, int32_t nlevels, double ratio);
+/* build_image_pyramid (image_operations.rs:47-78) */
+int rsvio_ft_build_pyramid(const float* img, int32_t w, int32_t h, int32_t nlevels, double ratio, int32_t blur,
+                           float sigma, float* out);
+/* feature_tracking::track_points (feature_tracking.rs:16-61) on packed pyramids: per feature the
+ * forward transform {cos, sin, tx, ty} (identity when lost) and the keep flag. */
+int rsvio_ft_track_points(const float* pyr0, const float* pyr1, int32_t w, int32_t h, int32_t nlevels,
+                          double ratio, const float* xy, int32_t n, int32_t max_iter, float lm_lambda,
+                          int32_t matching_cost, float* iso_out, uint8_t* valid_out);
+/* shi_tomasi_score (feature_detection.rs:82-164) */
+int rsvio_ft_shi_tomasi_score(const float* img, int32_t w, int32_t h, float detection_blur, float* score);
+/* feature_detection::add_points (feature_detection.rs:47-80) on the fine level with the tracked
+ * features' centres: new corners (u32 x, y) in (y, x) order. */
+int rsvio_ft_add_points(const float* fine, int32_t w, int32_t h, const float* tracked_xy, int32_t n_tracked,
+                        float threshold, int32_t min_dist, float detection_blur, uint32_t* out_xy, int32_t cap,
+                        int32_t* n_out);
+
 /* ================= T12: camera unprojection (Frame::add_*_feature) ================= */
 
 /* Camera models of src/datasets/mod.rs:93-163 (camera-intrinsic-model 0.7.2):

@@ -44,6 +44,25 @@ class OrcMotionResult(C.Structure):
 
 
 _SIG = {
+    "orc_ft_level_dims": (None, [C.c_int, C.c_int, C.c_int, C.c_double, P]),
+    "orc_ft_pyramid_floats": (C.c_size_t, [C.c_int, C.c_int, C.c_int, C.c_double]),
+    "orc_ft_resize_triangle": (None, [P, C.c_int, C.c_int, P, C.c_int, C.c_int]),
+    "orc_ft_gaussian_blur": (None, [P, C.c_int, C.c_int, C.c_float, P]),
+    "orc_ft_fast_blur": (None, [P, C.c_int, C.c_int, C.c_float, P]),
+    "orc_ft_boxes_for_gauss": (None, [C.c_float, C.c_int, P]),
+    "orc_ft_build_pyramid": (None, [P, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_float, P]),
+    "orc_ft_bicubic": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P]),
+    "orc_ft_exp_se2": (None, [P, P]),
+    "orc_ft_log_se2": (None, [P, P]),
+    "orc_ft_patch_new": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, P, P, P]),
+    "orc_ft_track_points": (None, [P, P, C.c_int, C.c_int, C.c_int, C.c_double, P, C.c_int, C.c_int, C.c_float,
+                                   C.c_int, P, P]),
+    "orc_ft_shi_tomasi_score": (None, [P, C.c_int, C.c_int, C.c_float, P]),
+    "orc_ft_suppress_non_maximum": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_float, P, P, C.c_int]),
+    "orc_ft_add_points": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_float, C.c_int, C.c_float, P, C.c_int]),
+    "orc_ft_create": (P, [C.c_void_p, C.c_int, C.c_int]),
+    "orc_ft_destroy": (None, [P]),
+    "orc_ft_process_frame": (C.c_int, [P, P, P, P, C.c_int, C.POINTER(C.c_int)]),
     "orc_track_motion": (C.c_int, [P, P, C.c_int, P, P, C.c_int, P, P, C.c_int, P, P, C.POINTER(LmCfg),
                                    C.c_double, C.c_double, C.POINTER(OrcMotionResult)]),
     "orc_unproject": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
@@ -290,3 +309,166 @@ def se3_plus(pose7, delta):
     a, d = np.ascontiguousarray(pose7, np.float64), np.ascontiguousarray(delta, np.float64)
     load().orc_se3_plus(_p(a), _p(d), _p(out))
     return out
+
+
+# ---------------- feature_tracker/ crate (secondary variant) ----------------
+
+class FtConfig(C.Structure):
+    """feature_tracker/src/feature_tracker.rs:25-38 (FeatureTrackingConfig) + the matching cost."""
+    _fields_ = [("nlevels", C.c_int32), ("ratio", C.c_double), ("preprocessing_blur", C.c_int32),
+                ("preprocessing_blur_sigma", C.c_float), ("detection_threshold", C.c_float),
+                ("detection_min_dist", C.c_uint32), ("detection_blur", C.c_float),
+                ("optical_flow_max_iter", C.c_int32), ("optical_flow_lm_lambda", C.c_float),
+                ("matching_cost", C.c_int32)]
+
+
+def ft_config(nlevels=5, ratio=2.0, preprocessing_blur=True, preprocessing_blur_sigma=2.0, detection_threshold=2.5,
+              detection_min_dist=15, detection_blur=6.0, optical_flow_max_iter=25, optical_flow_lm_lambda=0.1,
+              matching_cost=0):
+    """Defaults = feature_tracker/config/config.yaml; matching_cost 0 = SSD (feature_tracker.rs:125)."""
+    return FtConfig(nlevels, ratio, int(preprocessing_blur), preprocessing_blur_sigma, detection_threshold,
+                    detection_min_dist, detection_blur, optical_flow_max_iter, optical_flow_lm_lambda, matching_cost)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def ft_level_dims(w, h, nlevels, ratio=2.0):
+    d = np.zeros(2 * nlevels, np.int32)
+    load().orc_ft_level_dims(w, h, nlevels, ratio, _p(d))
+    return [(int(d[2 * i]), int(d[2 * i + 1])) for i in range(nlevels)]
+
+
+def ft_split_pyramid(pyr, w, h, nlevels, ratio=2.0):
+    out, o = [], 0
+    for lw, lh in ft_level_dims(w, h, nlevels, ratio):
+        out.append(pyr[o:o + lw * lh].reshape(lh, lw))
+        o += lw * lh
+    return out
+
+
+def ft_build_pyramid(img, nlevels=5, ratio=2.0, blur=True, sigma=2.0):
+    img = _f32(img)
+    h, w = img.shape
+    out = np.empty(int(load().orc_ft_pyramid_floats(w, h, nlevels, ratio)), np.float32)
+    load().orc_ft_build_pyramid(_p(img), w, h, nlevels, ratio, int(blur), C.c_float(sigma), _p(out))
+    return out
+
+
+def ft_resize_triangle(img, nw, nh):
+    img = _f32(img)
+    h, w = img.shape
+    out = np.empty((nh, nw), np.float32)
+    load().orc_ft_resize_triangle(_p(img), w, h, _p(out), nw, nh)
+    return out
+
+
+def ft_gaussian_blur(img, sigma):
+    img = _f32(img)
+    out = np.empty_like(img)
+    load().orc_ft_gaussian_blur(_p(img), img.shape[1], img.shape[0], C.c_float(sigma), _p(out))
+    return out
+
+
+def ft_fast_blur(img, sigma):
+    img = _f32(img)
+    out = np.empty_like(img)
+    load().orc_ft_fast_blur(_p(img), img.shape[1], img.shape[0], C.c_float(sigma), _p(out))
+    return out
+
+
+def ft_boxes_for_gauss(sigma, n=3):
+    out = np.zeros(n, np.int32)
+    load().orc_ft_boxes_for_gauss(C.c_float(sigma), n, _p(out))
+    return out.tolist()
+
+
+def ft_bicubic(img, x, y):
+    img = _f32(img)
+    out = np.zeros(3, np.float32)
+    ok = load().orc_ft_bicubic(_p(img), img.shape[1], img.shape[0], C.c_float(x), C.c_float(y), _p(out))
+    return (out if ok else None)
+
+
+def ft_exp_se2(twist):
+    tw = _f32(twist)
+    out = np.zeros(4, np.float32)
+    load().orc_ft_exp_se2(_p(tw), _p(out))
+    return out
+
+
+def ft_log_se2(iso):
+    a = _f32(iso)
+    out = np.zeros(3, np.float32)
+    load().orc_ft_log_se2(_p(a), _p(out))
+    return out
+
+
+def ft_patch_new(img, cx, cy, lam=0.1, cost=0):
+    img = _f32(img)
+    data = np.zeros(52, np.float32)
+    jac = np.zeros((52, 3), np.float32)
+    hinv = np.zeros((3, 3), np.float32)
+    ok = load().orc_ft_patch_new(_p(img), img.shape[1], img.shape[0], C.c_float(cx), C.c_float(cy), C.c_float(lam),
+                                 cost, _p(data), _p(jac), _p(hinv))
+    return bool(ok), data, jac, hinv
+
+
+def ft_track_points(pyr0, pyr1, w, h, xy, nlevels=5, ratio=2.0, max_iter=25, lam=0.1, cost=0):
+    xy = _f32(xy).reshape(-1, 2)
+    n = len(xy)
+    iso = np.zeros((n, 4), np.float32)
+    valid = np.zeros(n, np.uint8)
+    load().orc_ft_track_points(_p(pyr0), _p(pyr1), w, h, nlevels, ratio, _p(xy) if n else None, n, max_iter,
+                               C.c_float(lam), cost, _p(iso), _p(valid))
+    return iso, valid.astype(bool)
+
+
+def ft_shi_tomasi_score(img, blur=6.0):
+    img = _f32(img)
+    out = np.empty_like(img)
+    load().orc_ft_shi_tomasi_score(_p(img), img.shape[1], img.shape[0], C.c_float(blur), _p(out))
+    return out
+
+
+def ft_suppress_non_maximum(score, radius=1, threshold=2.5, cap=1 << 20):
+    score = _f32(score)
+    xy = np.zeros((cap, 2), np.uint32)
+    sc = np.zeros(cap, np.float32)
+    n = load().orc_ft_suppress_non_maximum(_p(score), score.shape[1], score.shape[0], radius, C.c_float(threshold),
+                                           _p(xy), _p(sc), cap)
+    return xy[:n].copy(), sc[:n].copy()
+
+
+def ft_add_points(fine, tracked_xy=None, threshold=2.5, min_dist=15, blur=6.0, cap=1 << 16):
+    fine = _f32(fine)
+    tr = np.zeros((0, 2), np.float32) if tracked_xy is None else _f32(tracked_xy).reshape(-1, 2)
+    out = np.zeros((cap, 2), np.uint32)
+    n = load().orc_ft_add_points(_p(fine), fine.shape[1], fine.shape[0], _p(tr) if len(tr) else None, len(tr),
+                                 C.c_float(threshold), min_dist, C.c_float(blur), _p(out), cap)
+    return out[:n].copy()
+
+
+class FeatureTracker:
+    """feature_tracker/src/feature_tracker.rs:51-185 restated: process_frame(img) -> (ids, xy)."""
+
+    def __init__(self, w, h, cfg=None, cap=1 << 16):
+        self.cfg = cfg or ft_config()
+        self.h = load().orc_ft_create(C.byref(self.cfg), w, h)
+        self.cap = cap
+        self.ids = np.zeros(cap, np.uint64)
+        self.xy = np.zeros((cap, 2), np.float32)
+
+    def process_frame(self, img):
+        img = _f32(img)
+        n = C.c_int(0)
+        rc = load().orc_ft_process_frame(self.h, _p(img), _p(self.ids), _p(self.xy), self.cap, C.byref(n))
+        assert rc == 0, rc
+        return self.ids[:n.value].copy(), self.xy[:n.value].copy()
+
+    def __del__(self):
+        try:
+            load().orc_ft_destroy(self.h)
+        except Exception:
+            pass

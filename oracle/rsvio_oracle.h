@@ -93,6 +93,60 @@ int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t
                               orc_feature* out_r, int cap_r, int* n_r);
 void orc_tracker_remove_ids(orc_tracker* t, const uint64_t* ids, int n);
 
+/* ---------------- feature_tracker/ crate (secondary tracker variant, SURVEY T-sec) ----------------
+ * f32 images in [0, 1] (image::DynamicImage::to_luma32f, players/tartanair_player.rs:53); pyramid
+ * levels packed back to back, level l = round(w / ratio^l) x round(h / ratio^l)
+ * (image_operations.rs:69-70).  SE(2) results as float[4] = {cos, sin, tx, ty} (Isometry2). */
+typedef struct {
+    int32_t nlevels;                  /* config.yaml:1  -> 5 */
+    double ratio;                     /* :2  -> 2.0 */
+    int32_t preprocessing_blur;       /* :4  -> true */
+    float preprocessing_blur_sigma;   /* :5  -> 2.0 */
+    float detection_threshold;        /* :8  -> 2.5 */
+    uint32_t detection_min_dist;      /* :7  -> 15 */
+    float detection_blur;             /* :9  -> 6.0 */
+    int32_t optical_flow_max_iter;    /* :11 -> 25 */
+    float optical_flow_lm_lambda;     /* :12 -> 0.1 */
+    int32_t matching_cost;            /* 0 = SSD (feature_tracker.rs:125), 1 = LSSD */
+} orc_ft_config;
+
+void orc_ft_level_dims(int w, int h, int nlevels, double ratio, int* dims);
+size_t orc_ft_pyramid_floats(int w, int h, int nlevels, double ratio);
+void orc_ft_resize_triangle(const float* src, int w, int h, float* dst, int nw, int nh);
+void orc_ft_gaussian_blur(const float* src, int w, int h, float sigma, float* dst);
+void orc_ft_fast_blur(const float* src, int w, int h, float sigma, float* dst);
+void orc_ft_boxes_for_gauss(float sigma, int n, int* out);
+/* image_operations.rs:47-78 */
+void orc_ft_build_pyramid(const float* img, int w, int h, int nlevels, double ratio, int blur, float sigma,
+                          float* out);
+/* image_operations.rs:140-229: returns 0 when out of bounds; out3 = {value, d/dx, d/dy} */
+int orc_ft_bicubic(const float* img, int w, int h, float x, float y, float* out3);
+/* feature_tracking.rs:195-219, twist {theta, vx, vy} -> {cos, sin, tx, ty} */
+void orc_ft_exp_se2(const float* twist, float* out4);
+/* feature_tracking.rs:221-244, {cos, sin, tx, ty} -> {theta, vx, vy} */
+void orc_ft_log_se2(const float* iso4, float* out3);
+/* patch.rs:240-255: data[52], jac[52*3] row-major, hinv[9]; returns try_inverse's success */
+int orc_ft_patch_new(const float* img, int w, int h, float cx, float cy, float lambda, int cost, float* data,
+                     float* jac, float* hinv);
+/* feature_tracking.rs:16-61 per feature: iso_out n x 4 (forward transform), valid n */
+void orc_ft_track_points(const float* pyr0, const float* pyr1, int w, int h, int nlevels, double ratio,
+                         const float* xy, int n, int max_iter, float lambda, int cost, float* iso_out,
+                         uint8_t* valid);
+/* feature_detection.rs:82-164 */
+void orc_ft_shi_tomasi_score(const float* img, int w, int h, float blur, float* score);
+/* feature_detection.rs:171-253; returns the full count (writes <= cap) */
+int orc_ft_suppress_non_maximum(const float* score, int w, int h, int radius, float threshold, uint32_t* out_xy,
+                                float* out_score, int cap);
+/* feature_detection.rs:47-80; returns the full count of new corners (writes <= cap) */
+int orc_ft_add_points(const float* fine, int w, int h, const float* tracked_xy, int n_tracked, float threshold,
+                      int min_dist, float blur, uint32_t* out_xy, int cap);
+
+typedef struct orc_ft orc_ft;
+orc_ft* orc_ft_create(const orc_ft_config* cfg, int w, int h);
+void orc_ft_destroy(orc_ft* t);
+/* feature_tracker.rs:77-185: frame features = tracked (previous order) then new (ids ascending) */
+int orc_ft_process_frame(orc_ft* t, const float* img, uint64_t* ids_out, float* xy_out, int cap, int* n_out);
+
 /* ---------------- camera unprojection (src/estimator/frame.rs:107-134) ---------------- */
 
 /* Same layout as rsvio_camera (include/rsvio_gpu.h): model 0 = OpenCVModel5

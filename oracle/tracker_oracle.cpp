@@ -550,6 +550,11 @@ std::vector<Corner> detect_key_points(const Img& im, uint32_t grid,
 extern "C" {
 
 void orc_set_trig_mode(int mode) { g_trig_mode = mode; }
+}  // extern "C"
+
+int orc_trig_mode_internal() { return g_trig_mode; }
+
+extern "C" {
 
 void orc_se2_exp(const float* twist, float* out9) {
     Aff E = se2_exp(twist);

@@ -14,6 +14,7 @@
 // are evaluated in f64 and rounded to f32 (glibc sinf differs from that on < 1e-4 of the
 // |theta| < 2^-6 inputs the tracker produces; DESIGN.md "Tracker parity").
 #include "lk_track.hpp"
+#include "trig.hpp"
 
 namespace rsvio {
 
@@ -120,24 +121,7 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
     return C;
 }
 
-// image_utilities.rs:82-106, twist [vx, vy, theta]
-// sin / cos of an f32 angle evaluated in f64 and rounded once to f32.  The tracker's increments
-// are tiny, so |theta| < 1/16 takes a Taylor path (truncation < 1e-19 relative, i.e. the f64
-// value is within a few f64 ulp of the true one, as OCML's sin/cos are); larger angles use OCML.
-__device__ __forceinline__ void sincos_f64_rounded(float theta, float* s, float* c) {
-    const double t = (double)theta;
-    if (fabs(t) < 0.0625) {
-        const double t2 = t * t;
-        const double sp = -1.0 / 6.0 + t2 * (1.0 / 120.0 + t2 * (-1.0 / 5040.0 + t2 * (1.0 / 362880.0)));
-        const double cp = -0.5 + t2 * (1.0 / 24.0 + t2 * (-1.0 / 720.0 + t2 * (1.0 / 40320.0 + t2 * (-1.0 / 3628800.0))));
-        *s = (float)(t + t * (t2 * sp));
-        *c = (float)(1.0 + t2 * cp);
-    } else {
-        *s = (float)sin(t);
-        *c = (float)cos(t);
-    }
-}
-
+// image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos from trig.hpp
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
     float s, c;
     sincos_f64_rounded(theta, &s, &c);

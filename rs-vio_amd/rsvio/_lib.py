@@ -75,6 +75,20 @@ class BaParams(C.Structure):
                 ("max_observations", C.c_int32), ("device", C.c_int32)]
 
 
+class FtConfig(C.Structure):
+    """rsvio_ft_config (64 B): FeatureTrackingConfig (feature_tracker/src/feature_tracker.rs:25-38)."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("nlevels", C.c_int32),
+                ("preprocessing_blur", C.c_int32), ("ratio", C.c_double), ("preprocessing_blur_sigma", C.c_float),
+                ("detection_threshold", C.c_float), ("detection_min_dist", C.c_uint32), ("detection_blur", C.c_float),
+                ("optical_flow_max_iter", C.c_int32), ("optical_flow_lm_lambda", C.c_float),
+                ("matching_cost", C.c_int32), ("device", C.c_int32), ("max_features", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class FtFeature(C.Structure):
+    _fields_ = [("feature_id", C.c_uint64), ("x", C.c_float), ("y", C.c_float)]
+
+
 P = C.c_void_p
 SIG = {
     "rsvio_last_error": (C.c_char_p, []),
@@ -127,6 +141,19 @@ SIG = {
     "rsvio_ba_build_system": (C.c_int, [P, C.c_double, C.c_double, P, P, C.POINTER(C.c_double)]),
     "rsvio_rccl_unique_id": (C.c_int, [P, C.c_size_t]),
     "rsvio_ba_attach_comm": (C.c_int, [P, C.c_int32, C.c_int32, P]),
+    "rsvio_ft_create": (C.c_int, [C.POINTER(FtConfig), C.POINTER(P)]),
+    "rsvio_ft_destroy": (None, [P]),
+    "rsvio_ft_process_frame": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rsvio_ft_process_frame_device": (C.c_int, [P, P, P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rsvio_ft_get_pyramid": (C.c_int, [P, P, C.c_size_t]),
+    "rsvio_ft_stream": (P, [P]),
+    "rsvio_ft_pyramid_floats": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32, C.c_double]),
+    "rsvio_ft_build_pyramid": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_int32, C.c_float, P]),
+    "rsvio_ft_track_points": (C.c_int, [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_double, P, C.c_int32, C.c_int32,
+                                        C.c_float, C.c_int32, P, P]),
+    "rsvio_ft_shi_tomasi_score": (C.c_int, [P, C.c_int32, C.c_int32, C.c_float, P]),
+    "rsvio_ft_add_points": (C.c_int, [P, C.c_int32, C.c_int32, P, C.c_int32, C.c_float, C.c_int32, C.c_float, P,
+                                      C.c_int32, C.POINTER(C.c_int32)]),
 }
 
 _lib = None

@@ -362,3 +362,52 @@ def motion_frame(n_map: int = 2000, n_feat: int = 300, seed: int = 3, step=(0.03
     return MotionFrame(map_ids=map_ids, map_pw=map_pw, ids_l=feats[0][0], uv_l=feats[0][1], ids_r=feats[1][0],
                        uv_r=feats[1][1], T_W_B_last_kf=T_last, T_W_B_true=T_true,
                        T_C_B2=np.stack([T_C_B[0].reshape(16), T_C_B[1].reshape(16)]))
+
+
+# ---------------- feature_tracker/ crate variant (mono, f32 in [0, 1]) ----------------
+
+def make_mosaic(w: int, h: int, n_rects: int = 1500, seed: int = 20260321, size=(8.0, 60.0)):
+    """Rectangle mosaic in texture coordinates: strong, well-separated corners for Shi-Tomasi
+    (the blob texture of config 2 has too little corner energy at detection_threshold 2.5)."""
+    rng = np.random.default_rng(seed)
+    margin = 60.0
+    x0 = rng.uniform(-margin, w + margin, n_rects)
+    y0 = rng.uniform(-margin, h + margin, n_rects)
+    ww = rng.uniform(size[0], size[1], n_rects)
+    hh = rng.uniform(size[0], size[1], n_rects)
+    val = rng.uniform(0.05, 0.95, n_rects)
+    return np.stack([x0, y0, x0 + ww, y0 + hh, val], 1)
+
+
+def render_mosaic(rects: np.ndarray, w: int, h: int, t: int, noise: np.ndarray) -> np.ndarray:
+    """Frame t: texture warped by the config-2 motion (0.2 deg/frame about the centre, then a
+    (1.7, -0.9) px/frame shift), painter's order, plus noise; f32 clamped to [0, 1]."""
+    ang = math.radians(0.2) * t
+    ca, sa = math.cos(ang), math.sin(ang)
+    sx, sy = 1.7 * t, -0.9 * t
+    cx, cy = w / 2.0, h / 2.0
+    img = np.full((h, w), 0.5)
+    for x0, y0, x1, y1, v in rects:
+        cs = np.array([[x0, y0], [x1, y0], [x0, y1], [x1, y1]])
+        px = ca * (cs[:, 0] - cx) - sa * (cs[:, 1] - cy) + cx + sx
+        py = sa * (cs[:, 0] - cx) + ca * (cs[:, 1] - cy) + cy + sy
+        a0, a1 = max(0, int(px.min()) - 1), min(w, int(px.max()) + 2)
+        b0, b1 = max(0, int(py.min()) - 1), min(h, int(py.max()) + 2)
+        if a0 >= a1 or b0 >= b1:
+            continue
+        ys, xs = np.mgrid[b0:b1, a0:a1].astype(np.float64)
+        x = xs - cx - sx
+        y = ys - cy - sy
+        u = ca * x + sa * y + cx
+        v_ = -sa * x + ca * y + cy
+        m = (u >= x0) & (u < x1) & (v_ >= y0) & (v_ < y1)
+        img[b0:b1, a0:a1][m] = v
+    return np.clip(img + noise, 0.0, 1.0).astype(np.float32)
+
+
+def mono_sequence(n_frames: int, w: int = 752, h: int = 480, seed: int = 20260321):
+    """Yield f32 frames (luma in [0, 1], as DynamicImage::to_luma32f) for the crate tracker."""
+    rects = make_mosaic(w, h, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    for t in range(n_frames):
+        yield render_mosaic(rects, w, h, t, 0.01 * rng.standard_normal((h, w)))

@@ -77,7 +77,52 @@ def ba_golden():
                         initial_cost=res.initial_cost, final_cost=res.final_cost)
 
 
+def ft_frames(n, w=160, h=120, seed=31):
+    """Noise-free mosaic frames (piecewise constant: the fixture compresses to a few KB)."""
+    rects = S.make_mosaic(w, h, n_rects=160, seed=seed, size=(6.0, 28.0))
+    return np.stack([S.render_mosaic(rects, w, h, t, np.zeros((h, w))) for t in range(n)])
+
+
+def sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def ft_golden():
+    """feature_tracker/ crate variant: 160 x 120 mosaic frames, 3 levels (trig mode 1 = the GPU's
+    f64-rounded sin/cos).  Large float outputs are pinned by SHA-256 of their bytes."""
+    w, h, L = 160, 120, 3
+    frames = ft_frames(4, w, h)
+    O.set_trig_mode(1)
+    pyr0 = O.ft_build_pyramid(frames[0], L)
+    pyr1 = O.ft_build_pyramid(frames[1], L)
+    pyr0_noblur = O.ft_build_pyramid(frames[0], L, blur=False)
+    fine0 = pyr0[:w * h].reshape(h, w)
+    score0 = O.ft_shi_tomasi_score(fine0)
+    new0 = O.ft_add_points(fine0)
+    trk_xy = (new0[: len(new0) // 2].astype(np.float32) + np.float32(0.3))
+    new0_tr = O.ft_add_points(fine0, trk_xy)
+    xy = new0.astype(np.float32)
+    iso_ssd, v_ssd = O.ft_track_points(pyr0, pyr1, w, h, xy, nlevels=L, cost=0)
+    iso_lssd, v_lssd = O.ft_track_points(pyr0, pyr1, w, h, xy, nlevels=L, cost=1)
+    ft = O.FeatureTracker(w, h, O.ft_config(nlevels=L))
+    pipe = []
+    for k in range(len(frames)):
+        ids, fxy = ft.process_frame(frames[k])
+        pipe += [(k, int(i), float(p[0]), float(p[1])) for i, p in zip(ids, fxy)]
+    O.set_trig_mode(0)
+    np.savez_compressed(OUT / "ft_small.npz", w=w, h=h, levels=L, frames=frames, sha_pyr0=sha(pyr0),
+                        sha_pyr1=sha(pyr1), sha_pyr0_noblur=sha(pyr0_noblur), sha_score0=sha(score0), new0=new0,
+                        trk_xy=trk_xy, new0_tr=new0_tr, xy=xy, iso_ssd=iso_ssd, v_ssd=v_ssd, iso_lssd=iso_lssd,
+                        v_lssd=v_lssd, pipe=np.array(pipe, np.float64))
+
+
 if __name__ == "__main__":
-    tracker_golden()
-    ba_golden()
+    which = sys.argv[1:] or ["tracker", "ba", "ft"]
+    if "tracker" in which:
+        tracker_golden()
+    if "ba" in which:
+        ba_golden()
+    if "ft" in which:
+        ft_golden()
     print("wrote", sorted(p.name for p in OUT.glob("*.npz")))

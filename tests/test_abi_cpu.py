@@ -46,6 +46,8 @@ def test_struct_layouts():
     assert C.sizeof(_lib.TrackerParams) == 32
     assert C.sizeof(_lib.TrackBatch) == 48
     assert C.sizeof(_lib.Camera) == 88
+    assert C.sizeof(_lib.FtConfig) == 64
+    assert C.sizeof(_lib.FtFeature) == 16
 
 
 def test_camera_struct_matches_oracle_layout():
@@ -72,3 +74,12 @@ def test_invalid_arguments_rejected_without_device():
     cam.model, cam.params[0], cam.params[1] = 0, 0.0, 1.0
     assert lib.rsvio_unproject(C.byref(cam), None, 0, None, None) == -1      # fx == 0
     assert lib.rsvio_tracker_set_cameras(None, None, None) == -1
+    # feature_tracker/ crate variant
+    assert lib.rsvio_ft_create(None, None) == -1
+    assert lib.rsvio_ft_pyramid_floats(752, 480, 5, 2.0) == 752 * 480 + 376 * 240 + 188 * 120 + 94 * 60 + 47 * 30
+    assert lib.rsvio_ft_pyramid_floats(752, 480, 0, 2.0) == 0
+    assert lib.rsvio_ft_track_points(None, None, 10, 10, 1, 2.0, None, 0, 25, C.c_float(0.1), 0, None, None) == -1
+    n = C.c_int32()
+    assert lib.rsvio_ft_add_points(img.ctypes.data, 10, 10, None, 0, C.c_float(2.5), 15, C.c_float(6.0), None, 0,
+                                   C.byref(n)) == -1                      # 2 * min_dist >= image size
+    assert lib.rsvio_ft_process_frame(None, None, 0, None, 0, None) == -1
