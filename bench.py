@@ -164,7 +164,81 @@ def measure_rows(device: int, cpu: bool, reps: int = 200):
                                "sample": f"{k} frames, oracle orc_track_motion"}
     out["track_motion"] = row
     mt.close()
+    out["ft_tracker"] = measure_ft_row(device, cpu)
     return out
+
+
+FT_LEVELS = 5                  # feature_tracker/config/config.yaml
+
+
+def ft_bytes_per_frame(n_tracked: int, w: int = W, h: int = H, levels: int = FT_LEVELS) -> int:
+    """Algorithmic HBM bytes of one FeatureTracker frame: pyramid (blur:
+    read + write the image; each level: read the previous level + write itself), Shi-Tomasi
+    (grad: read 1 + write 3 planes; fast_blur: 6 half passes over 3 planes, read + write; score:
+    read 3 + write 1; NMS: read 1 -> 45 plane passes) and LK (2 calls per tracked feature, an 18x18
+    f32 bicubic footprint of the 52-point pattern in template and target image per (call, level),
+    16 B of feature state per call)."""
+    dims = [(w, h)] + [(int(w / 2 ** l + 0.5), int(h / 2 ** l + 0.5)) for l in range(1, levels)]
+    px = [a * b for a, b in dims]
+    pyr = 4 * (2 * px[0] + sum(px[l - 1] + px[l] for l in range(1, levels)))
+    det = 4 * 45 * w * h
+    calls = 2 * n_tracked
+    return pyr + det + calls * levels * 2 * 18 * 18 * 4 + calls * 16
+
+
+def measure_ft_row(device: int, cpu: bool, reps: int = 60):
+    """T-sec: the feature_tracker/ crate's FeatureTracker::process_frame (feature_tracker.rs:77-185)
+    on a 752x480 f32 mosaic stream with config.yaml's parameters; frames resident on the device;
+    per-frame device time from HIP events on the tracker's stream; the frame list is read back
+    every frame (the API returns it)."""
+    import torch
+
+    from rsvio import ft
+    from rsvio import synthetic as S
+    frames = list(S.mono_sequence(6))
+    d = torch.from_numpy(np.stack(frames)).to(f"cuda:{device}")
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 3, 4, 5, 4, 3, 2, 1]          # palindromic: one frame of motion per step
+    t = ft.FeatureTracker(W, H, device=device)
+    for k in range(10):
+        t.process_frame_device(d[order[k % len(order)]].data_ptr())
+    st = torch.cuda.ExternalStream(t.stream, device=f"cuda:{device}")
+    evs, nfeat = [], []
+    t0 = time.perf_counter()
+    for k in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        nfeat.append(t.process_frame_device(d[order[k % len(order)]].data_ptr()))
+        b.record(st)
+        evs.append((a, b))
+    wall = (time.perf_counter() - t0) / reps
+    st.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    n = float(np.mean(nfeat))
+    byts = ft_bytes_per_frame(int(n))
+    gbs = byts / (ms * 1e-3) / 1e9
+    t.close()
+    row = {"workload": "feature_tracker crate FeatureTracker::process_frame, 752x480 f32 mosaic stream, "
+                       "config.yaml (5 levels, blur 2.0, Shi-Tomasi blur 6.0, min_dist 15, LM 25 it, lambda 0.1)",
+           "value": round(1.0 / wall, 1), "unit": "frames/s", "features_per_frame": round(n, 1),
+           "device_ms_per_frame": round(ms, 4), "host_inclusive_ms": round(wall * 1e3, 4),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 6), "algorithmic_bytes_per_frame": byts,
+                        "note": "whole frame (pyramid + LK + Shi-Tomasi); latency-bound: serial LK chains "
+                                "and fast_blur's sequential running sums (profiles/r01_ft_kernel_stats.csv)"}}
+    if cpu:
+        from oracle import oracle as O
+        ref = O.FeatureTracker(W, H)
+        ref.process_frame(frames[0])
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 3.0 or k < 5:
+            ref.process_frame(frames[order[(k + 1) % len(order)]])
+            k += 1
+        cms = 1e3 * (time.perf_counter() - t0) / k
+        row["cpu_baseline"] = {"value": round(1e3 / cms, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} frames of the same stream, oracle/ft_oracle.cpp, 1 thread"}
+    return row
 
 
 def pmc_traffic(kernel: str):

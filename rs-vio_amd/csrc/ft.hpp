@@ -77,8 +77,12 @@ struct DetectBufs {
     float* score;          // w x h
     uint32_t* nms;         // nbx x nby packed corner (x | y << 16) or kNone
     float* nms_score;      // nbx x nby
-    uint32_t* stats;       // [0] max(bits(score)) + 1 over corners (0: none), [1] max candidate y + 1
+    uint32_t* stats;       // [0] max(bits(score)) + 1 over corners (0: none), [1] max candidate y + 1,
+                           // [2] corner count
+    uint32_t* clist;       // corner block indices (any order)
+    uint8_t* keep;         // nbx x nby: corner survives local_maxima and the border filter
     uint2* tpos;           // tracked positions (round, saturating) or {kNone, kNone}
+    uint8_t* supp;         // nbx x nby: corner suppressed by a tracked feature
     int tpos_cap;
     uint32_t* staging;     // nby x nbx survivors (x | y << 16), (y, x) order within a block row
     int* row_count;        // nby

@@ -9,10 +9,14 @@
 //   Kb  box half:  fast_blur's running box sum, one lane per (plane, row) -- the reference's
 //                  sequential f32 sum is kept -- output transposed (coalesced stores); 6 launches
 //   Ks  score:     one lane per pixel
-//   Kn  NMS:       one lane per (r+1) x (r+1) block (+ the tracked positions, rounded)
-//   Kl  local max: one workgroup per block row; survivors ranked in (y, x) order in LDS
+//   Kn  NMS:       one lane per (r+1) x (r+1) block (+ the tracked positions, rounded), corner list
+//   Kt  tracked:   one wave per tracked feature marks the corners it suppresses
+//   Kc  local max: one wave per corner, lanes over the window's NMS blocks
+//   Kr  rank:      one workgroup per block row; survivors ranked in (y, x) order
 //   Ka  assemble:  one workgroup: surviving tracks, then new corners with consecutive ids
+#include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <stdexcept>
 
 #include "ft.hpp"
@@ -52,40 +56,110 @@ __global__ __launch_bounds__(256) void ft_grad_kernel(const float* __restrict__ 
 
 // image 0.25 fast_blur horizontal_fast_blur_half: per row a running sum over a (2r+1) window
 // (clamp-to-edge), value = clamp(sum / (2r + 1), 0, 1), written transposed.  The running sum is
-// the reference's sequential f32 recurrence, so each (plane, row) is one lane's serial loop.
-__global__ __launch_bounds__(64) void ft_boxblur_half(const float* __restrict__ in, float* __restrict__ out,
-                                                      int width, int rows, int r, long plane) {
-    const int row = blockIdx.x * 64 + threadIdx.x;
-    if (row >= rows) return;
-    const float* __restrict__ s = in + blockIdx.y * plane + (size_t)row * width;
-    float* __restrict__ d = out + blockIdx.y * plane + row;
+// the reference's sequential f32 recurrence, so one lane owns one row for the whole pass.
+// A workgroup (4 waves) owns 64 rows and walks them in chunks of kCW columns, pipelined:
+//   wave 0     runs the recurrence of chunk k from LDS (2 LDS reads, 2 adds, 1 LDS write a step)
+//   waves 1-3  divide / clamp / store chunk k-1 (coalesced: consecutive rows of one column) and
+//              stage chunk k+1's input window in LDS (coalesced along the row)
+constexpr int kCW = 32;      // columns per chunk
+constexpr int kVS = kCW + 1; // LDS row stride of the running-sum buffer
+
+__host__ __device__ inline int bb_stride(int r) {
+    const int s = kCW + 2 * r + 1;
+    return (s & 1) ? s : s + 1;  // odd row stride: lanes (rows) on distinct banks
+}
+
+__global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__ in, float* __restrict__ out,
+                                                       int width, int rows, int r, long plane) {
+    extern __shared__ float sm[];   // T[2][64][S] | V[2][64][kVS]  (offsets, not pointers: keeps ds_* ops)
+    const int S = bb_stride(r);
+    const int tbuf = 64 * S, vbase = 128 * S, vbuf = 64 * kVS;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int row0 = blockIdx.x * 64;
+    const float* __restrict__ src = in + blockIdx.y * plane;
+    float* __restrict__ dst = out + blockIdx.y * plane;
+    const int ncol = kCW + 2 * r + 1;
+    const int nch = (width + kCW - 1) / kCW;
     const int last = width - 1;
-    float val = -0.0f;  // Rust's float Sum starts from -0.0
-    for (int x = -r; x <= r; ++x) val = val + s[min(max(x, 0), last)];
     const float den = 2.0f * (float)r + 1.0f;
-    // the window's trailing / leading samples are independent of the running sum: load ahead
-    constexpr int U = 8;
-    int col = 0;
-    for (; col + U <= width; col += U) {
-        float a[U], b[U];
+    // tile column j of chunk c0 holds source column clamp(c0 - r + j).  Waves [wf, wf + NW) stage
+    // the tile, one row per wave at a time (lanes j and j + 64 of the row: coalesced); every load
+    // of a lane is issued before its LDS writes.
+    auto load_tile = [&](auto nw_tag, int toff, int c0, int wf) {
+        constexpr int NW = decltype(nw_tag)::value;
+        constexpr int M = (64 + NW - 1) / NW;
+        const int wv = wave - wf;
+        const int x0 = min(max(c0 - r + lane, 0), last), x1 = min(max(c0 - r + lane + 64, 0), last);
+        const bool in0 = lane < ncol, in1 = lane + 64 < ncol;
+        float v0[M], v1[M];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            a[u] = s[max(col + u - r, 0)];
-            b[u] = s[min(col + u + r + 1, last)];
+        for (int m = 0; m < M; ++m) {
+            const int rr = wv + m * NW;
+            const float* p = src + (size_t)min(row0 + min(rr, 63), rows - 1) * width;
+            v0[m] = (rr < 64 && in0) ? p[x0] : 0.0f;
+            v1[m] = (rr < 64 && in1) ? p[x1] : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            float v = val / den;
-            v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-            d[(size_t)(col + u) * rows] = v;
-            val = val - a[u] + b[u];
+        for (int m = 0; m < M; ++m) {
+            const int rr = wv + m * NW;
+            if (rr < 64 && in0) {
+                sm[toff + rr * S + lane] = v0[m];
+                if (in1) sm[toff + rr * S + lane + 64] = v1[m];
+            }
         }
-    }
-    for (; col < width; ++col) {
-        float v = val / den;
-        v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-        d[(size_t)col * rows] = v;
-        val = val - s[max(col - r, 0)] + s[min(col + r + 1, last)];
+    };
+    load_tile(std::integral_constant<int, 4>{}, 0, 0, 0);
+    __syncthreads();
+    float val = -0.0f;  // Rust's float Sum starts from -0.0
+    if (wave == 0)
+        for (int j = 0; j <= 2 * r; ++j) val = val + sm[lane * S + j];
+    for (int k = 0; k <= nch; ++k) {
+        if (wave == 0) {
+            if (k < nch) {
+                const int cw = min(kCW, width - k * kCW);
+                const int tr = (k & 1) * tbuf + lane * S;
+                const int vr = vbase + (k & 1) * vbuf + lane * kVS;
+                const int o = 2 * r + 1;
+                if (cw == kCW) {
+                    // all window samples first (independent of the running sum), then the chain
+                    float A[kCW], B[kCW], Vv[kCW];
+#pragma unroll
+                    for (int j = 0; j < kCW; ++j) {
+                        A[j] = sm[tr + j];
+                        B[j] = sm[tr + o + j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kCW; ++j) {
+                        Vv[j] = val;
+                        val = (val - A[j]) + B[j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kCW; ++j) sm[vr + j] = Vv[j];
+                } else {
+                    for (int j = 0; j < cw; ++j) {
+                        sm[vr + j] = val;
+                        val = (val - sm[tr + j]) + sm[tr + j + o];
+                    }
+                }
+            }
+        } else {
+            const int t = tid - 64;
+            if (k >= 1) {
+                const int c0 = (k - 1) * kCW;
+                const int cw = min(kCW, width - c0);
+                const int vp = vbase + ((k - 1) & 1) * vbuf;
+                for (int i = t; i < 64 * cw; i += 192) {
+                    const int col = i >> 6, rr = i & 63;
+                    if (row0 + rr < rows) {
+                        float v = sm[vp + rr * kVS + col] / den;
+                        v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+                        dst[(size_t)(c0 + col) * rows + row0 + rr] = v;
+                    }
+                }
+            }
+            if (k + 1 < nch) load_tile(std::integral_constant<int, 3>{}, ((k + 1) & 1) * tbuf, (k + 1) * kCW, 1);
+        }
+        __syncthreads();
     }
 }
 
@@ -120,11 +194,14 @@ __device__ __forceinline__ bool contains_greater(const float* __restrict__ s, in
 
 // suppress_non_maximum (feature_detection.rs:171-253), one lane per (r+1) x (r+1) block; lanes
 // past the blocks publish the tracked positions (add_points :61-66 rounds them to u32).
+// Corners are appended (any order) to clist for the per-corner local-maximum test.
 __global__ __launch_bounds__(256) void ft_nms_kernel(const float* __restrict__ s, int w, int h, int r, float thr,
                                                      int nbx, int nby, uint32_t* __restrict__ nms,
                                                      float* __restrict__ nms_score, uint32_t* __restrict__ stats,
                                                      const float2* __restrict__ txy, const uint8_t* __restrict__ tvalid,
-                                                     int n_tracked, uint2* __restrict__ tpos) {
+                                                     int n_tracked, uint2* __restrict__ tpos,
+                                                     uint8_t* __restrict__ supp, uint8_t* __restrict__ keep,
+                                                     uint32_t* __restrict__ clist) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int nb = nbx * nby;
     if (gid >= nb) {
@@ -168,79 +245,111 @@ __global__ __launch_bounds__(256) void ft_nms_kernel(const float* __restrict__ s
             out = bx | (by << 16);
             atomicMax(&stats[0], __float_as_uint(best) + 1u);  // scores are >= 0: bit order = value order
             atomicMax(&stats[1], by + 1u);
+            clist[atomicAdd(&stats[2], 1u)] = (uint32_t)gid;
         }
     }
     nms[gid] = out;
     nms_score[gid] = best;
+    supp[gid] = 0;
+    keep[gid] = 0;
 }
 
-// imageproc suppress::local_maxima (feature_detection.rs:68) + the filter of :70-79, one
-// workgroup per NMS block row.  A corner survives unless some candidate in rows
-// [y - md, min(y + md + 1, height)) and columns [x - md, x + md] has a greater score, or an equal
-// score at a smaller (y, x); height = the largest candidate y.  Tracked features (score
-// max + 1) are candidates but never survivors.  Survivors are ranked in (y, x) order.
-__global__ __launch_bounds__(1024) void ft_local_max_kernel(const uint32_t* __restrict__ nms,
+// imageproc suppress::local_maxima (feature_detection.rs:68): candidate c survives unless some
+// candidate in rows [y - md, min(y + md + 1, height)) and columns [x - md, x + md] has a greater
+// score, or an equal score at a smaller (y, x); height = the largest candidate y.
+__device__ __forceinline__ bool beats(uint32_t ny, uint32_t nx, float ns, uint32_t cy, uint32_t cx, float cs,
+                                      uint32_t lo, uint32_t hi, unsigned long long md) {
+    return ny >= lo && ny < hi && (unsigned long long)nx + md >= cx && (unsigned long long)nx <= cx + md &&
+           (ns > cs || (ns == cs && (ny < cy || (ny == cy && nx < cx))));
+}
+
+// The tracked features' side: all of them score max(corner scores) + 1 (feature_detection.rs:61-66).
+// One wave per tracked feature t marks the corners c it beats; t can lie in c's window only if
+// |cx - tx| <= md and |cy - ty| <= md, i.e. in a (2 md + 1)^2 box of NMS blocks (lanes in parallel).
+__global__ __launch_bounds__(256) void ft_tracked_suppress_kernel(const uint2* __restrict__ tpos, int n_tracked,
+                                                                  const uint32_t* __restrict__ nms,
+                                                                  const float* __restrict__ nms_score,
+                                                                  const uint32_t* __restrict__ stats, int r, int nbx,
+                                                                  int nby, int md, uint8_t* __restrict__ supp) {
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (i >= n_tracked) return;
+    const uint2 t = tpos[i];
+    if (t.x == kNone) return;
+    const unsigned long long step = (unsigned long long)r + 1ull, MD = (unsigned long long)md;
+    const uint32_t height = stats[1] > 0u ? stats[1] - 1u : 0u;
+    const float ts = (stats[0] ? __uint_as_float(stats[0] - 1u) : -INFINITY) + 1.0f;
+    const unsigned long long tx = t.x, ty = t.y;
+    const long long by0 = (long long)((ty > MD ? ty - MD : 0ull) / step);
+    const long long by1 = min((long long)nby - 1, (long long)((ty + MD) / step));
+    const long long bx0 = (long long)((tx > MD ? tx - MD : 0ull) / step);
+    const long long bx1 = min((long long)nbx - 1, (long long)((tx + MD) / step));
+    if (by1 < by0 || bx1 < bx0) return;
+    const int nbw = (int)(bx1 - bx0 + 1), ncell = (int)(by1 - by0 + 1) * nbw;
+    for (int k = lane; k < ncell; k += 64) {
+        const int q = k / nbw;
+        const long long g = (by0 + q) * nbx + bx0 + (k - q * nbw);
+        const uint32_t c = nms[g];
+        if (c == kNone) continue;
+        const uint32_t cx = c & 0xFFFFu, cy = c >> 16;
+        const uint32_t lo = (uint32_t)md > cy ? 0u : cy - (uint32_t)md;
+        const uint32_t hi = cy + (uint32_t)md + 1u > height ? height : cy + (uint32_t)md + 1u;
+        if (beats((uint32_t)ty, (uint32_t)tx, ts, cy, cx, nms_score[g], lo, hi, MD)) supp[g] = 1;
+    }
+}
+
+// The corners' side of local_maxima + the filter of add_points :70-79, one wave per corner
+// (persistent waves over clist): the lanes test the window's NMS blocks in parallel.
+__global__ __launch_bounds__(256) void ft_corner_max_kernel(const uint32_t* __restrict__ clist,
+                                                            const uint32_t* __restrict__ stats,
+                                                            const uint32_t* __restrict__ nms,
                                                             const float* __restrict__ nms_score,
-                                                            const uint32_t* __restrict__ stats, int w, int h, int r,
-                                                            int nbx, int nby, int md, const uint2* __restrict__ tpos,
-                                                            int n_tracked, uint32_t* __restrict__ staging,
-                                                            int* __restrict__ row_count) {
-    __shared__ uint2 tl[1024];
+                                                            const uint8_t* __restrict__ supp, int w, int h, int r,
+                                                            int nbx, int nby, int md, uint8_t* __restrict__ keep) {
+    const int n = (int)stats[2];
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t step = (uint32_t)r + 1u, MD = (uint32_t)md;
+    const uint32_t height = stats[1] > 0u ? stats[1] - 1u : 0u;
+    for (int q = wave; q < n; q += nwaves) {
+        const uint32_t g = clist[q];
+        const uint32_t c = nms[g];
+        const float cs = nms_score[g];
+        const uint32_t cx = c & 0xFFFFu, cy = c >> 16;
+        const uint32_t lo = MD > cy ? 0u : cy - MD;
+        const uint32_t hi = cy + MD + 1u > height ? height : cy + MD + 1u;
+        bool ok = !supp[g] && cx >= MD && cx < (uint32_t)w - MD && cy >= MD && cy < (uint32_t)h - MD;
+        if (ok && hi > lo) {
+            const int b0 = (int)(lo / step), b1 = min(nby - 1, (int)((hi - 1u) / step));
+            const int c0 = (int)((cx >= MD ? cx - MD : 0u) / step), c1 = min(nbx - 1, (int)((cx + MD) / step));
+            const int nbw = c1 - c0 + 1, ncell = (b1 - b0 + 1) * nbw;
+            bool beaten = false;
+            for (int k = lane; k < ncell; k += 64) {
+                const int qq = k / nbw;
+                const int gg = (b0 + qq) * nbx + c0 + (k - qq * nbw);
+                const uint32_t e = nms[gg];
+                if (e != kNone && (uint32_t)gg != g)
+                    beaten |= beats(e >> 16, e & 0xFFFFu, nms_score[gg], cy, cx, cs, lo, hi, MD);
+            }
+            ok = __ballot(beaten) == 0ull;
+        }
+        if (lane == 0) keep[g] = ok ? 1 : 0;
+    }
+}
+
+// Survivors of one NMS block row ranked in (y, x) order (sub-row y - by (r+1) first, then block
+// column) -> staging[by][rank], row_count[by].
+__global__ __launch_bounds__(1024) void ft_rank_kernel(const uint32_t* __restrict__ nms,
+                                                       const uint8_t* __restrict__ keep, int r, int nbx,
+                                                       uint32_t* __restrict__ staging, int* __restrict__ row_count) {
     __shared__ int scan[1024];
     const int by = blockIdx.x, bx = threadIdx.x;
-    const uint32_t step = (uint32_t)r + 1u, MD = (uint32_t)md;
-    const uint32_t c = bx < nbx ? nms[by * nbx + bx] : kNone;
-    const bool has = c != kNone;
-    const uint32_t cx = c & 0xFFFFu, cy = c >> 16;
-    const float cs = has ? nms_score[by * nbx + bx] : 0.0f;
-    const uint32_t height = stats[1] > 0u ? stats[1] - 1u : 0u;
-    const uint32_t lo = MD > cy ? 0u : cy - MD;
-    const uint32_t hi = cy + MD + 1u > height ? height : cy + MD + 1u;
-    bool keep = has;
-    if (keep && hi > lo) {
-        const int b0 = (int)(lo / step), b1 = (int)((hi - 1u) / step);
-        const int c0 = (int)((cx >= MD ? cx - MD : 0u) / step);
-        const int c1 = min(nbx - 1, (int)((cx + MD) / step));
-        for (int yb = b0; yb <= b1 && keep; ++yb)
-            for (int xb = c0; xb <= c1; ++xb) {
-                const uint32_t n = nms[yb * nbx + xb];
-                if (n == kNone || (yb == by && xb == bx)) continue;
-                const uint32_t nx = n & 0xFFFFu, ny = n >> 16;
-                if (ny < lo || ny >= hi || nx + MD < cx || nx > cx + MD) continue;
-                const float ns = nms_score[yb * nbx + xb];
-                if (ns > cs || (ns == cs && (ny < cy || (ny == cy && nx < cx)))) {
-                    keep = false;
-                    break;
-                }
-            }
-    }
-    // tracked candidates: all scored max(corner scores) + 1 (feature_detection.rs:61-66)
-    const float mx = stats[0] ? __uint_as_float(stats[0] - 1u) : -INFINITY;
-    const float ts = mx + 1.0f;
-    for (int t0 = 0; t0 < n_tracked; t0 += 1024) {
-        const int nt = min(1024, n_tracked - t0);
-        __syncthreads();
-        if ((int)threadIdx.x < nt) tl[threadIdx.x] = tpos[t0 + threadIdx.x];
-        __syncthreads();
-        if (!keep || hi <= lo) continue;
-        for (int k = 0; k < nt; ++k) {
-            const uint2 t = tl[k];
-            if (t.x == kNone) continue;
-            if (t.y < lo || t.y >= hi) continue;
-            if ((unsigned long long)t.x + MD < cx || (unsigned long long)t.x > (unsigned long long)cx + MD) continue;
-            if (ts > cs || (ts == cs && (t.y < cy || (t.y == cy && t.x < cx)))) {
-                keep = false;
-                break;
-            }
-        }
-    }
-    // add_points :70-79: new corners inside [md, w - md) x [md, h - md)
-    keep = keep && cx >= MD && cx < (uint32_t)w - MD && cy >= MD && cy < (uint32_t)h - MD;
-    // rank in (y, x) order: sub-row s = y - by * step first, then block column
-    const uint32_t sub = has ? cy - (uint32_t)by * step : 0u;
+    const uint32_t step = (uint32_t)r + 1u;
+    const bool kp = bx < nbx && keep[by * nbx + bx];
+    const uint32_t c = kp ? nms[by * nbx + bx] : kNone;
+    const uint32_t sub = kp ? (c >> 16) - (uint32_t)by * step : 0u;
     int base = 0;
     for (uint32_t sr = 0; sr < step; ++sr) {
-        const int f = keep && sub == sr ? 1 : 0;
+        const int f = kp && sub == sr ? 1 : 0;
         __syncthreads();
         scan[threadIdx.x] = f;
         __syncthreads();
@@ -342,11 +451,14 @@ void enqueue_score(const DetectBufs& D, const float* fine, hipStream_t s) {
     RSVIO_HIP(hipGetLastError());
     for (int k = 0; k < 3; ++k) {
         const int r = (D.boxes[k] - 1) / 2;
-        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.h + 63) / 64, 3), dim3(64), 0, s, D.planes, D.tmp, D.w, D.h, r,
-                           (long)n);
+        if (r > 15) throw std::invalid_argument("detection_blur too large (fast_blur box radius > 15)");  // kCW + 2r + 1 <= 128
+        const size_t lds = sizeof(float) * (128 * (size_t)bb_stride(r) + 128 * kVS);
+        if (lds > 64 * 1024) throw std::invalid_argument("detection_blur too large for the box-blur tile");
+        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.h + 63) / 64, 3), dim3(256), lds, s, D.planes, D.tmp, D.w, D.h,
+                           r, (long)n);
         RSVIO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.w + 63) / 64, 3), dim3(64), 0, s, D.tmp, D.planes, D.h, D.w, r,
-                           (long)n);
+        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.w + 63) / 64, 3), dim3(256), lds, s, D.tmp, D.planes, D.h, D.w,
+                           r, (long)n);
         RSVIO_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(ft_score_kernel, dim3((n + 255) / 256), dim3(256), 0, s, D.planes, n, D.score);
@@ -356,15 +468,24 @@ void enqueue_score(const DetectBufs& D, const float* fine, hipStream_t s) {
 void enqueue_select(const DetectBufs& D, float threshold, int min_dist, const float2* tracked_xy,
                     const uint8_t* tracked_valid, int n_tracked, hipStream_t s) {
     if (n_tracked > D.tpos_cap) throw std::invalid_argument("too many tracked features");
-    if (D.nbx > 1024) throw std::invalid_argument("image too wide for the local-maxima workgroup");
-    RSVIO_HIP(hipMemsetAsync(D.stats, 0, 2 * sizeof(uint32_t), s));
+    if (D.nbx > 1024) throw std::invalid_argument("image too wide for the ranking workgroup");
+    RSVIO_HIP(hipMemsetAsync(D.stats, 0, 4 * sizeof(uint32_t), s));
     const int total = D.nbx * D.nby + n_tracked;
     hipLaunchKernelGGL(ft_nms_kernel, dim3((total + 255) / 256), dim3(256), 0, s, D.score, D.w, D.h, D.r, threshold,
-                       D.nbx, D.nby, D.nms, D.nms_score, D.stats, tracked_xy, tracked_valid, n_tracked, D.tpos);
+                       D.nbx, D.nby, D.nms, D.nms_score, D.stats, tracked_xy, tracked_valid, n_tracked, D.tpos,
+                       D.supp, D.keep, D.clist);
+    RSVIO_HIP(hipGetLastError());
+    if (n_tracked > 0) {
+        hipLaunchKernelGGL(ft_tracked_suppress_kernel, dim3((n_tracked + 3) / 4), dim3(256), 0, s, D.tpos, n_tracked,
+                           D.nms, D.nms_score, D.stats, D.r, D.nbx, D.nby, min_dist, D.supp);
+        RSVIO_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(ft_corner_max_kernel, dim3(512), dim3(256), 0, s, D.clist, D.stats, D.nms, D.nms_score, D.supp,
+                       D.w, D.h, D.r, D.nbx, D.nby, min_dist, D.keep);
     RSVIO_HIP(hipGetLastError());
     const int threads = ((D.nbx + 63) / 64) * 64;
-    hipLaunchKernelGGL(ft_local_max_kernel, dim3(D.nby), dim3(threads), 0, s, D.nms, D.nms_score, D.stats, D.w, D.h,
-                       D.r, D.nbx, D.nby, min_dist, D.tpos, n_tracked, D.staging, D.row_count);
+    hipLaunchKernelGGL(ft_rank_kernel, dim3(D.nby), dim3(threads), 0, s, D.nms, D.keep, D.r, D.nbx, D.staging,
+                       D.row_count);
     RSVIO_HIP(hipGetLastError());
 }
 

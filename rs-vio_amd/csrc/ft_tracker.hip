@@ -26,6 +26,8 @@ struct Scratch {
     DevBuf<float> planes, tmp, score, nms_score;
     DevBuf<uint32_t> nms, stats, staging;
     DevBuf<uint2> tpos;
+    DevBuf<uint8_t> supp, keep;
+    DevBuf<uint32_t> clist;
     DevBuf<int> row_count;
     DetectBufs D{};
 
@@ -42,9 +44,12 @@ struct Scratch {
         score.alloc(n);
         nms.alloc((size_t)D.nbx * D.nby);
         nms_score.alloc((size_t)D.nbx * D.nby);
-        stats.alloc(2);
+        stats.alloc(4);
         staging.alloc((size_t)D.nbx * D.nby);
         tpos.alloc(std::max(1, tracked_cap));
+        supp.alloc((size_t)D.nbx * D.nby);
+        keep.alloc((size_t)D.nbx * D.nby);
+        clist.alloc((size_t)D.nbx * D.nby);
         row_count.alloc(D.nby);
         D.planes = planes.p;
         D.tmp = tmp.p;
@@ -53,6 +58,9 @@ struct Scratch {
         D.nms_score = nms_score.p;
         D.stats = stats.p;
         D.tpos = tpos.p;
+        D.supp = supp.p;
+        D.keep = keep.p;
+        D.clist = clist.p;
         D.tpos_cap = std::max(1, tracked_cap);
         D.staging = staging.p;
         D.row_count = row_count.p;
