@@ -1,10 +1,11 @@
 """Summarise a rocprofv3 kernel_stats.csv (and the BA kernel sequence of the last solve)."""
 import csv
+import re
 import sys
 
 d = sys.argv[1]
 for r in csv.DictReader(open(f"{d}/run_kernel_stats.csv")):
-    n = r["Name"].replace("rsvio::(anonymous namespace)::", "").split("(")[0]
+    n = re.sub(r"\(anonymous namespace\)::", "", r["Name"]).split("(")[0].replace("rsvio::", "")
     print(f"{n:36s} calls {r['Calls']:>5s} avg {float(r['AverageNs']) / 1000:8.2f} us  total "
           f"{float(r['TotalDurationNs']) / 1e3:9.1f} us")
 rows = sorted(csv.DictReader(open(f"{d}/run_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
