@@ -15,6 +15,7 @@
 //   Kr  rank:      one workgroup per block row; survivors ranked in (y, x) order
 //   Ka  assemble:  one workgroup: surviving tracks, then new corners with consecutive ids
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <type_traits>
 #include <stdexcept>
@@ -57,20 +58,28 @@ __global__ __launch_bounds__(256) void ft_grad_kernel(const float* __restrict__ 
 // image 0.25 fast_blur horizontal_fast_blur_half: per row a running sum over a (2r+1) window
 // (clamp-to-edge), value = clamp(sum / (2r + 1), 0, 1), written transposed.  The running sum is
 // the reference's sequential f32 recurrence, so one lane owns one row for the whole pass.
-// A workgroup (4 waves) owns 64 rows and walks them in chunks of kCW columns, pipelined:
-//   wave 0     runs the recurrence of chunk k from LDS (2 LDS reads, 2 adds, 1 LDS write a step)
-//   waves 1-3  divide / clamp / store chunk k-1 (coalesced: consecutive rows of one column) and
-//              stage chunk k+1's input window in LDS (coalesced along the row)
-constexpr int kCW = 32;      // columns per chunk
-constexpr int kVS = kCW + 1; // LDS row stride of the running-sum buffer
+// A workgroup (8 waves) owns 64 rows and walks them in chunks of kCW columns, three deep:
+//   wave 0     runs the recurrence of chunk k from LDS tile T[k & 1] into V[k & 1]
+//   waves 1-7  commit chunk k+1's window (already in registers) to T[(k+1) & 1], issue the global
+//              loads of chunk k+2 into registers (a whole step to land), then divide / clamp /
+//              store chunk k-1 from V[(k-1) & 1] (coalesced: 64 consecutive rows of one column)
+// so neither the HBM latency nor the division sits on the recurrence's path; one barrier a step
+// (which waits for LDS traffic only).  NSEG = 64-column segments of a tile row (kCW + 2r + 1).
+constexpr int kCW = 64;       // columns per chunk
+constexpr int kVS = kCW + 1;  // LDS row stride of the running-sum buffer (odd: conflict-free)
+constexpr int kBBThreads = 512;
+constexpr int kHW = kBBThreads / 64 - 1;           // helper waves
+constexpr int kHRows = (64 + kHW - 1) / kHW;       // tile rows per helper wave
 
 __host__ __device__ inline int bb_stride(int r) {
     const int s = kCW + 2 * r + 1;
     return (s & 1) ? s : s + 1;  // odd row stride: lanes (rows) on distinct banks
 }
+__host__ inline size_t bb_lds_bytes(int r) { return sizeof(float) * (2 * 64 * (size_t)bb_stride(r) + 2 * 64 * kVS); }
 
-__global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__ in, float* __restrict__ out,
-                                                       int width, int rows, int r, long plane) {
+template <int NSEG>
+__global__ __launch_bounds__(kBBThreads) void ft_boxblur_half(const float* __restrict__ in, float* __restrict__ out,
+                                                              int width, int rows, int r, long plane) {
     extern __shared__ float sm[];   // T[2][64][S] | V[2][64][kVS]  (offsets, not pointers: keeps ds_* ops)
     const int S = bb_stride(r);
     const int tbuf = 64 * S, vbase = 128 * S, vbuf = 64 * kVS;
@@ -82,33 +91,36 @@ __global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__
     const int nch = (width + kCW - 1) / kCW;
     const int last = width - 1;
     const float den = 2.0f * (float)r + 1.0f;
-    // tile column j of chunk c0 holds source column clamp(c0 - r + j).  Waves [wf, wf + NW) stage
-    // the tile, one row per wave at a time (lanes j and j + 64 of the row: coalesced); every load
-    // of a lane is issued before its LDS writes.
-    auto load_tile = [&](auto nw_tag, int toff, int c0, int wf) {
-        constexpr int NW = decltype(nw_tag)::value;
-        constexpr int M = (64 + NW - 1) / NW;
-        const int wv = wave - wf;
-        const int x0 = min(max(c0 - r + lane, 0), last), x1 = min(max(c0 - r + lane + 64, 0), last);
-        const bool in0 = lane < ncol, in1 = lane + 64 < ncol;
-        float v0[M], v1[M];
+    const int o = 2 * r + 1;
+    // helper state: tile rows hw + kHW * m, columns lane + 64 * q (clamped addresses: every load is
+    // in bounds; only the LDS commit is masked)
+    const int hw = wave - 1;
+    float pre[kHRows][NSEG];
+    const float* rowp[kHRows];
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const int rr = wv + m * NW;
-            const float* p = src + (size_t)min(row0 + min(rr, 63), rows - 1) * width;
-            v0[m] = (rr < 64 && in0) ? p[x0] : 0.0f;
-            v1[m] = (rr < 64 && in1) ? p[x1] : 0.0f;
-        }
+    for (int m = 0; m < kHRows; ++m) rowp[m] = src + (size_t)min(row0 + min(hw + kHW * m, 63), rows - 1) * width;
+    auto issue = [&](int c0) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const int rr = wv + m * NW;
-            if (rr < 64 && in0) {
-                sm[toff + rr * S + lane] = v0[m];
-                if (in1) sm[toff + rr * S + lane + 64] = v1[m];
-            }
+        for (int q = 0; q < NSEG; ++q) {
+            const int x = min(max(c0 - r + lane + 64 * q, 0), last);
+#pragma unroll
+            for (int m = 0; m < kHRows; ++m) pre[m][q] = rowp[m][x];
         }
     };
-    load_tile(std::integral_constant<int, 4>{}, 0, 0, 0);
+    auto commit = [&](int toff) {
+#pragma unroll
+        for (int m = 0; m < kHRows; ++m) {
+            const int rr = hw + kHW * m;
+#pragma unroll
+            for (int q = 0; q < NSEG; ++q)
+                if (rr < 64 && lane + 64 * q < ncol) sm[toff + rr * S + lane + 64 * q] = pre[m][q];
+        }
+    };
+    if (wave > 0) {
+        issue(0);
+        commit(0);
+        if (nch > 1) issue(kCW);
+    }
     __syncthreads();
     float val = -0.0f;  // Rust's float Sum starts from -0.0
     if (wave == 0)
@@ -119,22 +131,24 @@ __global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__
                 const int cw = min(kCW, width - k * kCW);
                 const int tr = (k & 1) * tbuf + lane * S;
                 const int vr = vbase + (k & 1) * vbuf + lane * kVS;
-                const int o = 2 * r + 1;
                 if (cw == kCW) {
-                    // all window samples first (independent of the running sum), then the chain
-                    float A[kCW], B[kCW], Vv[kCW];
+                    // window samples of 16 columns first (independent of the running sum), then the chain
 #pragma unroll
-                    for (int j = 0; j < kCW; ++j) {
-                        A[j] = sm[tr + j];
-                        B[j] = sm[tr + o + j];
+                    for (int j0 = 0; j0 < kCW; j0 += 16) {
+                        float A[16], B[16], Vv[16];
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) {
+                            A[j] = sm[tr + j0 + j];
+                            B[j] = sm[tr + o + j0 + j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) {
+                            Vv[j] = val;
+                            val = (val - A[j]) + B[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) sm[vr + j0 + j] = Vv[j];
                     }
-#pragma unroll
-                    for (int j = 0; j < kCW; ++j) {
-                        Vv[j] = val;
-                        val = (val - A[j]) + B[j];
-                    }
-#pragma unroll
-                    for (int j = 0; j < kCW; ++j) sm[vr + j] = Vv[j];
                 } else {
                     for (int j = 0; j < cw; ++j) {
                         sm[vr + j] = val;
@@ -143,12 +157,14 @@ __global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__
                 }
             }
         } else {
-            const int t = tid - 64;
+            if (k + 1 < nch) commit(((k + 1) & 1) * tbuf);
+            if (k + 2 < nch) issue((k + 2) * kCW);
             if (k >= 1) {
+                const int t = tid - 64;
                 const int c0 = (k - 1) * kCW;
                 const int cw = min(kCW, width - c0);
                 const int vp = vbase + ((k - 1) & 1) * vbuf;
-                for (int i = t; i < 64 * cw; i += 192) {
+                for (int i = t; i < 64 * cw; i += kBBThreads - 64) {
                     const int col = i >> 6, rr = i & 63;
                     if (row0 + rr < rows) {
                         float v = sm[vp + rr * kVS + col] / den;
@@ -157,10 +173,56 @@ __global__ __launch_bounds__(256) void ft_boxblur_half(const float* __restrict__
                     }
                 }
             }
-            if (k + 1 < nch) load_tile(std::integral_constant<int, 3>{}, ((k + 1) & 1) * tbuf, (k + 1) * kCW, 1);
         }
         __syncthreads();
     }
+}
+
+// Any radius: one lane per row straight from global memory (the same recurrence).
+__global__ __launch_bounds__(256) void ft_boxblur_half_any(const float* __restrict__ in, float* __restrict__ out,
+                                                          int width, int rows, int r, long plane) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= rows) return;
+    const float* __restrict__ p = in + blockIdx.y * plane + (size_t)row * width;
+    float* __restrict__ dst = out + blockIdx.y * plane;
+    const int last = width - 1;
+    const float den = 2.0f * (float)r + 1.0f;
+    float val = -0.0f;
+    for (int x = -r; x < r + 1; ++x) val = val + p[min(max(x, 0), last)];
+    for (int col = 0; col < width; ++col) {
+        float v = val / den;
+        v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+        dst[(size_t)col * rows + row] = v;
+        val = (val - p[min(max(col - r, 0), last)]) + p[min(col + r + 1, last)];
+    }
+}
+
+// > 64 KB of dynamic LDS needs the function attribute, once per (kernel, device)
+void allow_lds(const void* fn, int bytes, int slot) {
+    static std::atomic<uint32_t> done[2];
+    int dev = 0;
+    RSVIO_HIP(hipGetDevice(&dev));
+    const uint32_t bit = 1u << (dev & 31);
+    if (done[slot].load(std::memory_order_acquire) & bit) return;
+    RSVIO_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done[slot].fetch_or(bit, std::memory_order_acq_rel);
+}
+
+void launch_boxblur_half(const float* in, float* out, int width, int rows, int r, long plane, hipStream_t s) {
+    const int nseg = (kCW + 2 * r + 1 + 63) / 64;
+    const size_t lds = bb_lds_bytes(r);
+    const dim3 grid((rows + 63) / 64, 3);
+    if (nseg <= 2) {
+        allow_lds(reinterpret_cast<const void*>(&ft_boxblur_half<2>), (int)bb_lds_bytes(31), 0);
+        hipLaunchKernelGGL(ft_boxblur_half<2>, grid, dim3(kBBThreads), lds, s, in, out, width, rows, r, plane);
+    } else if (nseg == 3) {
+        allow_lds(reinterpret_cast<const void*>(&ft_boxblur_half<3>), (int)bb_lds_bytes(63), 1);
+        hipLaunchKernelGGL(ft_boxblur_half<3>, grid, dim3(kBBThreads), lds, s, in, out, width, rows, r, plane);
+    } else {
+        hipLaunchKernelGGL(ft_boxblur_half_any, dim3((rows + 255) / 256, 3), dim3(256), 0, s, in, out, width, rows, r,
+                           plane);
+    }
+    RSVIO_HIP(hipGetLastError());
 }
 
 // feature_detection.rs:134-155
@@ -451,15 +513,8 @@ void enqueue_score(const DetectBufs& D, const float* fine, hipStream_t s) {
     RSVIO_HIP(hipGetLastError());
     for (int k = 0; k < 3; ++k) {
         const int r = (D.boxes[k] - 1) / 2;
-        if (r > 15) throw std::invalid_argument("detection_blur too large (fast_blur box radius > 15)");  // kCW + 2r + 1 <= 128
-        const size_t lds = sizeof(float) * (128 * (size_t)bb_stride(r) + 128 * kVS);
-        if (lds > 64 * 1024) throw std::invalid_argument("detection_blur too large for the box-blur tile");
-        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.h + 63) / 64, 3), dim3(256), lds, s, D.planes, D.tmp, D.w, D.h,
-                           r, (long)n);
-        RSVIO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(ft_boxblur_half, dim3((D.w + 63) / 64, 3), dim3(256), lds, s, D.tmp, D.planes, D.h, D.w,
-                           r, (long)n);
-        RSVIO_HIP(hipGetLastError());
+        launch_boxblur_half(D.planes, D.tmp, D.w, D.h, r, (long)n, s);
+        launch_boxblur_half(D.tmp, D.planes, D.h, D.w, r, (long)n, s);
     }
     hipLaunchKernelGGL(ft_score_kernel, dim3((n + 255) / 256), dim3(256), 0, s, D.planes, n, D.score);
     RSVIO_HIP(hipGetLastError());

@@ -292,6 +292,29 @@ def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int =
                      true_pose7=true_pose7, true_p_W=p_W)
 
 
+def eucm_project(params, xy: np.ndarray) -> np.ndarray:
+    """EUCM projection (Khomutenko et al.; camera-intrinsic-model's EUCM, src/datasets/mod.rs:102-113)
+    of the rays (x, y, 1): u = fx x / (alpha d + (1 - alpha) z) + cx, d = sqrt(beta (x^2 + y^2) + z^2).
+    Config 5's pixel observations -- input generation, f64 in, f32 pixels out."""
+    fx, fy, cx, cy, alpha, beta = params[:6]
+    x, y = xy[:, 0], xy[:, 1]
+    d = np.sqrt(beta * (x * x + y * y) + 1.0)
+    den = alpha * d + (1.0 - alpha)
+    return np.stack([fx * x / den + cx, fy * y / den + cy], 1).astype(np.float32)
+
+
+def config5_problem(cams, seed: int = 55, init_seed: int = 56):
+    """BASELINE config 5: window 20 (19 free keyframes), 5,000 landmarks x 8 consecutive keyframes x
+    2 cameras = 80,000 observations, observed as EUCM pixels (TUM-VI cam0/cam1).  Returns the
+    problem (obs_uv still the true normalised coordinates) and the f32 pixel observations."""
+    prob = ba_problem(n_kf=20, n_lm=5000, kf_per_lm=8, seed=seed, init_seed=init_seed)
+    px = np.empty((prob.n_obs, 2), np.float32)
+    for c in range(2):
+        sel = prob.obs_cam == c
+        px[sel] = eucm_project(cams[c].params, prob.obs_uv[sel])
+    return prob, px
+
+
 @dataclass
 class MotionFrame:
     """One frame for track_motion: the map (ids ascending, p_W f32), the frame's features per

@@ -70,6 +70,16 @@ def test_score_bitexact(ftg, oracle, mono_frames):
         assert np.array_equal(ftg.shi_tomasi_score(small, blur), oracle.ft_shi_tomasi_score(small, blur))
 
 
+@pytest.mark.parametrize("blur", [0.5, 25.0, 40.0, 80.0])
+def test_score_box_radii(ftg, oracle, blur):
+    """fast_blur box radii across the kernel variants: 2-segment tiles (r <= 31), 3-segment tiles
+    (r <= 63) and the any-radius fallback (r = 79 at sigma 80), on a ragged 130 x 200 image."""
+    rng = np.random.default_rng(int(blur * 10))
+    img = rng.uniform(0, 1, (130, 200)).astype(np.float32)
+    a, b = ftg.shi_tomasi_score(img, blur), oracle.ft_shi_tomasi_score(img, blur)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 def test_add_points_identical(ftg, oracle, mono_frames):
     fine = oracle.ft_build_pyramid(mono_frames[0], 5)[:W * H].reshape(H, W)
     ref = oracle.ft_add_points(fine)
