@@ -1014,6 +1014,297 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     }  // blocked path
 }
 
+// ---------------------------------------------------------------------------------------
+// K5 for 11..20 free keyframes (61 <= n <= 120): the pipelined register LDL^T with two rows per
+// lane (rows lane and lane + 64) over 8 waves.  The system is padded to NP = 6 NF (NF in
+// {13, 16, 20}) with identity rows / columns after the real ones and b as row NP: a padded
+// column has pivot 1 and zero couplings, so every real entry sees exactly the operations of
+// the unpadded factorisation.  Wave WV owns columns [WV CW, WV CW + CW); a wave whose columns
+// all lie at or past 64 skips the upper half of the rows (lower triangle only).  LDS keeps the
+// unscaled columns U[.][K] = (D L)[.][K] and 1/d_K; L = U / d is re-formed with the owner's
+// multiply (same bits), so one NP x 121 array serves the updates and the back substitution.
+// ---------------------------------------------------------------------------------------
+constexpr int kX2Waves = 8;
+constexpr int kUcLd = kMaxN + 1;  // 121 (odd)
+
+__device__ __forceinline__ const double* sys_lower_rt(const double* sys, int nf, int r, int c) {
+    const int n = 6 * nf;
+    if (r == n) return sys + (nf * (nf + 1) / 2) * 36 + c;
+    const int a = c / 6, b = r / 6;
+    const int pb = a * nf - a * (a - 1) / 2 + (b - a);
+    const int k = (a == b) ? (r % 6) * 6 + (c % 6) : (c % 6) * 6 + (r % 6);
+    return sys + pb * 36 + k;
+}
+
+template <int NP, int CW, int WV, int K>
+__device__ __forceinline__ void chol2_step(double (&a)[2][CW], int lane, double* Uc, double* dinv, double* sink,
+                                           int* progress, int& seen, bool& bad, double inv) {
+    constexpr int c0 = WV * CW;
+    constexpr int c1 = (c0 + CW < NP) ? c0 + CW : NP;
+    constexpr int Q0 = (c0 < 64) ? 0 : 1;             // first active half of the rows
+    constexpr int KN = (K + 1 < c0) ? K + 2 : K + 1;  // consume columns in pairs
+    if constexpr (K < c0) {
+        if (seen < KN) {
+            do {
+                seen = __hip_atomic_load(progress, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (seen >= KN) break;
+                __builtin_amdgcn_s_sleep(1);
+            } while (true);
+        }
+        const double* u = Uc + K * kUcLd;
+        const double di = dinv[K];
+        double lr[2];
+#pragma unroll
+        for (int q = Q0; q < 2; ++q) lr[q] = u[min(lane + 64 * q, NP)] * di;
+        if constexpr (KN == K + 2) {
+            const double* u2 = Uc + (K + 1) * kUcLd;
+            const double di2 = dinv[K + 1];
+            double lr2[2];
+#pragma unroll
+            for (int q = Q0; q < 2; ++q) lr2[q] = u2[min(lane + 64 * q, NP)] * di2;
+            double v1[CW], v2[CW];
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) {
+                v1[jj] = u[c0 + jj];
+                v2[jj] = u2[c0 + jj];
+            }
+#pragma unroll
+            for (int q = Q0; q < 2; ++q)
+#pragma unroll
+                for (int jj = 0; jj < CW; ++jj)
+                    if (c0 + jj < NP) a[q][jj] = fma(-lr2[q], v2[jj], fma(-lr[q], v1[jj], a[q][jj]));
+        } else {
+#pragma unroll
+            for (int q = Q0; q < 2; ++q)
+#pragma unroll
+                for (int jj = 0; jj < CW; ++jj)
+                    if (c0 + jj < NP) a[q][jj] = fma(-lr[q], u[c0 + jj], a[q][jj]);
+        }
+        if constexpr (KN == c0) {  // first own pivot
+            const double piv = rl64(a[c0 >> 6][0], c0 & 63);
+            bad |= !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+    } else if constexpr (K < c1) {
+        constexpr int j = K - c0;
+        if constexpr (K > c0) __hip_atomic_store(progress, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        double uk[2], l[2];
+#pragma unroll
+        for (int q = Q0; q < 2; ++q) {
+            uk[q] = a[q][j];
+            l[q] = uk[q] * inv;
+            a[q][j] = l[q];
+            // every lane stores (rows past NP into the sink): the release below is then ordered
+            // after each lane's own writes (a lane-divergent store could be scheduled after
+            // another lane's release)
+            double* dst = (q == 0 || lane + 64 <= NP) ? Uc + K * kUcLd + lane + 64 * q : sink + lane;
+            *dst = uk[q];
+        }
+        dinv[K] = inv;  // uniform value, written by every lane for the same reason
+        double piv = 1.0;
+        const double* u = Uc + K * kUcLd;
+        if constexpr (j + 1 < CW && K + 1 < NP) {
+            constexpr int qn = (K + 1) >> 6, ln = (K + 1) & 63;
+            const double ukn = rl64(uk[qn], ln);
+#pragma unroll
+            for (int q = Q0; q < 2; ++q) a[q][j + 1] = fma(-l[q], ukn, a[q][j + 1]);
+            piv = rl64(a[qn][j + 1], ln);
+        }
+#pragma unroll
+        for (int jj = j + 2; jj < CW; ++jj) {
+            if (c0 + jj < NP) {
+                const double v = u[c0 + jj];
+#pragma unroll
+                for (int q = Q0; q < 2; ++q) a[q][jj] = fma(-l[q], v, a[q][jj]);
+            }
+        }
+        if constexpr (j + 1 < CW && K + 1 < NP) {
+            bad |= !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+        if constexpr (K + 1 == c1) __hip_atomic_store(progress, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if constexpr (K < c0) {
+#pragma unroll
+        for (int q = Q0; q < 2; ++q)
+#pragma unroll
+            for (int jj = 0; jj < CW; ++jj) __asm__ volatile("" : "+v"(a[q][jj]));
+    }
+    constexpr int KNEXT = (K < c0) ? KN : K + 1;
+    if constexpr (KNEXT < c1) chol2_step<NP, CW, WV, KNEXT>(a, lane, Uc, dinv, sink, progress, seen, bad, inv);
+}
+
+template <int NP, int CW, int WV>
+__device__ __forceinline__ void chol2_pipe(const double* sys, int nf, double* Uc, double* dinv, double* sink, int* progress,
+                                           int* badw, int lane) {
+    constexpr int c0 = WV * CW;
+    constexpr int Q0 = (c0 < 64) ? 0 : 1;
+    const int n = 6 * nf;
+    double a[2][CW];
+    // this wave's columns of its rows straight from sys: real rows / columns from the packed
+    // system, padded ones identity, row NP = b (zero in padded columns), upper triangle zero
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int r = lane + 64 * q;
+#pragma unroll
+        for (int jj = 0; jj < CW; ++jj) {
+            const int c = c0 + jj;
+            double v = 0.0;
+            if (q >= Q0 && c < NP && r <= NP && (c <= r || r == NP)) {
+                if (r == NP) v = c < n ? *sys_lower_rt(sys, nf, n, c) : 0.0;
+                else if (r < n) v = *sys_lower_rt(sys, nf, r, c);
+                else v = (r == c) ? 1.0 : 0.0;
+            }
+            a[q][jj] = v;
+        }
+    }
+    bool bad = false;
+    if constexpr (c0 < NP) {
+        double inv = 0.0;
+        if constexpr (c0 == 0) {
+            const double piv = rl64(a[0][0], 0);
+            bad = !(piv > 0.0) || !isfinite(piv);
+            inv = rcp_f64(piv);
+        }
+        int seen = 0;
+        chol2_step<NP, CW, WV, 0>(a, lane, Uc, dinv, sink + 64 * WV, progress, seen, bad, inv);
+    }
+    if (lane == 0) badw[WV] = bad ? 1 : 0;
+}
+
+template <int NF>
+__global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, Prob Pr, Work Wk) {
+    constexpr int NP = 6 * NF, CW = (NP + kX2Waves - 1) / kX2Waves;
+    static_assert(NP <= kMaxN && NP + 1 <= kUcLd && NP < 128, "padded system too large");
+    __shared__ double Uc[NP * kUcLd];
+    __shared__ double dinv[NP];
+    __shared__ double dcs[128];
+    __shared__ double sink[64 * kX2Waves];  // stores of rows past NP (see chol2_step)
+    __shared__ int badw[kX2Waves];
+    __shared__ int progress;
+    __shared__ int fail;
+    LmState* st = Wk.st;
+    if (st->done) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nF = G.n_free, n = 6 * nF;
+    const double* sys = Wk.sys;
+    const int SG0 = G.n_pb * 36 + 6 * nF, SC0 = SG0 + 6 * nF;
+    const int cur = st->cur;
+    double p7[7] = {0, 0, 0, 1, 0, 0, 0};
+    int fidx = -1;
+    double gcl[2] = {0.0, 0.0};
+    if (wave == 0) {
+        if (lane < G.n_kf) {
+            fidx = Pr.free_idx[lane];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (lane + 64 * q < n) gcl[q] = sys[SG0 + lane + 64 * q];
+    }
+    if (tid == 0) {
+        fail = (sys[SC0 + 1] != 0.0 || *Wk.singular) ? 1 : 0;
+        *Wk.singular = 0;
+        progress = 0;
+    }
+    __syncthreads();
+    if (fail) {
+        if (tid == 0) {
+            st->solve_ok = 0;
+            st->dc2 = 0.0;
+            st->gcdc = 0.0;
+        }
+        return;
+    }
+    switch (wave) {
+        case 0: chol2_pipe<NP, CW, 0>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 1: chol2_pipe<NP, CW, 1>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 2: chol2_pipe<NP, CW, 2>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 3: chol2_pipe<NP, CW, 3>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 4: chol2_pipe<NP, CW, 4>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 5: chol2_pipe<NP, CW, 5>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        case 6: chol2_pipe<NP, CW, 6>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+        default: chol2_pipe<NP, CW, 7>(sys, nF, Uc, dinv, sink, &progress, badw, lane); break;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    bool anybad = false;
+#pragma unroll
+    for (int w = 0; w < kX2Waves; ++w) anybad |= badw[w] != 0;
+    if (anybad) {
+        if (lane == 0) {
+            st->solve_ok = 0;
+            st->dc2 = 0.0;
+            st->gcdc = 0.0;
+        }
+        return;
+    }
+    // L^T x = z (unit diagonal), z = row NP of the factor: lane holds rows i = lane, lane + 64;
+    // L[j][i] = U[j][i] / d_i by the owner's multiply.  Padded rows have z = 0: start at n - 1.
+    double yv[2], di[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = min(lane + 64 * q, NP - 1);
+        di[q] = dinv[i];
+        yv[q] = Uc[i * kUcLd + NP] * di[q];
+    }
+    constexpr int kBs = 8;
+    for (int j0 = n - 1; j0 >= 0; j0 -= kBs) {
+        double lt[kBs][2];
+#pragma unroll
+        for (int t = 0; t < kBs; ++t) {
+            const int j = max(j0 - t, 0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) lt[t][q] = Uc[min(lane + 64 * q, NP - 1) * kUcLd + j];
+        }
+#pragma unroll
+        for (int t = 0; t < kBs; ++t) {
+            const int j = j0 - t;
+            if (j < 0) break;
+            const double xj = j >= 64 ? rl64(yv[1], j - 64) : rl64(yv[0], j);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const double l = lt[t][q] * di[q];
+                const double upd = fma(-l, xj, yv[q]);
+                yv[q] = lane + 64 * q < j ? upd : yv[q];
+            }
+        }
+    }
+    double x[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) x[q] = lane + 64 * q < n ? yv[q] : 0.0;
+    const double d2 = wave_sum_det(x[0] * x[0] + x[1] * x[1]);
+    const double gd = wave_sum_det(gcl[0] * x[0] + gcl[1] * x[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = lane + 64 * q;
+        if (i < n) {
+            Wk.dc[i] = x[q];
+            dcs[i] = x[q];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < G.n_kf) {
+        double* qd = Wk.pose[1 - st->cur] + 7 * lane;
+        if (fidx < 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) qd[i] = p7[i];
+        } else {
+            double qv[7];
+            se3_plus(p7, dcs + 6 * fidx, qv);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) qd[i] = qv[i];
+        }
+    }
+    if (lane == 0) {
+        st->solve_ok = 1;
+        st->dc2 = d2;
+        st->gcdc = gd;
+    }
+}
+
 // Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
 // owner rank), per-lane strided sums then a fixed-pairing wave reduction; every load is issued
 // before the state is read (the free-pose squares of both buffers; the current one is picked
@@ -1657,8 +1948,15 @@ struct BundleAdjuster {
             RSVIO_CAM(1) RSVIO_CAM(2) RSVIO_CAM(3) RSVIO_CAM(4) RSVIO_CAM(5)
             RSVIO_CAM(6) RSVIO_CAM(7) RSVIO_CAM(8) RSVIO_CAM(9) RSVIO_CAM(10)
 #undef RSVIO_CAM
-            default: hipLaunchKernelGGL(ba_camera_solve<0>, g, b, 0, stream, G, pr, wk); break;
+            default: {
+                const dim3 b2(64 * kX2Waves);
+                if (G.n_free <= 13) hipLaunchKernelGGL(ba_camera_solve_x2<13>, g, b2, 0, stream, G, pr, wk);
+                else if (G.n_free <= 16) hipLaunchKernelGGL(ba_camera_solve_x2<16>, g, b2, 0, stream, G, pr, wk);
+                else hipLaunchKernelGGL(ba_camera_solve_x2<20>, g, b2, 0, stream, G, pr, wk);
+                break;
+            }
         }
+        RSVIO_HIP(hipGetLastError());
     }
 
     void enqueue_iteration(const rsvio_lm_cfg& cfg) {
@@ -1856,6 +2154,17 @@ struct BundleAdjuster {
         for (int i = 0; i < n; ++i) b[i] = sys[36 * G.n_pb + i];
         *cost = sys[36 * G.n_pb + 12 * G.n_free];
     }
+
+    // diagnostic: one reduced system at lambda and its camera solve (K4c + K5) -> dc
+    void camera_step(double lambda, double huber_delta, double* dc) {
+        if (!has_problem) throw std::invalid_argument("no problem uploaded");
+        G.huber_delta = huber_delta;
+        enqueue_start(lambda);
+        enqueue_linear_system();
+        launch_camera_solve(prob(), work());
+        RSVIO_HIP(hipMemcpyAsync(dc, d_dc.p, sizeof(double) * 6 * G.n_free, hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipStreamSynchronize(stream));
+    }
 };
 
 }  // namespace rsvio
@@ -1956,6 +2265,14 @@ int rsvio_ba_solve(rsvio_ba* ba, int32_t n_kf, double* pose7, const uint8_t* kf_
         B.set_problem(n_kf, pose7, kf_fixed, n_lm, p_W, n_obs, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2);
         B.run(*cfg, res);
         if (res->status > 0) B.get_state(pose7, p_W);  // success: hand back the optimised state (:364-374)
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_dbg_ba_camera_step(rsvio_ba* ba, double lambda, double huber_delta, double* dc) {
+    if (!ba || !dc) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        ba->b.camera_step(lambda, huber_delta, dc);
         return (int)RSVIO_OK;
     });
 }

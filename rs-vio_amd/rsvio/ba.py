@@ -123,6 +123,18 @@ class BundleAdjuster:
         check(_lib.load().rsvio_ba_build_system(self._h, lam, huber_delta, ptr(S), ptr(b), C.byref(cost)))
         return S, b, cost.value
 
+    def camera_step(self, lam, huber_delta=2.0):
+        """Diagnostic (rsvio_dbg_ba_camera_step): the reduced system at lam and its dense camera
+        solve (K4c + K5) on the current state -> dc (6 n_free)."""
+        lib = _lib.load()
+        fn = lib.rsvio_dbg_ba_camera_step
+        fn.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_void_p]
+        fn.restype = C.c_int
+        nfree = int((self._keep[1] == 0).sum())
+        dc = np.zeros(6 * nfree)
+        check(fn(self._h, lam, huber_delta, ptr(dc)))
+        return dc
+
     def solve(self, pose7, kf_fixed, p_W, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2, cfg=None):
         """rsvio_ba_solve: returns (pose7, p_W, result); inputs are not modified."""
         pose = _c(pose7, np.float64).copy()

@@ -163,9 +163,30 @@ def test_sliding_window_mirror(gpu, oracle):
     assert sw.optimize()
 
 
-@pytest.mark.parametrize("n_kf", [2, 3, 4, 6, 8, 11, 12])
+@pytest.mark.parametrize("n_kf", [3, 11, 12, 14, 17, 20, 21])
+def test_camera_solve_matches_dense_solve(gpu, n_kf):
+    """K5 alone: dc of S dc = b for every solve variant (one row per lane up to 10 free keyframes,
+    two rows per lane padded to 13 / 16 / 20 above), repeated (a publication race would show as a
+    run-to-run difference), against numpy's dense solve of the same S, b (tolerance 1e-9 relative)."""
+    from rsvio import synthetic as S
+    prob = S.ba_problem(n_kf=n_kf, n_lm=40 * n_kf, kf_per_lm=min(n_kf, 4), seed=100 + n_kf, init_seed=200 + n_kf)
+    ba = _adjuster(gpu, prob)
+    S_, b, _ = ba.build_system(1e-4)
+    ref = np.linalg.solve(S_, b)
+    first = None
+    for _ in range(4):
+        dc = ba.camera_step(1e-4)
+        assert np.abs(dc - ref).max() <= 1e-9 * np.abs(ref).max()
+        if first is None:
+            first = dc
+        assert np.array_equal(dc, first)
+    ba.close()
+
+
+@pytest.mark.parametrize("n_kf", [2, 3, 4, 6, 8, 11, 12, 14, 17, 21])
 def test_window_sizes_match_oracle(gpu, oracle, n_kf):
-    """Every camera-solve variant (register path for 1..10 free keyframes, blocked path above)."""
+    """Every camera-solve variant: one row per lane for 1..10 free keyframes, two rows per lane
+    (padded to 13, 16 or 20 free keyframes) above."""
     from rsvio import synthetic as S
     prob = S.ba_problem(n_kf=n_kf, n_lm=40 * n_kf, kf_per_lm=min(n_kf, 4), seed=100 + n_kf, init_seed=200 + n_kf)
     ba = _adjuster(gpu, prob)
