@@ -47,7 +47,6 @@ RSVIO_DBG_DECL
 
 constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
 constexpr int kMaxN = 6 * kMaxFree;
-constexpr int kLdA = kMaxN + 1;         // odd stride
 // raw linearisation per slot, one contiguous 384-B record (AoS): W (6x3), U (6x6 packed upper),
 // g_c (6), pad; and per landmark (96 B): V (3x3 packed upper), g_p (3), pad
 enum { RW = 0, RU = 18, RG = 39, kRawF = 48 };
@@ -573,15 +572,11 @@ __global__ __launch_bounds__(64) void ba_schur_combine(Geometry G, Prob Pr, Work
 
 // ---------------------------------------------------------------------------------------
 // K5: camera system solve (one workgroup of 256):
-//   S (lower triangle) and b (as row n) from sys -> LDS, then
-//   n <= 60 (<= 10 free keyframes): pipelined 4-wave register LDL^T of [S; b^T] (chol_pipe),
-//     unit-L back substitution by wave 0;
-//   n > 60: blocked right-looking Cholesky in LDS (panels of 8: panel factor by wave 0 with
-//     v_readlane broadcasts, rank-8 trailing update by all 4 waves), back substitution by wave 0;
-//   |dc|^2, g_c.dc; SE3 (+) trial poses.
+//   n <= 60 (<= 10 free keyframes): pipelined 4-wave register LDL^T of [S; b^T] (chol_pipe)
+//     straight from sys, unit-L back substitution by wave 0; |dc|^2, g_c.dc; SE3 (+) trial poses.
+//   n > 60: ba_camera_solve_x2 below (two rows per lane, 8 waves).
 // ---------------------------------------------------------------------------------------
 
-constexpr int kNB = 8;  // Cholesky panel width (blocked path, n > 60)
 
 
 
@@ -718,8 +713,7 @@ __device__ void chol_pipe(const double* sys, double* Lc, double* Uc, int* progre
 }
 
 template <int NF>
-__device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, const double* gcl,
-                                int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
+__device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
     constexpr int NP = 6 * NF, CW = (NP + 3) / 4;
     const int lane = tid & 63, wave = tid >> 6;
     LmState* st = Wk.st;
@@ -791,9 +785,9 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
 
 template <int NF>
 __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
-    __shared__ __attribute__((aligned(16))) double A[(kMaxN + 1) * kLdA];
-    __shared__ double dL[kMaxN];
-    __shared__ double gcl[kMaxN];
+    static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
+    // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
+    __shared__ __attribute__((aligned(16))) double A[128 + 2 * 6 * NF * kLcLd];
     __shared__ int badw[4];
     __shared__ int progress;
     __shared__ int fail;
@@ -802,12 +796,12 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nF = G.n_free, n = 6 * nF;
     const double* sys = Wk.sys;
-    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * nF, SC0 = SG0 + 6 * nF;
+    const int SC0 = G.n_pb * 36 + 12 * nF;
     const int cur = st->cur;
-    // the trial-pose inputs of wave 0 are fetched now, behind the fill (register path)
+    // the trial-pose inputs of wave 0 are fetched now, behind the fill
     double p7[7] = {0, 0, 0, 1, 0, 0, 0};
     int fidx = -1;
-    if (NF > 0 && wave == 0 && lane < G.n_kf) {
+    if (wave == 0 && lane < G.n_kf) {
         fidx = Pr.free_idx[lane];
 #pragma unroll
         for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
@@ -820,49 +814,9 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         *Wk.singular = 0;
         progress = 0;
     }
-    // lower triangle only, one writer per element: diagonal blocks keep a >= c, off-diagonal
-    // blocks (fa < fb, upper) are transposed into the lower triangle; b as row n, g_c in gcl.
-    // Each element's value and its block's keyframe pair are loaded together (one round trip).
-    const int nel = NF > 0 ? 0 : SB0 + 12 * nF;  // the register path reads sys itself
-    auto place = [&](int e, double v, int fa, int fb) {
-        if (e >= SB0) {  // b, g_c
-            const int i = e - SB0;
-            if (i < n) A[n * kLdA + i] = v;
-            else gcl[i - n] = v;
-            return;
-        }
-        const int k = e % 36;
-        const int r = 6 * fa + k / 6, c = 6 * fb + k % 6;
-        if (fa == fb) {
-            if (r >= c) A[r * kLdA + c] = v;
-        } else {
-            A[c * kLdA + r] = v;
-        }
-    };
-    constexpr int kFillB = 9;  // 9 x 256 >= 55 * 36 + 120 (n_free <= 10)
-    for (int e0 = tid; e0 < nel; e0 += kFillB * 256) {
-        double v[kFillB];
-        int fa[kFillB], fb[kFillB];
-#pragma unroll
-        for (int u = 0; u < kFillB; ++u) {
-            const int e = e0 + u * 256;
-            v[u] = 0.0;
-            fa[u] = fb[u] = 0;
-            if (e < nel) {
-                v[u] = sys[e];
-                if (e < SB0) {
-                    fa[u] = Pr.pb_fa[e / 36];
-                    fb[u] = Pr.pb_fb[e / 36];
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kFillB; ++u)
-            if (e0 + u * 256 < nel) place(e0 + u * 256, v[u], fa[u], fb[u]);
-    }
     __syncthreads();
     STAMP(1);
-    if constexpr (NF > 0) {
+    {
         if (fail) {
             if (tid == 0) {
                 st->solve_ok = 0;
@@ -872,146 +826,9 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
             return;
         }
         STAMP(2);
-        camera_solve_w4<NF>(G, Pr, Wk, A, gcl, badw, &progress, n, tid, p7, fidx);
-        return;
-    } else {
-    for (int jb = 0; jb < n && !fail; jb += kNB) {
-        const int nb = min(kNB, n - jb);
-        if (wave == 0) {
-            // rows jb + lane (q = 0) and jb + 64 + lane (q = 1), up to row n (the b row)
-            double a[2][kNB];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int r = jb + lane + 64 * q;
-#pragma unroll
-                for (int t = 0; t < kNB; ++t) a[q][t] = (r <= n && t < nb) ? A[r * kLdA + jb + t] : 0.0;
-            }
-            bool bad = false;
-#pragma unroll
-            for (int t = 0; t < kNB; ++t) {
-                if (t < nb && !bad) {
-                    const double d = rl64(a[0][t], t);  // row jb + t lives in lane t
-                    if (!(d > 0.0) || !isfinite(d)) {
-                        bad = true;
-                    } else {
-                        const double ljj = sqrt(d);
-                        if (lane == 0) dL[jb + t] = ljj;
-#pragma unroll
-                        for (int q = 0; q < 2; ++q) {
-                            const int r = jb + lane + 64 * q;
-                            if (r > jb + t && r <= n) a[q][t] = a[q][t] / ljj;
-                        }
-#pragma unroll
-                        for (int t2 = t + 1; t2 < kNB; ++t2) {
-                            if (t2 < nb) {
-                                const double c = rl64(a[0][t], t2);  // L[jb + t2][jb + t]
-#pragma unroll
-                                for (int q = 0; q < 2; ++q) {
-                                    const int r = jb + lane + 64 * q;
-                                    if (r >= jb + t2 && r <= n) a[q][t2] -= a[q][t] * c;
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-            if (bad) {
-                if (lane == 0) fail = 1;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int r = jb + lane + 64 * q;
-#pragma unroll
-                    for (int t = 0; t < kNB; ++t)
-                        if (t < nb && r >= jb + t && r <= n) A[r * kLdA + jb + t] = a[q][t];
-                }
-            }
-        }
-        __syncthreads();
-        if (fail) break;
-        // rank-nb trailing update: A[r][k] -= sum_t L[r][jb+t] L[k][jb+t], jb+nb <= k <= min(r, n-1)
-        const int c0 = jb + nb;
-        const int m = n - c0;  // trailing columns; rows c0 .. n (m + 1 rows incl. the b row)
-        for (int e = tid; e < (m + 1) * m; e += 256) {
-            const int r = c0 + e / m, k = c0 + e % m;
-            if (k > r) continue;
-            const double* Lr = A + r * kLdA + jb;
-            const double* Lk = A + k * kLdA + jb;
-            double s = 0.0;
-#pragma unroll
-            for (int t = 0; t < kNB; ++t)
-                if (t < nb) s += Lr[t] * Lk[t];
-            A[r * kLdA + k] -= s;
-        }
-        __syncthreads();
-    }
-    if (fail) {
-        if (tid == 0) {
-            st->solve_ok = 0;
-            st->dc2 = 0.0;
-            st->gcdc = 0.0;
-        }
+        camera_solve_w4<NF>(G, Pr, Wk, A, badw, &progress, n, tid, p7, fidx);
         return;
     }
-    STAMP(2);
-    if (wave != 0) return;
-    // L^T dc = y by wave 0: lane holds y_i for i = lane, lane + 64
-    double yv[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int i = lane + 64 * q;
-        yv[q] = i < n ? A[n * kLdA + i] : 0.0;
-    }
-    for (int j = n - 1; j >= 0; --j) {
-        const int qj = j >> 6;
-        const double yj = qj == 0 ? rl64(yv[0], j & 63) : rl64(yv[1], j & 63);
-        const double xj = yj / dL[j];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int i = lane + 64 * q;
-            if (i < j) yv[q] -= A[j * kLdA + i] * xj;
-            else if (i == j) yv[q] = xj;
-        }
-    }
-    STAMP(3);
-    const int cur = st->cur;
-    double d2 = 0.0, gd = 0.0;
-    // rows 0-2 of A are no longer needed: dc, dc_i^2 and g_c,i dc_i staged for the sums below
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int i = lane + 64 * q;
-        if (i < n) {
-            const double x = yv[q];
-            Wk.dc[i] = x;
-            A[i] = x;
-            A[kLdA + i] = x * x;
-            A[2 * kLdA + i] = gcl[i] * x;
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    STAMP(4);
-    for (int k = lane; k < G.n_kf; k += 64) {
-        const int f = Pr.free_idx[k];
-        const double* p = Wk.pose[cur] + 7 * k;
-        double* q = Wk.pose[1 - cur] + 7 * k;
-        if (f < 0)
-            for (int i = 0; i < 7; ++i) q[i] = p[i];
-        else
-            se3_plus(p, A + 6 * f, q);
-    }
-    STAMP(5);
-    if (lane == 0) {
-        for (int i = 0; i < n; ++i) {
-            d2 += A[kLdA + i];
-            gd += A[2 * kLdA + i];
-        }
-        st->solve_ok = 1;
-        st->dc2 = d2;
-        st->gcdc = gd;
-    }
-    STAMP(6);
-    }  // blocked path
 }
 
 // ---------------------------------------------------------------------------------------
