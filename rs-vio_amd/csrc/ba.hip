@@ -646,15 +646,16 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
         Lc[K * kLcLd + lane] = l;
         Uc[K * kLcLd + lane] = uk;
         double piv = 1.0;
-        const double* u = Uc + K * kLcLd;
         if constexpr (j + 1 < CW && K + 1 < NP) {
             // column K+1 by readlane (no LDS round trip on the pivot chain)
             a[j + 1] = fma(-l, rl64(uk, K + 1), a[j + 1]);
             piv = rl64(a[j + 1], K + 1);
         }
+        // the rest of the own block: U[c0 + jj][K] straight from its lane (no LDS round trip
+        // on the next pivots' path)
 #pragma unroll
         for (int jj = j + 2; jj < CW; ++jj)
-            if (c0 + jj < NP) a[jj] = fma(-l, u[c0 + jj], a[jj]);
+            if (c0 + jj < NP) a[jj] = fma(-l, rl64(uk, c0 + jj), a[jj]);
         if constexpr (j + 1 < CW && K + 1 < NP) {
             bad |= !(piv > 0.0) || !isfinite(piv);
             inv = rcp_f64(piv);
@@ -919,7 +920,6 @@ __device__ __forceinline__ void chol2_step(double (&a)[2][CW], int lane, double*
         }
         dinv[K] = inv;  // uniform value, written by every lane for the same reason
         double piv = 1.0;
-        const double* u = Uc + K * kUcLd;
         if constexpr (j + 1 < CW && K + 1 < NP) {
             constexpr int qn = (K + 1) >> 6, ln = (K + 1) & 63;
             const double ukn = rl64(uk[qn], ln);
@@ -930,7 +930,7 @@ __device__ __forceinline__ void chol2_step(double (&a)[2][CW], int lane, double*
 #pragma unroll
         for (int jj = j + 2; jj < CW; ++jj) {
             if (c0 + jj < NP) {
-                const double v = u[c0 + jj];
+                const double v = rl64(uk[(c0 + jj) >> 6], (c0 + jj) & 63);  // U[c0 + jj][K] from its lane
 #pragma unroll
                 for (int q = Q0; q < 2; ++q) a[q][jj] = fma(-l[q], v, a[q][jj]);
             }
