@@ -1,0 +1,67 @@
+"""Test infrastructure (tests and bench.py's cpu_baseline leg only): the Estimator's backend
+seam filled with the CPU oracle, so the same host logic (rsvio.estimator.Estimator over rsvio.ba.SlidingWindow) runs once over the
+device library and once over the restatement.  Nothing in rsvio imports it.
+
+  track       -> oracle.StereoTracker (feature_tracker.rs:116-187) + oracle.unproject (frame.rs:107-134)
+  track_motion-> oracle.track_motion (sliding_window.rs:490-587 + estimator.rs:195-234)
+  solver      -> oracle.ba_solve (sliding_window.rs:159-381 + apex LM, restated)
+"""
+from types import SimpleNamespace
+
+import numpy as np
+
+from rsvio.camera import CONVENTIONS
+
+
+def _orc_cfg(oracle, cfg):
+    if cfg is None:
+        return None
+    return oracle.lm_cfg(cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance, cfg.huber_delta,
+                         cfg.lambda_init)
+
+
+class OracleSolver:
+    def __init__(self, oracle):
+        self.o = oracle
+
+    def solve(self, pose7, kf_fixed, p_W, obs_lm, obs_kf, obs_cam, obs_uv, T_C_B2, cfg=None):
+        prob = SimpleNamespace(pose7=pose7, kf_fixed=kf_fixed, p_W=p_W, obs_lm=obs_lm, obs_kf=obs_kf,
+                               obs_cam=obs_cam, obs_uv=obs_uv, T_C_B2=T_C_B2)
+        return self.o.ba_solve(prob, _orc_cfg(self.o, cfg))
+
+    def close(self):
+        pass
+
+
+class OracleBackend:
+    def __init__(self, oracle, width, height, cameras, levels=6, grid_size=50, max_iterations=20, thresh=0.01,
+                 translation_threshold=0.05, rotation_threshold=0.05):
+        self.o = oracle
+        self.tracker = oracle.StereoTracker(width, height, levels, grid_size, max_iterations, thresh)
+        self.cams = [oracle.camera(c.model, c.params, CONVENTIONS[c.convention], c.max_iterations) for c in cameras]
+        self.thr = (translation_threshold, rotation_threshold)
+        self.solver = OracleSolver(oracle)
+        self.map = (np.zeros(0, np.uint64), np.zeros((0, 3), np.float32))
+
+    def track(self, left, right):
+        out = []
+        for feats, cam in zip(self.tracker.process_frame(left, right), self.cams):
+            ids = np.array([f[0] for f in feats], np.int64)
+            px = np.array([[f[1], f[2]] for f in feats], np.float32).reshape(-1, 2)
+            uv, _ = self.o.unproject(cam, px)
+            out.append((ids, uv))
+        self.last = tuple(out)     # track_motion reads them (the device backend keeps them on device)
+        return self.last
+
+    def set_map(self, ids, p_W):
+        self.map = (np.asarray(ids, np.uint64), np.asarray(p_W, np.float32))
+
+    def track_motion(self, T_W_B_last_kf, T_C_B2):
+        (ids_l, uv_l), (ids_r, uv_r) = self.last
+        r = self.o.track_motion(ids_l, uv_l, ids_r, uv_r, self.map[0], self.map[1], T_W_B_last_kf, T_C_B2,
+                                thr_t=self.thr[0], thr_r=self.thr[1])
+        return r.status, bool(r.is_keyframe), np.array(r.T_W_B[:]).reshape(4, 4)
+
+    def close(self):
+        pass
+

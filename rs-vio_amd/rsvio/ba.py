@@ -160,9 +160,21 @@ class Frame:
     T_B_Cl: np.ndarray = field(default_factory=lambda: np.eye(4))
     T_B_Cr: np.ndarray = field(default_factory=lambda: np.eye(4))
     is_keyframe: bool = True
-    # (feature_id, undistorted (x, y)) per camera, in feature order
+    # per camera, in feature order: (ids, undistorted uv) arrays or [(feature_id, (x, y))]
     left_features: list = field(default_factory=list)
     right_features: list = field(default_factory=list)
+
+
+def _feature_arrays(feats):
+    """(ids int64, uv f64 n x 2) from a frame's features: (ids, uv) arrays or (id, (x, y)) pairs;
+    coordinates pass through f32 like Feature::undistorted_coord (frame.rs:118-119)."""
+    if isinstance(feats, tuple) and len(feats) == 2 and isinstance(feats[0], np.ndarray):
+        ids, uv = feats
+    else:
+        ids = [fid for fid, _ in feats]
+        uv = [xy for _, xy in feats]
+    return (np.asarray(ids, np.int64).reshape(-1),
+            np.asarray(uv, np.float64).reshape(-1, 2).astype(np.float32).astype(np.float64))
 
 
 def _quat_from_rot(R):
@@ -185,6 +197,7 @@ class SlidingWindow:
         self.max_frames = max_frames
         self.keyframes: deque[Frame] = deque()
         self.map_points: dict[int, np.ndarray] = {}  # feature id -> [f32; 3]
+        self.map_version = 0                           # bumped whenever map_points is replaced
         self.solver = solver or BundleAdjuster(max_keyframes=max(max_frames, 2), device=device)
         self.last_result = None
 
@@ -206,48 +219,59 @@ class SlidingWindow:
         return [f.T_W_B.copy() for f in self.keyframes]
 
     def build_problem(self):
-        """sliding_window.rs:174-300 in canonical order (frames, left then right, feature order)."""
+        """sliding_window.rs:174-300 in canonical order (frames, left then right, feature order):
+        landmarks = ids seen at least once left and once right in the window, indexed by first
+        appearance; initial point from map_points (f32) or the depth-2.0 ray of its first
+        observation (sliding_window.rs:248-272).  Vectorised over the window's observations."""
         kfs = list(self.keyframes)
         T_Cl_B = np.linalg.inv(kfs[0].T_B_Cl)
         T_Cr_B = np.linalg.inv(kfs[0].T_B_Cr)
-        cnt_l, cnt_r = {}, {}
-        for f in kfs:
-            for fid, _ in f.left_features:
-                cnt_l[fid] = cnt_l.get(fid, 0) + 1
-            for fid, _ in f.right_features:
-                cnt_r[fid] = cnt_r.get(fid, 0) + 1
+        ids, uv, kf, cam = [], [], [], []
+        for i, f in enumerate(kfs):
+            for c, feats in enumerate((f.left_features, f.right_features)):
+                fi, fu = _feature_arrays(feats)
+                ids.append(fi)
+                uv.append(fu)
+                kf.append(np.full(len(fi), i, np.int32))
+                cam.append(np.full(len(fi), c, np.uint8))
+        ids, uv = np.concatenate(ids), np.concatenate(uv)
+        kf, cam = np.concatenate(kf), np.concatenate(cam)
+        keep = np.isin(ids, ids[cam == 0]) & np.isin(ids, ids[cam == 1])
+        ids, uv, kf, cam = ids[keep], uv[keep], kf[keep], cam[keep]
+        uniq, first, inv = np.unique(ids, return_index=True, return_inverse=True)
+        order = np.argsort(first, kind="stable")          # landmarks by first appearance
+        rank = np.empty(len(uniq), np.int64)
+        rank[order] = np.arange(len(uniq))
+        obs_lm = rank[inv].astype(np.int32)
+        lm_ids = uniq[order]
+        p_init = np.zeros((len(lm_ids), 3))
+        in_map = np.zeros(len(lm_ids), bool)
+        if self.map_points:
+            mid = np.fromiter(self.map_points.keys(), np.int64, len(self.map_points))
+            mpw = np.stack([np.asarray(v, np.float32) for v in self.map_points.values()]).astype(np.float64)
+            srt = np.argsort(mid)
+            mid, mpw = mid[srt], mpw[srt]
+            pos = np.clip(np.searchsorted(mid, lm_ids), 0, len(mid) - 1)
+            in_map = mid[pos] == lm_ids
+            p_init[in_map] = mpw[pos[in_map]]
+        fo = first[order]                                  # first observation of each landmark
+        T_B_C = (np.linalg.inv(T_Cl_B), np.linalg.inv(T_Cr_B))
+        for j in np.nonzero(~in_map)[0]:
+            o = fo[j]
+            f = kfs[kf[o]]
+            Tbc = T_B_C[cam[o]]
+            p_C = np.array([uv[o, 0], uv[o, 1], 2.0])
+            p_init[j] = f.T_W_B[:3, :3] @ (Tbc[:3, :3] @ p_C + Tbc[:3, 3]) + f.T_W_B[:3, 3]
         pose7 = np.zeros((len(kfs), 7))
-        kf_fixed = np.zeros(len(kfs), np.uint8)
-        kf_fixed[0] = 1
-        lm_index: dict[int, int] = {}
-        p_init, obs_lm, obs_kf, obs_cam, obs_uv = [], [], [], [], []
         for i, f in enumerate(kfs):
             T_B_W = np.linalg.inv(f.T_W_B)
             pose7[i, :3] = T_B_W[:3, 3]
             pose7[i, 3:] = _quat_from_rot(T_B_W[:3, :3])
-            for cam, (feats, T_C_B) in enumerate(((f.left_features, T_Cl_B), (f.right_features, T_Cr_B))):
-                for fid, uv in feats:
-                    if cnt_l.get(fid, 0) == 0 or cnt_r.get(fid, 0) == 0:
-                        continue
-                    if fid not in lm_index:
-                        lm_index[fid] = len(p_init)
-                        if fid in self.map_points:
-                            p_init.append(np.asarray(self.map_points[fid], np.float32).astype(np.float64))
-                        else:
-                            # depth-2.0 ray (sliding_window.rs:256-269)
-                            p_C = np.array([float(np.float32(uv[0])), float(np.float32(uv[1])), 2.0])
-                            T_B_C = np.linalg.inv(T_C_B)
-                            p_W = f.T_W_B[:3, :3] @ (T_B_C[:3, :3] @ p_C + T_B_C[:3, 3]) + f.T_W_B[:3, 3]
-                            p_init.append(p_W)
-                    obs_lm.append(lm_index[fid])
-                    obs_kf.append(i)
-                    obs_cam.append(cam)
-                    obs_uv.append([float(np.float32(uv[0])), float(np.float32(uv[1]))])
-        p_init = np.array(p_init, np.float64).reshape(-1, 3)
+        kf_fixed = np.zeros(len(kfs), np.uint8)
+        kf_fixed[0] = 1
         T_C_B2 = np.stack([T_Cl_B.reshape(16), T_Cr_B.reshape(16)])
-        ids = sorted(lm_index, key=lm_index.get)
-        return (pose7, kf_fixed, p_init, np.array(obs_lm, np.int32), np.array(obs_kf, np.int32),
-                np.array(obs_cam, np.uint8), np.array(obs_uv, np.float64).reshape(-1, 2), T_C_B2, ids)
+        return (pose7, kf_fixed, p_init, obs_lm, kf.astype(np.int32), cam, uv, T_C_B2,
+                [int(x) for x in lm_ids])
 
     def optimize(self, cfg=None) -> bool:
         """Returns Ok(true)/Ok(false) as a bool; raises RuntimeError for a non-full window (:137-149)."""
@@ -264,7 +288,9 @@ class SlidingWindow:
         self.last_result = res
         if res.status <= 0:
             return False  # revert: nothing was modified
-        self.map_points = {fid: pw[j].astype(np.float32) for j, fid in enumerate(ids)}
+        pw32 = pw.astype(np.float32)
+        self.map_points = dict(zip(ids, pw32))
+        self.map_version += 1
         for i, f in enumerate(self.keyframes):
             f.T_W_B = np.linalg.inv(_T_from_pose7(pose[i]))
         return True

@@ -1,0 +1,128 @@
+"""Estimator::process_frame (src/estimator/estimator.rs:101-262) over the device pieces: the
+full per-frame pipeline of BASELINE config 4.
+
+Per frame (estimator.rs:190-248):
+  1. StereoPatchTracker::process_frame (feature_tracker.rs:116-187) -- pyramids, LK, FAST grid
+     detection, ids -- with Frame::add_{left,right}_feature's unprojection fused on the device;
+  2. if the sliding window is full: SlidingWindow::track_motion (sliding_window.rs:490-587,
+     PnP against map_points) and the keyframe rule (estimator.rs:195-234); a failed PnP leaves
+     the frame a keyframe with T_W_B = I (frame.rs:95);
+  3. a keyframe enters the window (add_frame) and, once the window is full, the window is
+     optimised (optimize, sliding_window.rs:159-381); map_points feed the next PnP.
+
+The host logic is the reference's, in canonical order (ids in detection scan
+order, features by id).  The heavy work is device work behind the C ABI; `Backend` is the seam
+the parity tests use to run the same host logic over the CPU restatement.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .ba import BundleAdjuster, Frame, SlidingWindow
+
+
+@dataclass
+class FrameResult:
+    frame_id: int
+    is_keyframe: bool
+    T_W_B: np.ndarray
+    n_left: int
+    n_right: int
+    pnp_status: int | None       # None: window not full yet (no motion tracking)
+    ba_status: int | None        # None: no optimisation this frame
+
+
+class DeviceBackend:
+    """StereoPatchTracker (+ fused unprojection), MotionTracker and BundleAdjuster on one device."""
+
+    def __init__(self, width, height, cameras, levels, grid_size, max_iterations, thresh, window,
+                 translation_threshold, rotation_threshold, device):
+        from .motion import MotionTracker
+        from .tracker import StereoPatchTracker
+        self.tracker = StereoPatchTracker(width, height, levels=levels, grid_size=grid_size,
+                                          optical_flow_max_iterations=max_iterations,
+                                          optical_flow_convergence_threshold=thresh, device=device)
+        self.tracker.set_cameras(cameras[0], cameras[1])
+        self.motion = MotionTracker(device, translation_threshold, rotation_threshold)
+        self.solver = BundleAdjuster(max_keyframes=max(window, 2), device=device)
+
+    def track(self, left, right):
+        """Host u8 arrays, or device-resident u8 tensors (data_ptr; no H2D copy)."""
+        if hasattr(left, "data_ptr"):
+            nl, nr = self.tracker.process_frame_device(left.data_ptr(), right.data_ptr())
+            fl, fr = self.tracker._out_l[:nl], self.tracker._out_r[:nr]
+        else:
+            fl, fr = self.tracker.process_frame(left, right)
+        ul, ur = self.tracker.undistorted()
+        return (fl["id"].astype(np.int64), ul), (fr["id"].astype(np.int64), ur)
+
+    def set_map(self, ids, p_W):
+        self.motion.set_map(np.asarray(ids, np.uint64), np.asarray(p_W, np.float32))
+
+    def track_motion(self, T_W_B_last_kf, T_C_B2):
+        r = self.motion.track_motion_tracker(self.tracker, T_W_B_last_kf, T_C_B2)
+        return r.status, r.is_keyframe, r.T_W_B
+
+    def close(self):
+        for o in (self.tracker, self.motion, self.solver):
+            o.close()
+
+
+class Estimator:
+    """Estimator (estimator.rs:25-262) for a stereo rig; parameters default to
+    config/euroc_vio.yaml (6 pyramid levels, grid 50, 20 LK iterations, threshold 0.01, window
+    10, keyframe thresholds 0.05 m / 0.05 rad)."""
+
+    def __init__(self, width: int, height: int, cameras, T_B_Cl, T_B_Cr, levels: int = 6, grid_size: int = 50,
+                 max_iterations: int = 20, thresh: float = 0.01, window: int = 10,
+                 translation_threshold: float = 0.05, rotation_threshold: float = 0.05, device: int = 0,
+                 backend=None):
+        self.backend = backend or DeviceBackend(width, height, cameras, levels, grid_size, max_iterations, thresh,
+                                                window, translation_threshold, rotation_threshold, device)
+        self.window = SlidingWindow(window, device, solver=self.backend.solver)
+        self.T_B_Cl = np.asarray(T_B_Cl, np.float64)
+        self.T_B_Cr = np.asarray(T_B_Cr, np.float64)
+        self.frame_id = 0
+        self._map_key = None
+
+    def _T_C_B2(self):
+        # extrinsics of the front keyframe (sliding_window.rs:519-520); the rig is fixed here
+        front = self.window.keyframes[0]
+        return np.stack([np.linalg.inv(front.T_B_Cl).reshape(16), np.linalg.inv(front.T_B_Cr).reshape(16)])
+
+    def process_frame(self, left: np.ndarray, right: np.ndarray) -> FrameResult:
+        self.frame_id += 1
+        (ids_l, uv_l), (ids_r, uv_r) = self.backend.track(left, right)
+        frame = Frame(frame_id=self.frame_id, T_W_B=np.eye(4), T_B_Cl=self.T_B_Cl, T_B_Cr=self.T_B_Cr,
+                      is_keyframe=True, left_features=(ids_l, uv_l), right_features=(ids_r, uv_r))
+        pnp_status = None
+        if self.window.is_full():
+            if self.window.map_version != self._map_key:  # map_points changes only in optimize
+                mp = self.window.map_points
+                ids = np.array(sorted(mp), np.int64)
+                self.backend.set_map(ids, np.stack([mp[i] for i in ids]) if len(ids) else np.zeros((0, 3), np.float32))
+                self._map_key = self.window.map_version
+            status, is_kf, T_W_B = self.backend.track_motion(self.window.get_keyframe_poses()[-1], self._T_C_B2())
+            pnp_status = status
+            if status > 0:
+                frame.T_W_B = T_W_B
+                frame.is_keyframe = bool(is_kf)
+        ba_status = None
+        if frame.is_keyframe:
+            self.window.add_frame(frame)
+            if self.window.is_full():
+                self.window.optimize()
+                r = self.window.last_result
+                ba_status = None if r is None else int(r.status)
+        return FrameResult(self.frame_id, frame.is_keyframe, frame.T_W_B.copy(), len(ids_l), len(ids_r),
+                           pnp_status, ba_status)
+
+    def trajectory(self):
+        """T_W_B of the keyframes in the window."""
+        return self.window.get_keyframe_poses()
+
+    def close(self):
+        if hasattr(self.backend, "close"):
+            self.backend.close()

@@ -434,3 +434,168 @@ def mono_sequence(n_frames: int, w: int = 752, h: int = 480, seed: int = 2026032
     rng = np.random.default_rng(seed + 1)
     for t in range(n_frames):
         yield render_mosaic(rects, w, h, t, 0.01 * rng.standard_normal((h, w)))
+
+
+# ----------------------------------------------------------------------------------------
+# Full-pipeline stream (config 4): rendered stereo of a piecewise-planar scene
+# ----------------------------------------------------------------------------------------
+# config/euroc_vio.yaml:11-17 (cam0 / cam1 intrinsics and radtan distortion)
+EUROC_INTRINSICS = ((458.654, 457.296, 367.215, 248.375, -0.28340811, 0.07395907, 0.00019359, 1.76187114e-05),
+                    (457.587, 456.134, 379.999, 255.238, -0.28368365, 0.07451284, -0.00010473, -3.55590700e-05))
+
+
+def radtan_undistort_map(params, w: int, h: int, iterations: int = 20) -> np.ndarray:
+    """Normalised undistorted (x, y) of every pixel centre (h x w x 2, f64): Newton on the
+    radtan model x_d = x (1 + k1 r^2 + k2 r^4) + 2 p1 x y + p2 (r^2 + 2 x^2) (and y)."""
+    fx, fy, cx, cy, k1, k2, p1, p2 = params
+    v, u = np.mgrid[0:h, 0:w].astype(np.float64)
+    xd, yd = (u - cx) / fx, (v - cy) / fy
+    x, y = xd.copy(), yd.copy()
+    for _ in range(iterations):
+        r2 = x * x + y * y
+        rad = 1.0 + k1 * r2 + k2 * r2 * r2
+        fxv = x * rad + 2 * p1 * x * y + p2 * (r2 + 2 * x * x) - xd
+        fyv = y * rad + 2 * p2 * x * y + p1 * (r2 + 2 * y * y) - yd
+        drad = 2 * k1 + 4 * k2 * r2
+        j11 = rad + x * x * drad + 2 * p1 * y + 6 * p2 * x
+        j12 = x * y * drad + 2 * p1 * x + 2 * p2 * y
+        j21 = x * y * drad + 2 * p2 * y + 2 * p1 * x
+        j22 = rad + y * y * drad + 2 * p2 * x + 6 * p1 * y
+        det = j11 * j22 - j12 * j21
+        x = x - (j22 * fxv - j12 * fyv) / det
+        y = y - (-j21 * fxv + j11 * fyv) / det
+    return np.stack([x, y], -1)
+
+
+@dataclass
+class SceneStream:
+    """Config-4 input: rendered stereo frames, their true body poses and the rig."""
+    frames: list            # [(left u8 h x w, right u8 h x w)]
+    T_W_B: list             # true body poses (4 x 4)
+    T_B_Cl: np.ndarray
+    T_B_Cr: np.ndarray
+    intrinsics: tuple       # (cam0, cam1) radtan parameters (fx, fy, cx, cy, k1, k2, p1, p2)
+
+
+def _scene_setup(n_frames, w, h, step, seed):
+    rng = np.random.default_rng(seed)
+    s = w / 752.0
+    intr = tuple((p[0] * s, p[1] * s, p[2] * s, p[3] * (h / 480.0)) + tuple(p[4:]) for p in EUROC_INTRINSICS)
+    tex_w, tex_h = 1536, 1024
+    tex = make_texture(tex_w, tex_h, n_blobs=int(6000 * tex_w * tex_h / (752 * 480)), seed=seed + 100)
+    T = _render(tex, tex_w, tex_h, 0, False, np.zeros((tex_h, tex_w))).astype(np.float64)
+    bands = []  # (y0, y1, z, texture offset)
+    y = -3.0
+    while y < 3.0 + step * n_frames + 3.0:
+        wdt = rng.uniform(0.6, 1.6)
+        bands.append((y, y + wdt, rng.uniform(3.0, 8.0), rng.uniform(0, tex_w * 0.004)))
+        y += wdt
+    bands.append((-1e9, 1e9, 12.0, 0.77))
+    rays = [radtan_undistort_map(p[:8], w, h) for p in intr]
+    return rng, intr, T, bands, rays
+
+
+def _scene_image(xp, T, bands, ray, T_W_C):
+    """Noise-free image of the plane scene through one camera; xp is numpy or torch (same math,
+    f64).  Each pixel's ray hits the nearest band plane; texture sampled bilinearly, periodic."""
+    res = 0.004
+    tex_h, tex_w = T.shape
+    R, o = T_W_C[:3, :3], T_W_C[:3, 3]
+    d = [ray[..., 0] * R[i, 0] + ray[..., 1] * R[i, 1] + R[i, 2] for i in range(3)]
+    best = xp.full(ray.shape[:2], float("inf"), **xp.kw)
+    u = xp.zeros(ray.shape[:2], **xp.kw)
+    v = xp.zeros(ray.shape[:2], **xp.kw)
+    for (y0, y1, z, off) in bands:
+        tt = (z - o[2]) / d[2]
+        X = o[0] + tt * d[0]
+        Y = o[1] + tt * d[1]
+        hit = (tt > 0) & (Y >= y0) & (Y < y1) & (tt < best)
+        best = xp.where(hit, tt, best)
+        u = xp.where(hit, (Y + off) / res, u)
+        v = xp.where(hit, X / res, v)
+    u = u % (tex_w - 1)
+    v = v % (tex_h - 1)
+    iu, iv = xp.floor(u), xp.floor(v)
+    fu, fv = u - iu, v - iv
+    iu, iv = xp.long(iu), xp.long(iv)
+    iu1, iv1 = xp.minimum(iu + 1, tex_w - 1), xp.minimum(iv + 1, tex_h - 1)
+    return (1 - fv) * ((1 - fu) * T[iv, iu] + fu * T[iv, iu1]) + fv * ((1 - fu) * T[iv1, iu] + fu * T[iv1, iu1])
+
+
+class _NumpyOps:
+    kw = {}
+    where, floor, minimum, full, zeros = np.where, np.floor, np.minimum, np.full, np.zeros
+
+    @staticmethod
+    def long(a):
+        return a.astype(np.int64)
+
+
+def euroc_scene_stream(n_frames: int, w: int = 752, h: int = 480, step: float = 0.02, seed: int = 4,
+                       noise: float = 2.0) -> SceneStream:
+    """BASELINE config 4: stereo renderings of textured planes at 3-8 m with the
+    EuRoC rig (intrinsics, radtan distortion, T_B_Cl / T_B_Cr) moving `step` m per frame along
+    the body y axis (the cameras' x axis).  Planes are world z = const over bands of world y,
+    a background plane at 12 m; each plane carries a blob texture (4 mm texels, periodic),
+    sampled bilinearly, plus `noise` * N(0, 1) per pixel.  Intrinsics scale with w / 752."""
+    rng, intr, T, bands, rays = _scene_setup(n_frames, w, h, step, seed)
+    T_B_C = (T_B_CL, T_B_CR)
+    frames, poses = [], []
+    for t in range(n_frames):
+        T_W_B = np.eye(4)
+        T_W_B[1, 3] = step * t
+        poses.append(T_W_B)
+        pair = []
+        for c in range(2):
+            img = _scene_image(_NumpyOps, T, bands, rays[c], T_W_B @ T_B_C[c])
+            img += noise * rng.standard_normal((h, w))
+            pair.append(np.clip(np.rint(img), 0, 255).astype(np.uint8))
+        frames.append(tuple(pair))
+    return SceneStream(frames=frames, T_W_B=poses, T_B_Cl=T_B_CL.copy(), T_B_Cr=T_B_CR.copy(), intrinsics=intr)
+
+
+def euroc_scene_stream_device(n_frames: int, device, w: int = 752, h: int = 480, step: float = 0.02, seed: int = 4,
+                              noise: float = 2.0) -> SceneStream:
+    """euroc_scene_stream rendered with torch on `device` (bench input generation: 500 frames in
+    seconds, resident in HBM).  Same scene and poses; the noise comes from torch's generator, so
+    frames differ from the numpy stream by the noise only.  frames: [(left, right)] u8 tensors."""
+    import torch
+
+    class Ops:
+        kw = {"dtype": torch.float64, "device": device}
+        where, floor = torch.where, torch.floor
+
+        @staticmethod
+        def minimum(a, b):
+            return torch.clamp(a, max=b)
+
+        @staticmethod
+        def full(shape, val, **kw):
+            return torch.full(tuple(shape), val, **kw)
+
+        @staticmethod
+        def zeros(shape, **kw):
+            return torch.zeros(tuple(shape), **kw)
+
+        @staticmethod
+        def long(a):
+            return a.long()
+
+    _, intr, T, bands, rays = _scene_setup(n_frames, w, h, step, seed)
+    T = torch.as_tensor(T, device=device)
+    rays = [torch.as_tensor(r, device=device) for r in rays]
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    T_B_C = (T_B_CL, T_B_CR)
+    frames, poses = [], []
+    for t in range(n_frames):
+        T_W_B = np.eye(4)
+        T_W_B[1, 3] = step * t
+        poses.append(T_W_B)
+        pair = []
+        for c in range(2):
+            img = _scene_image(Ops, T, bands, rays[c], T_W_B @ T_B_C[c])
+            img += noise * torch.randn((h, w), generator=gen, dtype=torch.float64, device=device)
+            pair.append(torch.clamp(torch.round(img), 0, 255).to(torch.uint8).contiguous())
+        frames.append(tuple(pair))
+    return SceneStream(frames=frames, T_W_B=poses, T_B_Cl=T_B_CL.copy(), T_B_Cr=T_B_CR.copy(), intrinsics=intr)

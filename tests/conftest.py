@@ -35,3 +35,10 @@ def gpu():
 def stereo_frames():
     from rsvio import synthetic as S
     return list(S.stereo_sequence(4))
+
+
+@pytest.fixture(scope="session")
+def scene_stream():
+    """Config 4's rendered stereo stream, shortened: 24 frames, window 5."""
+    from rsvio import synthetic as S
+    return S.euroc_scene_stream(24), 5

@@ -1,0 +1,67 @@
+"""Config 4 on the GPU: the Estimator (estimator.rs:101-262) over the device backend -- tracker
+with fused unprojection, PnP + keyframe rule, BA -- against the same host logic over the oracle
+backend (oracle/estimator.py), frame by frame on the rendered stream.
+
+Parity: features (ids, f32 undistorted coordinates) bit-exact every frame (trig mode 1, the
+oracle's device-matched sin/cos); integer outcomes (keyframe flag, PnP status, BA status) equal;
+poses within 1e-6 m / rad -- BA and PnP agree to 1e-7 per solve (test_ba_gpu, test_motion_gpu)
+and map points are narrowed to f32 between solves, so differences may carry over frames.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-6
+
+
+class _Spy:
+    """Wraps a backend's track() to keep what it returned."""
+
+    def __init__(self, be):
+        self.be = be
+        self.solver = be.solver
+        self.feats = None
+
+    def track(self, l, r):
+        self.feats = self.be.track(l, r)
+        return self.feats
+
+    def __getattr__(self, k):
+        return getattr(self.be, k)
+
+
+def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
+    from oracle.estimator import OracleBackend
+    from rsvio.camera import Camera
+    from rsvio.estimator import DeviceBackend, Estimator
+    s, win = scene_stream
+    h, w = s.frames[0][0].shape
+    cams = [Camera.opencv5(*p) for p in s.intrinsics]
+    oracle.set_trig_mode(1)
+    try:
+        dev = _Spy(DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0))
+        orc = _Spy(OracleBackend(oracle, w, h, cams))
+        ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev)
+        eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=orc)
+        n_kf = 0
+        for k, (l, r) in enumerate(s.frames):
+            rd = ed.process_frame(l, r)
+            ro = eo.process_frame(l, r)
+            for (ids_d, uv_d), (ids_o, uv_o) in zip(dev.feats, orc.feats):
+                assert np.array_equal(ids_d, ids_o), f"frame {k}"
+                assert np.array_equal(np.asarray(uv_d, np.float32).view(np.uint32),
+                                      np.asarray(uv_o, np.float32).view(np.uint32)), f"frame {k}"
+            assert (rd.is_keyframe, rd.pnp_status, rd.ba_status) == (ro.is_keyframe, ro.pnp_status, ro.ba_status), \
+                f"frame {k}"
+            assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
+            n_kf += rd.is_keyframe
+        for Td, To in zip(ed.trajectory(), eo.trajectory()):
+            assert np.abs(Td - To).max() <= POSE_TOL
+        assert win < n_kf < len(s.frames)
+        md, mo = ed.window.map_points, eo.window.map_points
+        assert sorted(md) == sorted(mo)
+        assert max(np.abs(md[i].astype(np.float64) - mo[i]).max() for i in md) <= 1e-5
+        dev.be.close()
+    finally:
+        oracle.set_trig_mode(0)
