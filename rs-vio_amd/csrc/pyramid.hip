@@ -15,9 +15,10 @@ namespace rsvio {
 
 namespace {
 
-constexpr int TW = 64;
-constexpr int TH = 8;
-constexpr int LDS_COLS = 1024;  // >= 64 * ratio + 2 * ratio + 4 for every level of a <= 2048-wide image
+constexpr int TW = 64;               // widest output tile (level 1)
+constexpr int TH = 8;                // tallest output tile (level 1)
+constexpr int STRIP_COLS = 320;      // target input columns of a tile's source strip
+constexpr size_t LDS_CAP = 64 << 10; // a level whose strip exceeds this reads its taps from HBM
 
 __device__ __forceinline__ float triangle_kernel(float x) {
     float ax = fabsf(x);
@@ -56,15 +57,16 @@ __global__ void make_taps_kernel(TapTable tab, int n_entries) {
 }
 
 __global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
-    __shared__ float tmp[TH * LDS_COLS];
+    extern __shared__ uint32_t smem[];
     const int img = blockIdx.y;
     const uint8_t* __restrict__ src = io.src[img];
     uint8_t* __restrict__ dst_base = io.dst[img];
     int b = blockIdx.x;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst_base)) & 15) == 0;
     // level-0 copy blocks first (16 B per lane)
     if (b < L.copy_blocks) {
         const size_t tot = (size_t)L.w * L.h;
-        if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst_base)) & 15) {
+        if (!aligned) {
             for (size_t i = (size_t)b * blockDim.x + threadIdx.x; i < tot; i += (size_t)L.copy_blocks * blockDim.x)
                 dst_base[i] = src[i];
             return;
@@ -84,44 +86,76 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
     while (lev < L.levels - 1 && b >= L.tile_start[lev + 1]) ++lev;
     b -= L.tile_start[lev];
     const int nw = (int)level_w(L.w, lev), nh = (int)level_h(L.h, lev);
-    const int tw = L.tile_w[lev];
+    const int tw = L.tile_w[lev], th = L.tile_h[lev];
     const int tiles_x = (nw + tw - 1) / tw;
     const int tx = b % tiles_x, ty = b / tiles_x;
     const int ox0 = tx * tw, ox1 = min(ox0 + tw, nw);
-    const int oy0 = ty * TH, oy1 = min(oy0 + TH, nh);
+    const int oy0 = ty * th, oy1 = min(oy0 + th, nh);
     const int rows = oy1 - oy0, cols_out = ox1 - ox0;
     const int hx = L.hx_ent[lev], vy = L.vy_ent[lev];
     const TapTable& T = L.tab;
     const int xl = T.left[hx + ox0];
     const int xr = T.left[hx + ox1 - 1] + T.count[hx + ox1 - 1];
-    const int ncols = xr - xl;
-    // vertical pass: tmp[r][c] = sum_k src[(vleft + k) * w + xl + c] * vw[k]
+    const int yl = T.left[vy + oy0];
+    const int yr = T.left[vy + oy1 - 1] + T.count[vy + oy1 - 1];
+    const int ncols = xr - xl, nrows = yr - yl;
+    // 1. stage the source strip [yl, yr) x [xa, xr) in LDS: dword loads (every lane independent,
+    //    one latency round) when rows are 4-byte aligned, else bytes.  Levels whose strip would
+    //    not fit (ratio >= 64) read their taps from HBM instead (L.direct).
+    const int xa = xl & ~3, xoff = xl - xa;
+    const int pd = (xr - xa + 3) >> 2;  // dwords per strip row
+    const bool direct = (L.direct >> lev) & 1;
+    uint8_t* strip = reinterpret_cast<uint8_t*>(smem);
+    if (!direct) {
+        if (aligned && (L.w & 3) == 0) {
+            // xr <= w and w % 4 == 0: the last dword of a row ends at or before the row's end
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+            const int wd = (int)(L.w >> 2);
+            for (int idx = threadIdx.x; idx < nrows * pd; idx += blockDim.x) {
+                const int r = idx / pd, d = idx - r * pd;
+                smem[idx] = s32[(size_t)(yl + r) * wd + (xa >> 2) + d];
+            }
+        } else {
+            for (int idx = threadIdx.x; idx < nrows * pd * 4; idx += blockDim.x) {
+                const int r = idx / (pd * 4), c = idx - r * pd * 4;
+                strip[idx] = (xa + c < (int)L.w) ? src[(size_t)(yl + r) * L.w + xa + c] : 0;
+            }
+        }
+    }
+    float* tmp = reinterpret_cast<float*>(smem + (direct ? 0 : nrows * pd));
+    __syncthreads();
+    // 2. vertical pass: tmp[r][c] = sum_k src[vleft + k][c] * vw[k], taps summed in order
     for (int idx = threadIdx.x; idx < rows * ncols; idx += blockDim.x) {
         const int r = idx / ncols, c = idx - r * ncols;
         const int e = vy + oy0 + r;
         const int vl = T.left[e], vc = T.count[e];
         const float* __restrict__ vw = T.weights + (size_t)e * T.max_taps;
-        const uint8_t* __restrict__ col = src + (size_t)vl * L.w + xl + c;
         float acc = 0.0f;
-        // taps loaded 8 at a time (independent loads in flight), summed in tap order
-        for (int k = 0; k < vc; k += 8) {
-            float px[8];
+        if (!direct) {
+            const uint8_t* col = strip + (vl - yl) * pd * 4 + xoff + c;
+            for (int k = 0; k < vc; ++k) acc += (float)col[k * pd * 4] * vw[k];
+        } else {
+            const uint8_t* __restrict__ col = src + (size_t)vl * L.w + xl + c;
+            for (int k = 0; k < vc; k += 8) {
+                float px[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) px[u] = (k + u < vc) ? (float)col[(size_t)(k + u) * L.w] : 0.0f;
+                for (int u = 0; u < 8; ++u) px[u] = (k + u < vc) ? (float)col[(size_t)(k + u) * L.w] : 0.0f;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (k + u < vc) acc += px[u] * vw[k + u];
+                for (int u = 0; u < 8; ++u)
+                    if (k + u < vc) acc += px[u] * vw[k + u];
+            }
         }
-        tmp[r * LDS_COLS + c] = acc;
+        tmp[r * ncols + c] = acc;
     }
     __syncthreads();
+    // 3. horizontal pass, clamp, round to u8
     uint8_t* __restrict__ dst = dst_base + level_offset(L.w, L.h, lev);
     for (int idx = threadIdx.x; idx < rows * cols_out; idx += blockDim.x) {
         const int r = idx / cols_out, c = idx - r * cols_out;
         const int e = hx + ox0 + c;
         const int hl = T.left[e] - xl, hc = T.count[e];
         const float* __restrict__ hw = T.weights + (size_t)e * T.max_taps;
-        const float* __restrict__ row = tmp + r * LDS_COLS + hl;
+        const float* __restrict__ row = tmp + r * ncols + hl;
         float acc = 0.0f;
         for (int k = 0; k < hc; ++k) acc += row[k] * hw[k];
         float cl = acc < 0.0f ? 0.0f : (acc > 255.0f ? 255.0f : acc);
@@ -148,12 +182,13 @@ void PyramidPlan::init(int w_, int h_, int levels_) {
         for (int o = 0; o < nw; ++o) { in_len.push_back(w); out_len.push_back(nw); out_idx.push_back(o); }
         launch.vy_ent[i] = (int)in_len.size();
         for (int o = 0; o < nh; ++o) { in_len.push_back(h); out_len.push_back(nh); out_idx.push_back(o); }
-        float rx = (float)w / nw;
-        max_ratio = std::max(max_ratio, std::max(rx, (float)h / nh));
-        // widest input span of a tile of tw outputs: tw * rx + 2 * rx + 3 columns
-        int tw = std::min(TW, (int)std::floor((LDS_COLS - 2.0f * rx - 4.0f) / rx));
-        if (tw < 1) throw std::invalid_argument("image too wide for the pyramid tile");
-        launch.tile_w[i] = tw;
+        float rx = (float)w / nw, ry = (float)h / nh;
+        max_ratio = std::max(max_ratio, std::max(rx, ry));
+        // Equal work per tile across levels: deeper levels (more taps per output) get fewer
+        // output rows and columns, so a level-5 tile is not 100x a level-1 tile.  A tile of tw
+        // outputs spans at most tw * rx + 2 * rx + 3 input columns.
+        launch.tile_h[i] = std::max(1, std::min(TH, (int)(16.0f / ry)));
+        launch.tile_w[i] = std::max(1, std::min(TW, (int)std::floor((STRIP_COLS - 2.0f * rx - 4.0f) / rx)));
     }
     n_entries = (int)in_len.size();
     max_taps = (int)std::ceil(2.0f * max_ratio) + 4;
@@ -161,7 +196,7 @@ void PyramidPlan::init(int w_, int h_, int levels_) {
     for (int i = 1; i < levels; ++i) {
         launch.tile_start[i] = tiles;
         int nw = (int)level_w(w, i), nh = (int)level_h(h, i);
-        tiles += ((nw + launch.tile_w[i] - 1) / launch.tile_w[i]) * ((nh + TH - 1) / TH);
+        tiles += ((nw + launch.tile_w[i] - 1) / launch.tile_w[i]) * ((nh + launch.tile_h[i] - 1) / launch.tile_h[i]);
     }
     launch.tile_start[levels] = tiles;
     launch.copy_blocks = std::max(1, (int)(((size_t)w * h / 16 + 255) / 256 / 4));
@@ -184,13 +219,38 @@ void PyramidPlan::init(int w_, int h_, int levels_) {
         RSVIO_HIP(hipGetLastError());
         RSVIO_HIP(hipDeviceSynchronize());
         launch.tab = t;
+        // exact dynamic LDS: the largest (strip + vertical-pass) footprint over all tiles
+        std::vector<int> left(n_entries), count(n_entries);
+        RSVIO_HIP(hipMemcpy(left.data(), d_left.p, sizeof(int) * n_entries, hipMemcpyDeviceToHost));
+        RSVIO_HIP(hipMemcpy(count.data(), d_count.p, sizeof(int) * n_entries, hipMemcpyDeviceToHost));
+        for (int i = 1; i < levels; ++i) {
+            const int nw = (int)level_w(w, i), nh = (int)level_h(h, i);
+            const int tw = launch.tile_w[i], th = launch.tile_h[i];
+            size_t strip = 0, vert = 0;
+            for (int ox0 = 0; ox0 < nw; ox0 += tw) {
+                const int ox1 = std::min(ox0 + tw, nw);
+                const int xl = left[launch.hx_ent[i] + ox0];
+                const int xr = left[launch.hx_ent[i] + ox1 - 1] + count[launch.hx_ent[i] + ox1 - 1];
+                const size_t pd = (size_t)(xr - (xl & ~3) + 3) / 4;
+                for (int oy0 = 0; oy0 < nh; oy0 += th) {
+                    const int oy1 = std::min(oy0 + th, nh);
+                    const int yl = left[launch.vy_ent[i] + oy0];
+                    const int yr = left[launch.vy_ent[i] + oy1 - 1] + count[launch.vy_ent[i] + oy1 - 1];
+                    strip = std::max(strip, 4 * pd * (size_t)(yr - yl));
+                    vert = std::max(vert, 4 * (size_t)(oy1 - oy0) * (size_t)(xr - xl));
+                }
+            }
+            if (vert > LDS_CAP) throw std::invalid_argument("image too wide for the pyramid tile");
+            if (strip + vert > LDS_CAP) launch.direct |= 1u << i;
+            lds_bytes = std::max(lds_bytes, ((launch.direct >> i) & 1) ? vert : strip + vert);
+        }
     }
 }
 
 void PyramidPlan::enqueue(const PyrIO& io, int n_img, hipStream_t s) const {
     if (n_img <= 0) return;
     if (n_img > kMaxPyrIO) throw std::invalid_argument("too many images per pyramid launch");
-    hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks, n_img), dim3(256), 0, s, launch, io);
+    hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks, n_img), dim3(256), lds_bytes, s, launch, io);
     RSVIO_HIP(hipGetLastError());
 }
 

@@ -30,6 +30,8 @@ struct PyrLaunch {
     int copy_blocks;
     int tile_start[kMaxLevels + 1];
     int tile_w[kMaxLevels];
+    int tile_h[kMaxLevels];
+    uint32_t direct;  // bit i: level i reads its vertical taps from HBM (strip exceeds LDS_CAP)
     int hx_ent[kMaxLevels];
     int vy_ent[kMaxLevels];
     TapTable tab;
@@ -44,6 +46,7 @@ struct PyrIO {
 struct PyramidPlan {
     int w = 0, h = 0, levels = 0;
     int n_entries = 0, max_taps = 0, total_blocks = 0;
+    size_t lds_bytes = 0;  // dynamic LDS of pyramid_kernel: source strip (u8) + vertical pass (f32)
     PyrLaunch launch;
     DevBuf<int> i_in, i_out, i_idx, d_left, d_count;
     DevBuf<float> d_w;
