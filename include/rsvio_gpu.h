@@ -128,6 +128,14 @@ typedef struct {
 } rsvio_track_batch;
 int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, int32_t n_batches,
                          int32_t max_iterations, float thresh, void* stream);
+/* Batched serving mode: any number of independent track_points batches (e.g. 3 per stereo
+ * stream for many streams) in one launch.  d_table: n_batches descriptors in DEVICE memory;
+ * d_start: n_batches + 1 int32 prefix sums of their sizes in device memory (d_start[0] = 0);
+ * total = d_start[n_batches], given on the host for the grid size.  Same per-feature results as
+ * rsvio_track_points_d (feature_tracker.rs:252-291). */
+int rsvio_track_points_table_d(rsvio_track_ctx* c, const rsvio_track_batch* d_table, const int32_t* d_start,
+                               int32_t n_batches, int32_t total, int32_t max_iterations, float thresh,
+                               void* stream);
 
 /* ====== T-sec: the feature_tracker/ crate (FeatureTracker, bicubic LK + Shi-Tomasi) ====== */
 

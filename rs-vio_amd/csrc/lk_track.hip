@@ -343,15 +343,35 @@ __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, 
 
 __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     const int job = blockIdx.x;
-    int b = 0;
-    while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
-    const int idx = job - L.start[b];
-    if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
+    const uint8_t* pyr0;
+    const uint8_t* pyr1;
+    const float* ain;
+    float* aout;
+    uint8_t* valid;
+    int idx;
+    if (L.table != nullptr) {
+        // largest b with tstart[b] <= job (binary search over the device prefix)
+        int lo = 0, hi = L.nb - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L.tstart[mid] <= job) lo = mid; else hi = mid - 1;
+        }
+        const rsvio_track_batch& d = L.table[lo];
+        idx = job - L.tstart[lo];
+        if (idx >= d.n) return;
+        pyr0 = d.d_pyr0; pyr1 = d.d_pyr1; ain = d.d_aff_in; aout = d.d_aff_out; valid = d.d_valid;
+    } else {
+        int b = 0;
+        while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
+        idx = job - L.start[b];
+        if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
+        pyr0 = L.pyr0[b]; pyr1 = L.pyr1[b]; ain = L.ain[b]; aout = L.aout[b]; valid = L.valid[b];
+    }
     __shared__ __attribute__((aligned(16))) float sh[6 * kChainLd];
     const int lane = threadIdx.x;
     const float patx = lane < NP ? (float)kPattern[lane][0] / 2.0f : 0.0f;
     const float paty = lane < NP ? (float)kPattern[lane][1] / 2.0f : 0.0f;
-    const float* a = L.ain[b] + 6 * (size_t)idx;
+    const float* a = ain + 6 * (size_t)idx;
     Aff T0;
     T0.m00 = a[0]; T0.m01 = a[1]; T0.m10 = a[2]; T0.m11 = a[3]; T0.m02 = a[4]; T0.m12 = a[5];
     T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
@@ -360,11 +380,11 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] = 0;
 #endif
     STAMP(0);
-    bool ok = track_one(L.pyr0[b], L.pyr1[b], L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
+    bool ok = track_one(pyr0, pyr1, L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
                         L.thresh, fwd, sh);
     STAMP(1);
     if (ok)
-        ok = track_one(L.pyr1[b], L.pyr0[b], L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
+        ok = track_one(pyr1, pyr0, L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
                        L.thresh, bwd, sh);
     STAMP(2);
     if (ok) {
@@ -373,13 +393,13 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
         ok = (dx * dx + dy * dy) < 0.4f;
     }
     if (lane == 0) {
-        float* o = L.aout[b] + 6 * (size_t)idx;
+        float* o = aout + 6 * (size_t)idx;
         if (ok) {
             o[0] = fwd.m00; o[1] = fwd.m01; o[2] = fwd.m10; o[3] = fwd.m11; o[4] = fwd.m02; o[5] = fwd.m12;
         } else {
             for (int k = 0; k < 6; ++k) o[k] = a[k];
         }
-        L.valid[b][idx] = ok ? 1 : 0;
+        valid[idx] = ok ? 1 : 0;
     }
 }
 
@@ -388,7 +408,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
 RSVIO_DBG_READER(rsvio_dbg_lk_stamps)
 
 void enqueue_track(const TrackLaunch& L, hipStream_t s) {
-    const int total = L.start[L.nb];
+    const int total = L.table != nullptr ? L.start[0] : L.start[L.nb];
     if (total <= 0) return;
     hipLaunchKernelGGL(lk_track_kernel, dim3(total), dim3(64), 0, s, L);
     RSVIO_HIP(hipGetLastError());

@@ -21,6 +21,10 @@ struct TrackLaunch {
     float* aout[kMaxTrackBatches];
     uint8_t* valid[kMaxTrackBatches];
     const int* dcount[kMaxTrackBatches];       // optional device-side count (early exit)
+    // batched serving mode (rsvio_track_points_table_d): when set, batch descriptors and the
+    // prefix of their sizes come from device memory and nb may exceed kMaxTrackBatches
+    const rsvio_track_batch* table;
+    const int32_t* tstart;
 };
 
 void enqueue_track(const TrackLaunch& L, hipStream_t s);

@@ -59,8 +59,8 @@ __global__ void make_taps_kernel(TapTable tab, int n_entries) {
 __global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
     extern __shared__ uint32_t smem[];
     const int img = blockIdx.y;
-    const uint8_t* __restrict__ src = io.src[img];
-    uint8_t* __restrict__ dst_base = io.dst[img];
+    const uint8_t* __restrict__ src = io.psrc ? io.psrc + (size_t)img * L.w * L.h : io.src[img];
+    uint8_t* __restrict__ dst_base = io.psrc ? io.pdst + (size_t)img * L.pyr_bytes : io.dst[img];
     int b = blockIdx.x;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst_base)) & 15) == 0;
     // level-0 copy blocks first (16 B per lane)
@@ -249,20 +249,17 @@ void PyramidPlan::init(int w_, int h_, int levels_) {
 
 void PyramidPlan::enqueue(const PyrIO& io, int n_img, hipStream_t s) const {
     if (n_img <= 0) return;
-    if (n_img > kMaxPyrIO) throw std::invalid_argument("too many images per pyramid launch");
+    if (n_img > (io.psrc ? 65535 : kMaxPyrIO)) throw std::invalid_argument("too many images per pyramid launch");
     hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks, n_img), dim3(256), lds_bytes, s, launch, io);
     RSVIO_HIP(hipGetLastError());
 }
 
 void PyramidPlan::enqueue(const uint8_t* d_imgs, int n_img, uint8_t* d_pyrs, hipStream_t s) const {
-    for (int i0 = 0; i0 < n_img; i0 += kMaxPyrIO) {
-        PyrIO io;
-        int n = std::min(kMaxPyrIO, n_img - i0);
-        for (int k = 0; k < n; ++k) {
-            io.src[k] = d_imgs + (size_t)(i0 + k) * w * h;
-            io.dst[k] = d_pyrs + (size_t)(i0 + k) * pyr_bytes();
-        }
-        enqueue(io, n, s);
+    for (int i0 = 0; i0 < n_img; i0 += 65535) {
+        PyrIO io{};
+        io.psrc = d_imgs + (size_t)i0 * w * h;
+        io.pdst = d_pyrs + (size_t)i0 * pyr_bytes();
+        enqueue(io, std::min(65535, n_img - i0), s);
     }
 }
 

@@ -41,6 +41,9 @@ constexpr int kMaxPyrIO = 8;
 struct PyrIO {
     const uint8_t* src[kMaxPyrIO];
     uint8_t* dst[kMaxPyrIO];
+    // packed mode (any number of images): image i at psrc + i * w * h, pyramid i at pdst + i * pyr_bytes
+    const uint8_t* psrc;
+    uint8_t* pdst;
 };
 
 struct PyramidPlan {

@@ -430,7 +430,7 @@ struct Tracker {
     // Enqueue one frame; images already in device memory.
     void enqueue_frame(const uint8_t* d_left, const uint8_t* d_right) {
         const int nxt = has_prev ? 1 - cur : cur;
-        PyrIO io;
+        PyrIO io{};
         io.src[0] = d_left; io.dst[0] = pyr(nxt, 0);
         io.src[1] = d_right; io.dst[1] = pyr(nxt, 1);
         plan.enqueue(io, 2, stream);
@@ -728,6 +728,23 @@ int rsvio_track_points_d(rsvio_track_ctx* c, const rsvio_track_batch* batches, i
             L.ain[b] = batches[b].d_aff_in; L.aout[b] = batches[b].d_aff_out; L.valid[b] = batches[b].d_valid;
             L.dcount[b] = nullptr;
         }
+        rsvio::enqueue_track(L, (hipStream_t)stream);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_track_points_table_d(rsvio_track_ctx* c, const rsvio_track_batch* d_table, const int32_t* d_start,
+                               int32_t n_batches, int32_t total, int32_t max_iterations, float thresh,
+                               void* stream) {
+    if (!c || n_batches < 0 || total < 0 || (n_batches > 0 && (!d_table || !d_start))) return RSVIO_ERR_INVALID_ARG;
+    if (n_batches == 0 || total == 0) return RSVIO_OK;
+    return guarded([&] {
+        rsvio::TrackLaunch L{};
+        L.w = c->c.plan.w; L.h = c->c.plan.h; L.levels = c->c.plan.levels;
+        L.max_iter = max_iterations; L.thresh = thresh; L.nb = n_batches;
+        L.start[0] = total;  // table mode: the grid size
+        L.table = d_table;
+        L.tstart = d_start;
         rsvio::enqueue_track(L, (hipStream_t)stream);
         return (int)RSVIO_OK;
     });

@@ -123,6 +123,7 @@ SIG = {
     "rsvio_track_ctx_destroy": (None, [P]),
     "rsvio_build_pyramids_d": (C.c_int, [P, P, C.c_int32, P, P]),
     "rsvio_track_points_d": (C.c_int, [P, C.POINTER(TrackBatch), C.c_int32, C.c_int32, C.c_float, P]),
+    "rsvio_track_points_table_d": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_float, P]),
     "rsvio_ba_create": (C.c_int, [C.POINTER(BaParams), C.POINTER(P)]),
     "rsvio_ba_destroy": (None, [P]),
     "rsvio_ba_solve": (C.c_int, [P, C.c_int32, P, P, C.c_int32, P, C.c_int32, P, P, P, P, P,

@@ -206,3 +206,86 @@ def test_stereo_tracker_bad_input(gpu):
         trk.process_frame(np.zeros((10, 10), np.uint8), np.zeros((10, 10), np.uint8))
     with pytest.raises(gpu.RsvioError):
         gpu.StereoPatchTracker(8, 8, levels=3)
+
+
+def _batch_table(lib_mod, specs, dev):
+    """Device descriptor table (rsvio_track_batch[]) + int32 prefix of the batch sizes."""
+    import ctypes as C
+
+    import torch
+    tb = (lib_mod.TrackBatch * len(specs))()
+    for i, (p0, p1, a, o, v, n) in enumerate(specs):
+        tb[i] = lib_mod.TrackBatch(p0, p1, a, o, v, n)
+    raw = np.frombuffer(C.string_at(C.addressof(tb), C.sizeof(tb)), np.uint8).copy()
+    start = np.concatenate([[0], np.cumsum([s[5] for s in specs])]).astype(np.int32)
+    return torch.from_numpy(raw).to(dev), torch.from_numpy(start).to(dev), int(start[-1])
+
+
+def test_track_points_table_batched(gpu, oracle, stereo_frames):
+    """Batched serving mode: 4 stereo streams x 3 batches (cam0 temporal, cam1 temporal, stereo)
+    in ONE rsvio_track_points_table_d launch, ragged sizes plus an empty batch; pyramids of 10
+    images through the packed path (more than one launch's worth of pointer slots).  Every batch
+    is bit-identical to the oracle (trig mode 1)."""
+    import ctypes as C
+
+    import torch
+
+    from rsvio import _lib
+    from rsvio import synthetic as S
+    lib = _lib.load()
+    w, h, L = 752, 480, 3
+    dev = torch.device("cuda", 0)
+    frames = stereo_frames
+    # streams s = 0..3 track frame (s % 3) -> (s % 3) + 1; images of 5 frames (10 images), packed
+    imgs = np.stack([np.stack(f) for f in frames[:4]] + [np.stack(frames[0])]).reshape(10, h, w)
+    pb = int(lib.rsvio_pyramid_bytes(w, h, L))
+    ctx = C.c_void_p()
+    _lib.check(lib.rsvio_track_ctx_create(w, h, L, 0, C.byref(ctx)))
+    try:
+        d_imgs = torch.from_numpy(imgs).to(dev)
+        d_pyr = torch.empty((10, pb), dtype=torch.uint8, device=dev)
+        _lib.check(lib.rsvio_build_pyramids_d(ctx, d_imgs.data_ptr(), 10, d_pyr.data_ptr(), None))
+        torch.cuda.synchronize()
+        pyr = d_pyr.cpu().numpy()
+        for i in range(10):
+            assert np.array_equal(pyr[i], oracle.build_pyramid(imgs[i], L)), i
+        sizes = [300, 257, 300, 1, 0, 300, 300, 300, 120, 64, 300, 299]
+        specs, keep, ref = [], [], []
+        for s in range(4):
+            t = s % 3
+            a0 = S.track_features(frames[t][0], 300)
+            a1 = S.stereo_shift(a0)
+            jobs = [(2 * t, 2 * t + 2, a0), (2 * t + 1, 2 * t + 3, a1), (2 * t + 2, 2 * t + 3, a0)]
+            for j, (i0, i1, a) in enumerate(jobs):
+                n = sizes[3 * s + j]
+                a = np.ascontiguousarray(a[:n])
+                da = torch.from_numpy(a).to(dev) if n else torch.zeros((1, 6), device=dev)
+                do = torch.full((max(n, 1), 6), -7.0, device=dev)
+                dv = torch.full((max(n, 1),), 9, dtype=torch.uint8, device=dev)
+                keep += [da, do, dv]
+                specs.append((d_pyr[i0].data_ptr(), d_pyr[i1].data_ptr(), da.data_ptr(), do.data_ptr(),
+                              dv.data_ptr(), n))
+                ref.append((i0, i1, a, do, dv))
+        table, start, total = _batch_table(_lib, specs, dev)
+        assert total == sum(sizes)
+        _lib.check(lib.rsvio_track_points_table_d(ctx, table.data_ptr(), start.data_ptr(), len(specs), total,
+                                                  20, C.c_float(0.01), None))
+        torch.cuda.synchronize()
+        oracle.set_trig_mode(1)
+        try:
+            for i0, i1, a, do, dv in ref:
+                if len(a) == 0:
+                    assert float(do[0, 0]) == -7.0 and int(dv[0]) == 9  # empty batch untouched
+                    continue
+                ra, rv = oracle.track_points(pyr[i0], pyr[i1], w, h, L, a)
+                gv = dv[:len(a)].cpu().numpy().astype(bool)
+                ga = do[:len(a)].cpu().numpy()
+                assert np.array_equal(gv, rv)
+                assert np.array_equal(ga.view(np.uint32), ra.view(np.uint32))
+        finally:
+            oracle.set_trig_mode(0)
+        # zero batches / zero total are no-ops; bad arguments are rejected
+        assert lib.rsvio_track_points_table_d(ctx, None, None, 0, 0, 20, C.c_float(0.01), None) == 0
+        assert lib.rsvio_track_points_table_d(ctx, None, None, 3, 10, 20, C.c_float(0.01), None) < 0
+    finally:
+        lib.rsvio_track_ctx_destroy(ctx)
