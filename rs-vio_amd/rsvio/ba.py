@@ -200,6 +200,7 @@ class SlidingWindow:
         self.map_version = 0                           # bumped whenever map_points is replaced
         self.solver = solver or BundleAdjuster(max_keyframes=max(max_frames, 2), device=device)
         self.last_result = None
+        self._pending = None                           # landmark ids of a solve in flight (optimize_async)
 
     def add_frame(self, frame: Frame) -> bool:
         if not frame.is_keyframe:
@@ -285,6 +286,10 @@ class SlidingWindow:
             self.last_result = None
             return False
         pose, pw, res = self.solver.solve(pose7, fixed, p_init, lm, kf, cam, uv, tcb, cfg)
+        return self._apply(ids, pose, pw, res)
+
+    def _apply(self, ids, pose, pw, res) -> bool:
+        """process_optimization_result (sliding_window.rs:418-486)."""
         self.last_result = res
         if res.status <= 0:
             return False  # revert: nothing was modified
@@ -294,3 +299,35 @@ class SlidingWindow:
         for i, f in enumerate(self.keyframes):
             f.T_W_B = np.linalg.inv(_T_from_pose7(pose[i]))
         return True
+
+    def optimize_async(self, cfg=None):
+        """optimize() in two halves: assemble the problem, enqueue the solve on the device
+        (rsvio_ba_run_async) and return None; finish() waits and applies the result.  The window
+        must not be read or changed in between (the Estimator calls finish() before its next use
+        of the window, so the result is the same as optimize()'s).  Returns optimize()'s bool when
+        nothing was enqueued (guards, or a solver without an asynchronous path)."""
+        self.finish()
+        if not self.keyframes:
+            raise RuntimeError("Window is empty")
+        if len(self.keyframes) < self.max_frames:
+            raise RuntimeError("Need more keyframes")
+        if not hasattr(self.solver, "run_async"):
+            return self.optimize(cfg)
+        pose7, fixed, p_init, lm, kf, cam, uv, tcb, ids = self.build_problem()
+        num_vars = len(self.keyframes) + len(p_init)
+        if len(lm) < 6 or len(lm) < num_vars:
+            self.last_result = None
+            return False
+        self.solver.set_problem(pose7, fixed, p_init, lm, kf, cam, uv, tcb)
+        self.solver.run_async(cfg)
+        self._pending = ids
+        return None
+
+    def finish(self):
+        """Complete a solve started by optimize_async (no-op otherwise); returns its bool."""
+        if self._pending is None:
+            return None
+        ids, self._pending = self._pending, None
+        res = self.solver.wait()
+        pose, pw = self.solver.state()
+        return self._apply(ids, pose, pw, res)

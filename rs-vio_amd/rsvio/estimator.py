@@ -78,7 +78,7 @@ class Estimator:
     def __init__(self, width: int, height: int, cameras, T_B_Cl, T_B_Cr, levels: int = 6, grid_size: int = 50,
                  max_iterations: int = 20, thresh: float = 0.01, window: int = 10,
                  translation_threshold: float = 0.05, rotation_threshold: float = 0.05, device: int = 0,
-                 backend=None):
+                 backend=None, pipelined: bool = False):
         self.backend = backend or DeviceBackend(width, height, cameras, levels, grid_size, max_iterations, thresh,
                                                 window, translation_threshold, rotation_threshold, device)
         self.window = SlidingWindow(window, device, solver=self.backend.solver)
@@ -86,6 +86,22 @@ class Estimator:
         self.T_B_Cr = np.asarray(T_B_Cr, np.float64)
         self.frame_id = 0
         self._map_key = None
+        # pipelined: a keyframe's BA solve runs on the device while the next frame is tracked
+        # (the tracker never reads the window); its result is applied before the window is next
+        # read, so every output equals the sequential order's.  The keyframe's FrameResult gets
+        # its ba_status at that point (or at flush()).
+        self.pipelined = pipelined
+        self._pending_frame = None
+
+    def flush(self):
+        """Complete an in-flight BA solve (pipelined mode) and fill its frame's ba_status."""
+        if self._pending_frame is not None:
+            self.window.finish()
+            r = self.window.last_result
+            out, frame = self._pending_frame
+            out.ba_status = None if r is None else int(r.status)
+            out.T_W_B = frame.T_W_B.copy()  # the solve refined this keyframe's pose too
+            self._pending_frame = None
 
     def _T_C_B2(self):
         # extrinsics of the front keyframe (sliding_window.rs:519-520); the rig is fixed here
@@ -98,6 +114,7 @@ class Estimator:
         frame = Frame(frame_id=self.frame_id, T_W_B=np.eye(4), T_B_Cl=self.T_B_Cl, T_B_Cr=self.T_B_Cr,
                       is_keyframe=True, left_features=(ids_l, uv_l), right_features=(ids_r, uv_r))
         pnp_status = None
+        self.flush()
         if self.window.is_full():
             if self.window.map_version != self._map_key:  # map_points changes only in optimize
                 mp = self.window.map_points
@@ -110,19 +127,28 @@ class Estimator:
                 frame.T_W_B = T_W_B
                 frame.is_keyframe = bool(is_kf)
         ba_status = None
+        pending = False
         if frame.is_keyframe:
             self.window.add_frame(frame)
             if self.window.is_full():
-                self.window.optimize()
-                r = self.window.last_result
-                ba_status = None if r is None else int(r.status)
-        return FrameResult(self.frame_id, frame.is_keyframe, frame.T_W_B.copy(), len(ids_l), len(ids_r),
-                           pnp_status, ba_status)
+                if self.pipelined and self.window.optimize_async() is None:
+                    pending = True
+                else:
+                    self.window.optimize()
+                    r = self.window.last_result
+                    ba_status = None if r is None else int(r.status)
+        out = FrameResult(self.frame_id, frame.is_keyframe, frame.T_W_B.copy(), len(ids_l), len(ids_r),
+                          pnp_status, ba_status)
+        if pending:
+            self._pending_frame = (out, frame)
+        return out
 
     def trajectory(self):
         """T_W_B of the keyframes in the window."""
+        self.flush()
         return self.window.get_keyframe_poses()
 
     def close(self):
+        self.flush()
         if hasattr(self.backend, "close"):
             self.backend.close()

@@ -115,3 +115,64 @@ def test_estimator_oracle_pipeline(oracle, scene_stream):
     assert all(r.ba_status > 0 for r in tracked if r.is_keyframe)
     err = [np.linalg.norm(r.T_W_B[:3, 3] - T[:3, 3]) for r, T in zip(tracked, s.T_W_B[win:])]
     assert max(err) < 0.01
+
+
+class _DeferredSolver:
+    """The oracle solver behind the asynchronous interface SlidingWindow.optimize_async uses
+    (set_problem / run_async / wait / state); the solve happens at wait()."""
+
+    def __init__(self, solver):
+        self.s = solver
+        self.in_flight = 0
+
+    def solve(self, *a, **k):
+        return self.s.solve(*a, **k)
+
+    def set_problem(self, *a):
+        assert self.in_flight == 0
+        self.args = a
+
+    def run_async(self, cfg=None):
+        self.cfg, self.in_flight = cfg, 1
+
+    def wait(self):
+        assert self.in_flight == 1
+        self.in_flight = 0
+        self.pose, self.pw, res = self.s.solve(*self.args, self.cfg)
+        return res
+
+    def state(self):
+        return self.pose, self.pw
+
+
+def test_estimator_pipelined_equals_sequential(oracle, scene_stream):
+    """Pipelined mode (a keyframe's BA completes during the next frame's tracking): every frame
+    result (after flush), the trajectory and the map equal the sequential order's exactly."""
+    from oracle.estimator import OracleBackend
+    from rsvio.camera import Camera
+    from rsvio.estimator import Estimator
+    s, win = scene_stream
+    cams = [Camera.opencv5(*p) for p in s.intrinsics]
+    h, w = s.frames[0][0].shape
+    seq = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=OracleBackend(oracle, w, h, cams))
+    be = OracleBackend(oracle, w, h, cams)
+    be.solver = _DeferredSolver(be.solver)
+    pip = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=be, pipelined=True)
+    a = [seq.process_frame(l, r) for l, r in s.frames]
+    b = []
+    deferred = 0
+    for l, r in s.frames:
+        b.append(pip.process_frame(l, r))
+        deferred += be.solver.in_flight
+        if b[-1].is_keyframe and len(pip.window) == win:
+            assert b[-1].ba_status is None or be.solver.in_flight == 0
+    pip.flush()
+    assert deferred > 0
+    for x, y in zip(a, b):
+        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right) == \
+               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right)
+        assert np.array_equal(x.T_W_B, y.T_W_B)
+    for Ta, Tb in zip(seq.trajectory(), pip.trajectory()):
+        assert np.array_equal(Ta, Tb)
+    ma, mb = seq.window.map_points, pip.window.map_points
+    assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)

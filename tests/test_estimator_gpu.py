@@ -65,3 +65,30 @@ def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
         dev.be.close()
     finally:
         oracle.set_trig_mode(0)
+
+
+def test_estimator_pipelined_matches_sequential(gpu, scene_stream):
+    """Pipelined mode on the device (the BA solve on its stream overlaps the next frame's
+    tracking): frame results, trajectory and map bit-identical to the sequential order."""
+    from rsvio.camera import Camera
+    from rsvio.estimator import DeviceBackend, Estimator
+    s, win = scene_stream
+    h, w = s.frames[0][0].shape
+    cams = [Camera.opencv5(*p) for p in s.intrinsics]
+    res, ests = [], []
+    for pipelined in (False, True):
+        be = DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0)
+        est = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=be, pipelined=pipelined)
+        res.append([est.process_frame(l, r) for l, r in s.frames])
+        est.flush()
+        ests.append(est)
+    for x, y in zip(*res):
+        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right) == \
+               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right)
+        assert np.array_equal(x.T_W_B, y.T_W_B)
+    for Ta, Tb in zip(ests[0].trajectory(), ests[1].trajectory()):
+        assert np.array_equal(Ta, Tb)
+    ma, mb = ests[0].window.map_points, ests[1].window.map_points
+    assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
+    for e in ests:
+        e.close()
