@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 #include <stdexcept>
 #include <vector>
@@ -1526,16 +1527,27 @@ struct BundleAdjuster {
     static void grow(DevBuf<T>& b, size_t n) {
         if (b.n < n) b.alloc(std::max<size_t>(n, 1));
     }
-    template <class T>
-    void up(DevBuf<T>& b, const std::vector<T>& v) {
-        grow(b, v.size());
-        if (!v.empty()) RSVIO_HIP(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
-    }
+    // set_problem's uploads go through one pinned staging buffer (sized per problem), so each is a
+    // real asynchronous DMA instead of a pageable copy the host waits for
+    HostBuf<uint8_t> h_stage;
+    size_t stage_off = 0;
+    static size_t stage_bytes(size_t bytes) { return (bytes + 255) & ~(size_t)255; }
     template <class T>
     void up(DevBuf<T>& b, const T* src, size_t n) {
         grow(b, n);
-        if (n) RSVIO_HIP(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, stream));
+        if (!n) return;
+        const size_t bytes = n * sizeof(T);
+        if (stage_off + bytes <= h_stage.n) {
+            uint8_t* dst = h_stage.p + stage_off;
+            std::memcpy(dst, static_cast<const void*>(src), bytes);
+            stage_off += stage_bytes(bytes);
+            RSVIO_HIP(hipMemcpyAsync(b.p, dst, bytes, hipMemcpyHostToDevice, stream));
+        } else {
+            RSVIO_HIP(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
+        }
     }
+    template <class T>
+    void up(DevBuf<T>& b, const std::vector<T>& v) { up(b, v.data(), v.size()); }
 
     Prob prob() const {
         Prob p;
@@ -1676,6 +1688,17 @@ struct BundleAdjuster {
                 pbv.push_back(pslot[pr.second]);
                 pl.push_back(slot_lm[pr.first]);
             }
+        }
+        {
+            // every DMA of the previous set_problem finished (it ends with a stream sync) and no
+            // kernel reads the stage, so it can be refilled (or regrown) now
+            size_t need = stage_bytes(sizeof(double) * 7 * (size_t)n_kf) + stage_bytes(sizeof(double) * 3 * (size_t)n_lm);
+            for (size_t b : {free_idx.size(), hdr.size(), chunk_pb.size(), chunk_pair.size(), pb_chunk.size(), pa.size(),
+                             pbv.size(), pl.size(), pb_fa.size(), pb_fb.size()})
+                need += stage_bytes(sizeof(int) * b);
+            need += stage_bytes(sizeof(double) * huv.size());
+            if (h_stage.n < need) h_stage.alloc(need + need / 2);
+            stage_off = 0;
         }
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = (int)chunk_pb.size();
