@@ -23,6 +23,7 @@ namespace {
 RSVIO_DBG_DECL
 
 constexpr int NP = 52;
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dispatched round-robin
 
 // patch.rs:19-72 -- the 52-point pattern (pixel offsets before the 1/2 scale of :126)
 __constant__ int8_t kPattern[64][2] = {
@@ -342,7 +343,11 @@ __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, 
 }
 
 __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
-    const int job = blockIdx.x;
+    // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of jobs (whole
+    // batches, i.e. 2 of the 4 pyramids) so its L2 fetches only what its features read
+    const int per = (L.njobs + kXcds - 1) / kXcds;
+    const int job = (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
+    if (job >= L.njobs) return;
     const uint8_t* pyr0;
     const uint8_t* pyr1;
     const float* ain;
@@ -407,10 +412,13 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
 
 RSVIO_DBG_READER(rsvio_dbg_lk_stamps)
 
-void enqueue_track(const TrackLaunch& L, hipStream_t s) {
+void enqueue_track(const TrackLaunch& L0, hipStream_t s) {
+    TrackLaunch L = L0;
     const int total = L.table != nullptr ? L.start[0] : L.start[L.nb];
     if (total <= 0) return;
-    hipLaunchKernelGGL(lk_track_kernel, dim3(total), dim3(64), 0, s, L);
+    L.njobs = total;
+    const int grid = ((total + kXcds - 1) / kXcds) * kXcds;
+    hipLaunchKernelGGL(lk_track_kernel, dim3(grid), dim3(64), 0, s, L);
     RSVIO_HIP(hipGetLastError());
 }
 

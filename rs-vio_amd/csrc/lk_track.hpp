@@ -25,6 +25,7 @@ struct TrackLaunch {
     // prefix of their sizes come from device memory and nb may exceed kMaxTrackBatches
     const rsvio_track_batch* table;
     const int32_t* tstart;
+    int njobs;  // set by enqueue_track: jobs in this launch
 };
 
 void enqueue_track(const TrackLaunch& L, hipStream_t s);
