@@ -225,8 +225,8 @@ class SlidingWindow:
         appearance; initial point from map_points (f32) or the depth-2.0 ray of its first
         observation (sliding_window.rs:248-272).  Vectorised over the window's observations."""
         kfs = list(self.keyframes)
-        T_Cl_B = np.linalg.inv(kfs[0].T_B_Cl)
-        T_Cr_B = np.linalg.inv(kfs[0].T_B_Cr)
+        # stacked inversions (numpy inverts each matrix exactly as a single call would)
+        T_Cl_B, T_Cr_B = np.linalg.inv(np.stack([kfs[0].T_B_Cl, kfs[0].T_B_Cr]))
         ids, uv, kf, cam = [], [], [], []
         for i, f in enumerate(kfs):
             for c, feats in enumerate((f.left_features, f.right_features)):
@@ -256,16 +256,19 @@ class SlidingWindow:
             in_map = mid[pos] == lm_ids
             p_init[in_map] = mpw[pos[in_map]]
         fo = first[order]                                  # first observation of each landmark
-        T_B_C = (np.linalg.inv(T_Cl_B), np.linalg.inv(T_Cr_B))
-        for j in np.nonzero(~in_map)[0]:
-            o = fo[j]
-            f = kfs[kf[o]]
-            Tbc = T_B_C[cam[o]]
-            p_C = np.array([uv[o, 0], uv[o, 1], 2.0])
-            p_init[j] = f.T_W_B[:3, :3] @ (Tbc[:3, :3] @ p_C + Tbc[:3, 3]) + f.T_W_B[:3, 3]
+        T_B_C = np.linalg.inv(np.stack([T_Cl_B, T_Cr_B]))
+        T_W_B = np.stack([f.T_W_B for f in kfs])
+        new = np.nonzero(~in_map)[0]
+        if len(new):
+            # p_W = T_W_B (T_B_C (u, v, 2.0)) of the first observation, batched (same per-row bits
+            # as the 3x3 @ 3 products of a per-landmark loop)
+            o = fo[new]
+            Tbc, Twb = T_B_C[cam[o]], T_W_B[kf[o]]
+            p_C = np.stack([uv[o, 0], uv[o, 1], np.full(len(o), 2.0)], 1)
+            p_B = np.matmul(Tbc[:, :3, :3], p_C[:, :, None])[:, :, 0] + Tbc[:, :3, 3]
+            p_init[new] = np.matmul(Twb[:, :3, :3], p_B[:, :, None])[:, :, 0] + Twb[:, :3, 3]
         pose7 = np.zeros((len(kfs), 7))
-        for i, f in enumerate(kfs):
-            T_B_W = np.linalg.inv(f.T_W_B)
+        for i, T_B_W in enumerate(np.linalg.inv(T_W_B)):
             pose7[i, :3] = T_B_W[:3, 3]
             pose7[i, 3:] = _quat_from_rot(T_B_W[:3, :3])
         kf_fixed = np.zeros(len(kfs), np.uint8)
@@ -296,8 +299,9 @@ class SlidingWindow:
         pw32 = pw.astype(np.float32)
         self.map_points = dict(zip(ids, pw32))
         self.map_version += 1
-        for i, f in enumerate(self.keyframes):
-            f.T_W_B = np.linalg.inv(_T_from_pose7(pose[i]))
+        T_W_B = np.linalg.inv(np.stack([_T_from_pose7(pose[i]) for i in range(len(self.keyframes))]))
+        for f, T in zip(self.keyframes, T_W_B):
+            f.T_W_B = T
         return True
 
     def optimize_async(self, cfg=None):

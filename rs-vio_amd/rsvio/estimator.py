@@ -86,6 +86,7 @@ class Estimator:
         self.T_B_Cr = np.asarray(T_B_Cr, np.float64)
         self.frame_id = 0
         self._map_key = None
+        self._tcb_key = None
         # pipelined: a keyframe's BA solve runs on the device while the next frame is tracked
         # (the tracker never reads the window); its result is applied before the window is next
         # read, so every output equals the sequential order's.  The keyframe's FrameResult gets
@@ -106,7 +107,11 @@ class Estimator:
     def _T_C_B2(self):
         # extrinsics of the front keyframe (sliding_window.rs:519-520); the rig is fixed here
         front = self.window.keyframes[0]
-        return np.stack([np.linalg.inv(front.T_B_Cl).reshape(16), np.linalg.inv(front.T_B_Cr).reshape(16)])
+        key = front.T_B_Cl.tobytes() + front.T_B_Cr.tobytes()
+        if self._tcb_key != key:   # the rig's extrinsics: inverted once, not per frame
+            self._tcb = np.linalg.inv(np.stack([front.T_B_Cl, front.T_B_Cr])).reshape(2, 16)
+            self._tcb_key = key
+        return self._tcb
 
     def process_frame(self, left: np.ndarray, right: np.ndarray) -> FrameResult:
         self.frame_id += 1
