@@ -377,6 +377,7 @@ struct Tracker {
     CamPair cams{};                 // T12 unprojection fused into append_pack_kernel when on
     DevBuf<float2> undist;          // 2 x cap
     HostBuf<float2> h_undist;       // last process_frame's undistorted coordinates
+    HostBuf<rsvio_feature> h_out;   // pinned staging of both packed feature lists (2 x cap)
     size_t last_n[2] = {0, 0};
 
     uint8_t* pyr(int slot, int cam) { return d_pyr.p + (size_t)(2 * slot + cam) * pyr_bytes; }
@@ -414,6 +415,7 @@ struct Tracker {
         last_id.alloc(1);
         out.alloc((size_t)2 * cap);
         h_counts.alloc(4);
+        h_out.alloc((size_t)2 * cap);
         RSVIO_HIP(hipMemsetAsync(counts.p, 0, sizeof(int) * 2, stream));
         RSVIO_HIP(hipMemsetAsync(last_id.p, 0, sizeof(unsigned long long), stream));
         RSVIO_HIP(hipMemsetAsync(overflow.p, 0, sizeof(int), stream));
@@ -477,22 +479,40 @@ struct Tracker {
         has_prev = true;
     }
 
+    // Counts, overflow flag and both feature lists (+ undistorted coordinates) in ONE round trip:
+    // the lists are copied up to a host-known bound into pinned staging -- a camera's list is its
+    // previous survivors plus at most one new point per grid cell (feature_tracker.rs:143-170) --
+    // and a second copy covers any excess (never expected).
+    void copy_lists(size_t l0, size_t l1, size_t r0, size_t r1) {
+        if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_out.p + l0, out.p + l0, (l1 - l0) * sizeof(rsvio_feature),
+                                              hipMemcpyDeviceToHost, stream));
+        if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_out.p + cap + r0, out.p + cap + r0, (r1 - r0) * sizeof(rsvio_feature),
+                                              hipMemcpyDeviceToHost, stream));
+        if (cams.on) {
+            if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + l0, undist.p + l0, (l1 - l0) * sizeof(float2),
+                                                  hipMemcpyDeviceToHost, stream));
+            if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap + r0, undist.p + cap + r0,
+                                                  (r1 - r0) * sizeof(float2), hipMemcpyDeviceToHost, stream));
+        }
+    }
+
     void fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
+        const size_t bl = std::min((size_t)cap, (size_t)host_count[0] + (size_t)n_cells);
+        const size_t br = std::min((size_t)cap, (size_t)host_count[1] + (size_t)n_cells);
         RSVIO_HIP(hipMemcpyAsync(h_counts.p, counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipMemcpyAsync(h_counts.p + 2, overflow.p, sizeof(int), hipMemcpyDeviceToHost, stream));
+        copy_lists(0, bl, 0, br);
         RSVIO_HIP(hipStreamSynchronize(stream));
         host_count[0] = h_counts.p[0];
         host_count[1] = h_counts.p[1];
-        const size_t nl = std::min((size_t)host_count[0], cap_l), nr = std::min((size_t)host_count[1], cap_r);
-        if (nl) RSVIO_HIP(hipMemcpyAsync(out_l, out.p, nl * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
-        if (nr) RSVIO_HIP(hipMemcpyAsync(out_r, out.p + cap, nr * sizeof(rsvio_feature), hipMemcpyDeviceToHost, stream));
-        if (cams.on) {
-            if (nl) RSVIO_HIP(hipMemcpyAsync(h_undist.p, undist.p, nl * sizeof(float2), hipMemcpyDeviceToHost, stream));
-            if (nr)
-                RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap, undist.p + cap, nr * sizeof(float2), hipMemcpyDeviceToHost,
-                                         stream));
+        const size_t ml = std::min((size_t)host_count[0], (size_t)cap), mr = std::min((size_t)host_count[1], (size_t)cap);
+        if (ml > bl || mr > br) {
+            copy_lists(bl, std::max(ml, bl), br, std::max(mr, br));
+            RSVIO_HIP(hipStreamSynchronize(stream));
         }
-        RSVIO_HIP(hipStreamSynchronize(stream));
+        const size_t nl = std::min(ml, cap_l), nr = std::min(mr, cap_r);
+        if (nl) std::memcpy(out_l, h_out.p, nl * sizeof(rsvio_feature));
+        if (nr) std::memcpy(out_r, h_out.p + cap, nr * sizeof(rsvio_feature));
         last_n[0] = cams.on ? nl : 0;
         last_n[1] = cams.on ? nr : 0;
         *n_l = nl;
