@@ -237,7 +237,11 @@ __device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P,
 #pragma unroll
     for (int i = 0; i < 6; ++i) L.gc[i] = 0.0;
     L.cost = 0.0;
-    for (int o = 0; o < nobs; ++o) {
+    // unrolled over the <= 2 observations of a slot: a runtime-indexed uvq[o] was lowered to a
+    // scratch-memory array (a store + reload on the linearisation's critical path)
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+        if (o >= nobs) break;
         double r[2], J[2][9];
         const double uv[2] = {uvq[o].x, uvq[o].y};
         linearize(p, P, G.TCB[(cams >> o) & 1].m, uv, r, J, true);

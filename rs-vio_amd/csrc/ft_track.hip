@@ -153,12 +153,15 @@ __device__ __forceinline__ void chains(const float (&v)[N], const float (&init)[
                                        int lane) {
 #pragma unroll
     for (int i = 0; i < N; ++i) sh[i * kLd + lane] = v[i];
+    // chain i's start value rides in its row's padding column 64 (a per-lane select of init[]
+    // was lowered to a scratch-memory array index, a spill round trip on every chain)
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) sh[i * kLd + 64] = init[i];
+    }
     __builtin_amdgcn_wave_barrier();
     const int c = lane < N ? lane : 0;
-    float acc = init[0];
-#pragma unroll
-    for (int i = 1; i < N; ++i)
-        if (c == i) acc = init[i];
+    float acc = sh[c * kLd + 64];
     const float4* row = reinterpret_cast<const float4*>(sh + c * kLd);
 #pragma unroll
     for (int q = 0; q < NP / 4; ++q) {

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
         }
         const rsvio_track_batch& d = L.table[lo];
         idx = job - L.tstart[lo];
-        if (idx >= d.n) return;
+        if (idx < 0 || idx >= d.n) return;  // a malformed caller prefix never indexes out of a batch
         pyr0 = d.d_pyr0; pyr1 = d.d_pyr1; ain = d.d_aff_in; aout = d.d_aff_out; valid = d.d_valid;
     } else {
         int b = 0;
