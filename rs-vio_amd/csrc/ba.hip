@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
@@ -1485,6 +1486,58 @@ struct BundleAdjuster {
     bool has_problem = false;
     bool fuse_combine = true;  // single rank: K4d folded into K4c
     int iter_chunk = 2;       // LM iterations enqueued per status read-back after the first chunk
+    // Single rank: the start of a solve (K0 + K4 + the first chunk of k LM iterations, ~17
+    // kernels) captured once as a HIP graph and replayed by one hipGraphLaunch -- the host
+    // enqueue drops from ~80 us to a few us.  Keyed by k and the LM configuration; dropped when
+    // set_problem may have moved buffers.  Any capture failure falls back to direct launches.
+    hipGraphExec_t gexec = nullptr;
+    int g_k = -1;
+    rsvio_lm_cfg g_cfg{};
+    bool graphs_ok = true;
+    void drop_graph() {
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        gexec = nullptr;
+        g_k = -1;
+    }
+    static bool same_cfg(const rsvio_lm_cfg& a, const rsvio_lm_cfg& b) {
+        return a.max_iterations == b.max_iterations && a.cost_tolerance == b.cost_tolerance &&
+               a.parameter_tolerance == b.parameter_tolerance && a.huber_delta == b.huber_delta &&
+               a.lambda_init == b.lambda_init;
+    }
+    bool start_graph(const rsvio_lm_cfg& cfg, int k) {
+        if (sharded() || !graphs_ok) return false;
+        if (!(gexec && g_k == k && same_cfg(g_cfg, cfg))) {
+            drop_graph();
+            if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                (void)hipGetLastError();
+                graphs_ok = false;
+                return false;
+            }
+            bool ok = true;
+            try {
+                enqueue_start(cfg.lambda_init);
+                for (int i = 0; i < k; ++i) enqueue_iteration(cfg);
+            } catch (...) {
+                ok = false;
+            }
+            hipGraph_t g = nullptr;
+            if (hipStreamEndCapture(stream, &g) != hipSuccess) ok = false;
+            if (ok && hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+                gexec = nullptr;
+                ok = false;
+            }
+            if (g) (void)hipGraphDestroy(g);
+            if (!ok) {
+                (void)hipGetLastError();
+                graphs_ok = false;
+                return false;
+            }
+            g_k = k;
+            g_cfg = cfg;
+        }
+        RSVIO_HIP(hipGraphLaunch(gexec, stream));
+        return true;
+    }
     int last_iterations = 3;  // first chunk = previous solve's iteration count
     DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_slot_uv;
     DevBuf<int> d_slot_hdr;
@@ -1516,8 +1569,11 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
         h_state.alloc(1);
+        const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
+        graphs_ok = !(ge && ge[0] == '0');
     }
     ~BundleAdjuster() {
+        drop_graph();
         if (comm) ncclCommDestroy(comm);
         for (int r = 0; r < kP2PMax; ++r)
             if (p2p_opened[r]) (void)hipIpcCloseMemHandle(p2p.peer[r]);
@@ -1579,6 +1635,7 @@ struct BundleAdjuster {
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
+        drop_graph();  // kernel arguments (sizes, buffers) change with the problem
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
             throw std::invalid_argument("problem exceeds the handle's capacities");
@@ -1855,8 +1912,15 @@ struct BundleAdjuster {
         }
         pend.max_it = std::max(cfg.max_iterations, 1);
         RSVIO_HIP(hipEventRecord(ev0, stream));
-        enqueue_start(cfg.lambda_init);
-        enqueue_chunk(std::min(std::max(last_iterations, 1), pend.max_it));
+        const int k = std::min(std::max(last_iterations, 1), pend.max_it);
+        if (start_graph(cfg, k)) {
+            pend.enq += k;
+            RSVIO_HIP(hipEventRecord(ev1, stream));
+            RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+        } else {
+            enqueue_start(cfg.lambda_init);
+            enqueue_chunk(k);
+        }
     }
 
     void finish(rsvio_ba_result* res) {
