@@ -327,10 +327,34 @@ __device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda
 // K4: linearisation of the initial state (buffer 0) -- one wave per landmark group, one lane
 // per (landmark, keyframe) slot.  Its cost partials (partA) give the initial cost.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk) {
+// with_reset: K0 folded in (one kernel boundary less per solve): the grid also copies the
+// initial state into both state buffers and initialises the LM state; the linearisation reads
+// the initial state directly (the same values K0 copies).
+__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk, int with_reset, double lambda0) {
     __shared__ double sh[10][64];
     const int w = blockIdx.x, lane = threadIdx.x;
     const int s = 64 * w + lane;
+    if (with_reset) {
+        const int nt = (int)gridDim.x * 64;
+        for (int i = s; i < 7 * G.n_kf; i += nt) {
+            Wk.pose[0][i] = Wk.pose_init[i];
+            Wk.pose[1][i] = Wk.pose_init[i];
+        }
+        for (int i = s; i < 3 * G.n_lm; i += nt) {
+            Wk.pw[0][i] = Wk.pw_init[i];
+            Wk.pw[1][i] = Wk.pw_init[i];
+        }
+        for (int i = s; i < G.n_pb + 1; i += nt) Wk.cnt[i] = 0;
+        if (s == 0) {
+            *Wk.singular = 0;
+            LmState st{};
+            st.lambda = lambda0;
+            st.nu = 2.0;
+            *Wk.st = st;
+        }
+    }
+    const double* pose0 = with_reset ? Wk.pose_init : Wk.pose[0];
+    const double* pw0 = with_reset ? Wk.pw_init : Wk.pw[0];
     const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
     const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
     STAMP(11);
@@ -339,8 +363,8 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk)
     const bool fr = h1.x >= 0;
     SlotLin L;
     if (act) {
-        const Pose P = pose_from7(Wk.pose[0] + 7 * kf);
-        const double* pwp = Wk.pw[0] + 3 * l;
+        const Pose P = pose_from7(pose0 + 7 * kf);
+        const double* pwp = pw0 + 3 * l;
         const double p[3] = {pwp[0], pwp[1], pwp[2]};
         slot_linearize(G, P, p, h1.y, h1.z, uvq, fr, L);
     } else {
@@ -1818,8 +1842,10 @@ struct BundleAdjuster {
 
     // K0 + K4: initial state and its linearisation (buffer 0)
     void enqueue_start(double lambda0) {
-        enqueue_reset(lambda0);
-        if (G.n_wave) hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work());
+        if (G.n_wave)  // K0 folded into K4
+            hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work(), 1, lambda0);
+        else
+            enqueue_reset(lambda0);
         RSVIO_HIP(hipGetLastError());
     }
 
