@@ -205,7 +205,7 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[0][i] = Wk.pw_init[i];
         Wk.pw[1][i] = Wk.pw_init[i];
     }
-    if (i < G.n_pb + 1) Wk.cnt[i] = 0;
+    if (i < G.n_pb + 3) Wk.cnt[i] = 0;
     if (i == 0) {
         *Wk.singular = 0;
         LmState s{};
@@ -274,6 +274,14 @@ __device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P,
 // Store one wave's linearisation into raw buffer `buf`: the slot records (free keyframes), then
 // the landmark sums V, g_p in slot order by each landmark's first lane.  Called by the whole
 // wave (contains barriers); sh is a [10][64] LDS scratch.
+// intra-wave LDS hand-off (a wave's LDS operations execute in order; this keeps the compiler
+// from moving them across)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool WAVE = false>
 __device__ void store_linearization(const Work& Wk, int buf, int s, int lane, bool act, bool fr, int first, int nk,
                                     int l, const SlotLin& L, double (*sh)[64]) {
     if (act && fr) {
@@ -293,7 +301,7 @@ __device__ void store_linearization(const Work& Wk, int buf, int s, int lane, bo
     for (int i = 0; i < 6; ++i) sh[i][lane] = L.V[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) sh[6 + i][lane] = L.gp[i];
-    __syncthreads();
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
     if (act && lane == first) {  // landmark sums in slot order
         double Vl[6] = {0, 0, 0, 0, 0, 0}, gl[3] = {0, 0, 0};
         for (int k = 0; k < nk; ++k) {
@@ -344,7 +352,7 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk,
             Wk.pw[0][i] = Wk.pw_init[i];
             Wk.pw[1][i] = Wk.pw_init[i];
         }
-        for (int i = s; i < G.n_pb + 1; i += nt) Wk.cnt[i] = 0;
+        for (int i = s; i < G.n_pb + 3; i += nt) Wk.cnt[i] = 0;
         if (s == 0) {
             *Wk.singular = 0;
             LmState st{};
@@ -410,6 +418,7 @@ __device__ double block_ordered_sum(const double* __restrict__ v, int n, int str
 __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, int fused) {
     __shared__ double sh[kBlockF * 65];
     const int c = blockIdx.x, lane = threadIdx.x;
+    if (fused && c == 0 && lane == 0) Wk.cnt[G.n_pb + 1] = 0;  // the K5 flag of this iteration's K5+K6
     if (c == G.n_chunk) {  // fused: the initial cost of this rank for the first decision
         if (Wk.st->done) return;
         const int SC0 = G.n_pb * 36 + 12 * G.n_free;
@@ -815,10 +824,13 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
 }
 
 template <int NF>
-__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
+constexpr size_t k5_lds_doubles() { return 128 + 2 * 6 * NF * kLcLd; }
+
+// K5 body (one 256-thread block); A: k5_lds_doubles<NF>() of LDS.  Every write of its results
+// (dc, trial poses, st->solve_ok/dc2/gcdc) is made by wave 0.
+template <int NF>
+__device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, double* A) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
-    // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
-    __shared__ __attribute__((aligned(16))) double A[128 + 2 * 6 * NF * kLcLd];
     __shared__ int badw[4];
     __shared__ int progress;
     __shared__ int fail;
@@ -860,6 +872,13 @@ __global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work
         camera_solve_w4<NF>(G, Pr, Wk, A, badw, &progress, n, tid, p7, fidx);
         return;
     }
+}
+
+template <int NF>
+__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
+    // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
+    __shared__ __attribute__((aligned(16))) double A[k5_lds_doubles<NF>()];
+    k5_body<NF>(G, Pr, Wk, A);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1288,19 +1307,20 @@ __device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk
 // the trial cost).  Accepted: the next iteration starts from that linearisation; rejected:
 // from the current one, untouched.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr, Work Wk, int fuse_decide,
-                                                             LmArgs la) {
-    __shared__ double sh[10][64];     // W_s^T dc_f per slot; then the linearisation scratch
-    __shared__ double shp[3][64];     // trial point at the landmark's first lane
-    __shared__ double shs[4][64];     // per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
-    const int w = blockIdx.x, lane = threadIdx.x;
+// FUSED: one wave of a ba_solve_backsub block; its inputs from K5 (dc, trial poses, st) are
+// awaited on the K5 flag (agent-scope acquire) instead of a kernel boundary.
+template <bool FUSED>
+__device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int fuse_decide, const LmArgs& la, int w,
+                        int lane, double (*sh)[64], double (*shp)[64], double (*shs)[64]) {
+    // sh: W_s^T dc_f per slot, then the linearisation scratch; shp: trial point at the
+    // landmark's first lane; shs: per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int s = 64 * w + lane;
     const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
     const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
     const LmState* st = Wk.st;
     if (st->done) return;
     if (!st->solve_ok) {  // no step: the decision (lambda up) is all there is
-        if (fuse_decide && blockIdx.x == 0) lm_decide_wave(G, Pr, Wk, 0, la);
+        if (fuse_decide && w == 0) lm_decide_wave(G, Pr, Wk, 0, la);
         return;
     }
     STAMP(20);
@@ -1347,7 +1367,7 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
     for (int c = 0; c < 3; ++c) sh[c][lane] = t3[c];
 #pragma unroll
     for (int i = 0; i < 4; ++i) shs[i][lane] = 0.0;
-    __syncthreads();
+    if constexpr (FUSED) wave_sync(); else __syncthreads();
     STAMP(22);
     if (act && lane == first) {
         double Vi[3][3];
@@ -1373,7 +1393,7 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
         shs[2][lane] = gpdp;
         shs[3][lane] = p2;
     }
-    __syncthreads();
+    if constexpr (FUSED) wave_sync(); else __syncthreads();
     STAMP(23);
     // linearisation of the trial state
     SlotLin L;
@@ -1387,9 +1407,9 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
         slot_linearize(G, P, q, 0, 0, uvq, false, L);
     }
     shs[0][lane] = L.cost;
-    __syncthreads();  // sh is reused below
+    if constexpr (FUSED) wave_sync(); else __syncthreads();  // sh is reused below
     STAMP(24);
-    store_linearization(Wk, 1 - cur, s, lane, act, fr, first, nk, l, L, sh);
+    store_linearization<FUSED>(Wk, 1 - cur, s, lane, act, fr, first, nk, l, L, sh);
     STAMP(25);
     {  // wave partials: fixed-pairing butterflies over the lanes
         double v[kPartD];
@@ -1422,6 +1442,53 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
         if (lane == 0) __hip_atomic_store(Wk.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         lm_decide_wave<true>(G, Pr, Wk, 0, la);
     }
+}
+
+__global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr, Work Wk, int fuse_decide,
+                                                             LmArgs la) {
+    __shared__ double sh[10][64];
+    __shared__ double shp[3][64];
+    __shared__ double shs[4][64];
+    k6_body<false>(G, Pr, Wk, fuse_decide, la, blockIdx.x, threadIdx.x, sh, shp, shs);
+}
+
+// K5 + K6 in one launch (single rank, n_free <= 10): block 0 runs the camera solve and raises
+// the K5 flag (reset by K4c) after an agent-scope release; blocks 1.. carry four K6 waves each
+// (one landmark group per wave) that wait on the flag -- one kernel boundary less per LM
+// iteration.  Used only when every block is co-resident (<= kFusedMaxBlocks), so block 0 always
+// runs; the waits are bounded regardless.
+constexpr int kFusedMaxBlocks = 64;
+constexpr int kK6Rows = 17;  // 10 + 3 + 4 rows of 64 doubles per wave
+
+template <int NF>
+__global__ __launch_bounds__(256) void ba_solve_backsub(Geometry G, Prob Pr, Work Wk, LmArgs la) {
+    extern __shared__ __attribute__((aligned(16))) double dsm[];
+    if (blockIdx.x == 0) {
+        k5_body<NF>(G, Pr, Wk, dsm);
+        if ((threadIdx.x >> 6) == 0) {
+            __threadfence();  // wave 0 made every K5 write; release them device-wide
+            if (threadIdx.x == 0)
+                __hip_atomic_store(Wk.cnt + G.n_pb + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    // one poller per block (agent-scope acquire), the block's waves released by the barrier
+    if (threadIdx.x == 0) {
+        int polls = 0;
+        while (__hip_atomic_load(Wk.cnt + G.n_pb + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __builtin_amdgcn_s_sleep(4);
+            if (++polls > (1 << 22)) {  // bounded: flag the timeout, never hang the queue
+                __hip_atomic_store(Wk.cnt + G.n_pb + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = (blockIdx.x - 1) * 4 + wave;
+    if (w >= G.n_wave) return;
+    double (*sh)[64] = reinterpret_cast<double (*)[64]>(dsm + (size_t)wave * kK6Rows * 64);
+    k6_body<true>(G, Pr, Wk, 1, la, w, lane, sh, sh + 10, sh + 13);
 }
 
 __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
@@ -1595,6 +1662,8 @@ struct BundleAdjuster {
         h_state.alloc(1);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
+        const char* fe = std::getenv("RSVIO_BA_FUSE");    // "1": fused K5 + K6 (experiment)
+        fuse_k5k6 = fe && fe[0] == '1';
     }
     ~BundleAdjuster() {
         drop_graph();
@@ -1813,7 +1882,7 @@ struct BundleAdjuster {
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
-        grow(d_cnt, (size_t)n_pb + 1);
+        grow(d_cnt, (size_t)n_pb + 3);  // K6 arrivals, K4c block arrivals, K5 flag, wait timeout
         grow(d_state, 1);
         enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
         RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
@@ -1835,7 +1904,7 @@ struct BundleAdjuster {
     }
 
     void enqueue_reset(double lambda0) {
-        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb + 1);
+        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb + 3);
         hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work(), lambda0);
         RSVIO_HIP(hipGetLastError());
     }
@@ -1886,12 +1955,39 @@ struct BundleAdjuster {
         RSVIO_HIP(hipGetLastError());
     }
 
+    // RSVIO_BA_FUSE=1: K5 + K6 as one launch (ba_solve_backsub).  Off by default: measured
+    // slower (0.049-0.052 vs 0.044 ms per LM iteration) -- the flag
+    // hand-off's device-scope release/acquire costs more than the kernel boundary it replaces.
+    bool fuse_k5k6 = false;
+    bool fused_ok() const {
+        const int blocks = 1 + (G.n_wave + 3) / 4;
+        return fuse_k5k6 && !sharded() && fuse_combine && G.n_wave > 0 && G.n_free <= 10 &&
+               blocks <= kFusedMaxBlocks;
+    }
+    void launch_solve_backsub(const Prob& pr, const Work& wk, const LmArgs& la) {
+        const dim3 g(1 + (G.n_wave + 3) / 4), b(256);
+        const size_t lds = sizeof(double) * std::max<size_t>((size_t)4 * kK6Rows * 64, 128 + 2 * 6 * 10 * kLcLd);
+        switch (G.n_free) {
+#define RSVIO_FUSED(NF) \
+    case NF: hipLaunchKernelGGL(ba_solve_backsub<NF>, g, b, lds, stream, G, pr, wk, la); break;
+            RSVIO_FUSED(1) RSVIO_FUSED(2) RSVIO_FUSED(3) RSVIO_FUSED(4) RSVIO_FUSED(5)
+            RSVIO_FUSED(6) RSVIO_FUSED(7) RSVIO_FUSED(8) RSVIO_FUSED(9) RSVIO_FUSED(10)
+#undef RSVIO_FUSED
+            default: throw std::logic_error("fused K5+K6 needs n_free <= 10");
+        }
+        RSVIO_HIP(hipGetLastError());
+    }
+
     void enqueue_iteration(const rsvio_lm_cfg& cfg) {
         const Prob pr = prob();
         const Work wk = work();
         enqueue_linear_system();
-        launch_camera_solve(pr, wk);
         const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
+        if (fused_ok()) {
+            launch_solve_backsub(pr, wk, la);
+            return;
+        }
+        launch_camera_solve(pr, wk);
         // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
         const int fuse = (!sharded() && G.n_wave) ? 1 : 0;
         if (G.n_wave)
