@@ -79,7 +79,10 @@ void rsvio_tracker_destroy(rsvio_tracker* t);
 /* StereoPatchTracker::process_frame(&mut self, &GrayImage, &GrayImage, &mut Frame) (:116-187)
  * followed by get_track_points (:188-200).  Images are u8, row stride `stride` bytes.
  * Outputs are sorted by ascending id (canonical order; the reference iterates HashMaps).
- * New ids are assigned in detection scan order (image_utilities.rs:141-142). */
+ * New ids are assigned in detection scan order (image_utilities.rs:141-142).
+ * RSVIO_ERR_CAPACITY (lists still consistent and returned) when the frame's new points exceed
+ * max_features -- both cameras then admit the same leading new points and the rest are dropped
+ * -- or when cap_l / cap_r truncated a list. */
 int rsvio_tracker_process_frame(rsvio_tracker* t, const uint8_t* left, const uint8_t* right,
                                 size_t stride, rsvio_feature* out_l, size_t cap_l, size_t* n_l,
                                 rsvio_feature* out_r, size_t cap_r, size_t* n_r);
@@ -245,7 +248,15 @@ enum {
     RSVIO_LM_MAX_ITERATIONS = 3,      /* ::MaxIterationsReached (counts as success, sliding_window.rs:393) */
     RSVIO_LM_TRUST_REGION = 4,        /* ::TrustRegionRadiusTooSmall */
     RSVIO_LM_NUMERICAL_FAILURE = -1,  /* ::NumericalFailure -> caller reverts (:354-359) */
-    RSVIO_LM_SKIPPED = -2             /* too few residuals (:309-319) -> Ok(false) */
+    RSVIO_LM_SKIPPED = -2,            /* too few residuals (:309-319) -> Ok(false) */
+    RSVIO_LM_LINEAR_SOLVE_FAILED = -3 /* Err(LinearSolveFailed / "Singular matrix"): the caller retries
+                                       * with RSVIO_SOLVER_CHOLESKY, then reverts (:326-353) */
+};
+
+enum {
+    RSVIO_SOLVER_SCHUR = 0,     /* LinearSolverType::SparseSchurComplement (sliding_window.rs:126-135) */
+    RSVIO_SOLVER_CHOLESKY = 1   /* LinearSolverType::SparseCholesky, the fallback (:334-341): the full
+                                 * damped system, landmarks eliminated first (3x3 LL^T blocks) */
 };
 
 typedef struct {
@@ -254,6 +265,7 @@ typedef struct {
     double parameter_tolerance;   /* 1e-9 (:133) */
     double huber_delta;           /* 2.0 (:295) */
     double lambda_init;           /* 1e-4 (build's LM) */
+    int32_t linear_solver;        /* RSVIO_SOLVER_* (BA only; PnP always solves its 6x6 by Cholesky) */
 } rsvio_lm_cfg;
 
 typedef struct {
@@ -347,6 +359,10 @@ typedef struct {
 
 int rsvio_pnp_create(int32_t device, rsvio_pnp** out);
 void rsvio_pnp_destroy(rsvio_pnp* p);
+/* UnitQuaternion::from_matrix (sliding_window.rs:221,511; estimator.rs:209-211): nalgebra's
+ * iterative Rotation3::from_matrix_eps(m, f64::EPSILON, 0, identity) then from_rotation_matrix,
+ * for n row-major 3x3 matrices -> n quaternions (w, i, j, k).  Host only (no device needed). */
+int rsvio_quat_from_matrix(const double* R, size_t n, double* q);
 /* Launch rsvio_track_motion on a caller-owned stream (hipStream_t; NULL: the handle's own). */
 int rsvio_pnp_set_stream(rsvio_pnp* p, void* stream);
 /* SlidingWindow::map_points after optimize (sliding_window.rs:466-475): feature ids strictly

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <limits>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -27,6 +28,7 @@ enum {
     LM_TRUST_REGION = 4,
     LM_NUMERICAL_FAILURE = -1,
     LM_SKIPPED = -2,
+    LM_LINEAR_SOLVE_FAILED = -3,
 };
 
 struct Pose {
@@ -282,6 +284,49 @@ System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW
     return sy;
 }
 
+// The SparseCholesky fallback's system (sliding_window.rs:334-341): the FULL damped normal
+// equations (H + lambda I) dx = -g, assembled densely and factored by a dense LL^T -- the
+// oracle's independent restatement.  Unknowns are ordered [landmarks (3 each) | free poses (6
+// each)]: the elimination order a fill-reducing sparse Cholesky gives the BA arrow matrix (the
+// device eliminates the landmarks first with 3x3 LL^T blocks), so both fail on the same pivots.
+// Returns the cost; H is N x N, g is N.
+double build_full(const Problem& pr, const std::vector<Pose>& poses, const double* pW, double lambda,
+                  std::vector<double>& H, std::vector<double>& g) {
+    const int n = 6 * pr.n_free, m3 = 3 * pr.n_lm, N = n + m3;
+    H.assign((size_t)N * N, 0.0);
+    g.assign(N, 0.0);
+    double cost = 0.0;
+    for (int l = 0; l < pr.n_lm; ++l) {
+        const int pl = 3 * l;
+        for (int q = pr.lm_ptr[l]; q < pr.lm_ptr[l + 1]; ++q) {
+            const int o = pr.order[q];
+            const int kf = pr.obs_kf[o];
+            double r[2], J[2][9];
+            linearize(pW + 3 * l, poses[kf], pr.TCB2 + 16 * pr.obs_cam[o], pr.obs_uv + 2 * o, r, J);
+            double s = r[0] * r[0] + r[1] * r[1], rho, w;
+            huber(s, pr.delta, &rho, &w);
+            cost += 0.5 * rho;
+            const double wr[2] = {w * r[0], w * r[1]};
+            // the observation's columns: point (3) then, for a free keyframe, the pose (6)
+            int idx[9];
+            int m = 3;
+            for (int c = 0; c < 3; ++c) idx[c] = pl + c;
+            const int fb = pr.free_idx[kf];
+            if (fb >= 0) {
+                for (int a = 0; a < 6; ++a) idx[3 + a] = m3 + 6 * fb + a;
+                m = 9;
+            }
+            for (int a = 0; a < m; ++a) {
+                for (int c = 0; c < m; ++c)
+                    H[(size_t)idx[a] * N + idx[c]] += w * (J[0][a] * J[0][c] + J[1][a] * J[1][c]);
+                g[idx[a]] += J[0][a] * wr[0] + J[1][a] * wr[1];
+            }
+        }
+    }
+    for (int i = 0; i < N; ++i) H[(size_t)i * N + i] += lambda;
+    return cost;
+}
+
 // dense Cholesky solve (in place), returns false if not positive definite
 bool chol_solve(std::vector<double> A, int n, const std::vector<double>& b, std::vector<double>& x) {
     for (int j = 0; j < n; ++j) {
@@ -332,6 +377,98 @@ void orc_quat_from_rotation(const double* R, double* q) {
         w = (m(1, 0) - m(0, 1)) / d; x = (m(0, 2) + m(2, 0)) / d; y = (m(1, 2) + m(2, 1)) / d; z = 0.25 * d;
     }
     q[0] = w; q[1] = x; q[2] = y; q[3] = z;
+}
+
+// nalgebra 0.33 UnitQuaternion::from_matrix(m) (sliding_window.rs:221,511; estimator.rs:209-211):
+// Rotation3::from_matrix_eps(m, f64::EPSILON, 0, identity) -- Mueller et al.'s iteration
+//   omega = sum_c r_c x m_c / (|sum_c r_c . m_c| + eps);  r <- AxisAngle(omega / |omega|, |omega|) r
+// until |omega|^2 <= eps^2, then nalgebra's stationary-point check: perturb r by
+// AxisAngle(axis, sqrt(eps)) (right product, repeated until ||m - r||_F^2 moves by > eps); a
+// larger norm means a minimum (stop), else continue from the perturbed r with the axis
+// swizzled .yzx() -- followed by UnitQuaternion::from_rotation_matrix.  Column-major matrices
+// here (nalgebra's storage), so every sum runs in nalgebra's element order.
+namespace {
+struct M3 {
+    double a[9];  // column-major: a[3 * c + r]
+    double& operator()(int r, int c) { return a[3 * c + r]; }
+    double operator()(int r, int c) const { return a[3 * c + r]; }
+};
+M3 m3_mul(const M3& A, const M3& B) {  // gemv per column: A[:,0] b0 + A[:,1] b1 + A[:,2] b2
+    M3 C;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) C(r, c) = (A(r, 0) * B(0, c) + A(r, 1) * B(1, c)) + A(r, 2) * B(2, c);
+    return C;
+}
+M3 m3_axis_angle(const double u[3], double ang) {  // Rotation3::from_axis_angle
+    const double s = std::sin(ang), co = std::cos(ang), omc = 1.0 - co;
+    M3 R;
+    R(0, 0) = u[0] * u[0] + (1.0 - u[0] * u[0]) * co;
+    R(0, 1) = u[0] * u[1] * omc - u[2] * s;
+    R(0, 2) = u[0] * u[2] * omc + u[1] * s;
+    R(1, 0) = u[0] * u[1] * omc + u[2] * s;
+    R(1, 1) = u[1] * u[1] + (1.0 - u[1] * u[1]) * co;
+    R(1, 2) = u[1] * u[2] * omc - u[0] * s;
+    R(2, 0) = u[0] * u[2] * omc - u[1] * s;
+    R(2, 1) = u[1] * u[2] * omc + u[0] * s;
+    R(2, 2) = u[2] * u[2] + (1.0 - u[2] * u[2]) * co;
+    return R;
+}
+double m3_dist2(const M3& A, const M3& B) {  // (A - B).norm_squared(), storage order
+    double s = 0.0;
+    for (int k = 0; k < 9; ++k) s += (A.a[k] - B.a[k]) * (A.a[k] - B.a[k]);
+    return s;
+}
+}  // namespace
+
+extern "C" void orc_quat_from_matrix(const double* Rrow, double* q) {
+    const double eps = std::numeric_limits<double>::epsilon();
+    const double dist = std::max(std::sqrt(eps), eps * eps);
+    M3 m, r;
+    for (int i = 0; i < 9; ++i) {
+        m(i / 3, i % 3) = Rrow[i];
+        r.a[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    }
+    double pert[3] = {1.0, 0.0, 0.0};
+    for (int guard = 0; guard < 100000; ++guard) {
+        double w[3], den;
+        {
+            // sum over columns of cross(r_c, m_c) and dot(r_c, m_c), column order
+            double cx[3][3], dt[3];
+            for (int c = 0; c < 3; ++c) {
+                cx[c][0] = r(1, c) * m(2, c) - r(2, c) * m(1, c);
+                cx[c][1] = r(2, c) * m(0, c) - r(0, c) * m(2, c);
+                cx[c][2] = r(0, c) * m(1, c) - r(1, c) * m(0, c);
+                dt[c] = (r(0, c) * m(0, c) + r(1, c) * m(1, c)) + r(2, c) * m(2, c);
+            }
+            for (int k = 0; k < 3; ++k) w[k] = (cx[0][k] + cx[1][k]) + cx[2][k];
+            den = (dt[0] + dt[1]) + dt[2];
+        }
+        const double scale = std::fabs(den) + eps;
+        for (int k = 0; k < 3; ++k) w[k] = w[k] / scale;
+        const double n2 = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        if (n2 > eps * eps) {
+            const double n = std::sqrt(n2);
+            const double u[3] = {w[0] / n, w[1] / n, w[2] / n};
+            r = m3_mul(m3_axis_angle(u, n), r);
+            continue;
+        }
+        const double before = m3_dist2(m, r);
+        M3 p = r;
+        double after = before;
+        do {
+            p = m3_mul(p, m3_axis_angle(pert, dist));
+            after = m3_dist2(m, p);
+        } while (!(std::fabs(before - after) > eps));
+        if (before < after) break;
+        const double t = pert[0];
+        pert[0] = pert[1];
+        pert[1] = pert[2];
+        pert[2] = t;
+        r = p;
+    }
+    double R9[9];
+    for (int i = 0; i < 9; ++i) R9[i] = r(i / 3, i % 3);
+    orc_quat_from_rotation(R9, q);
 }
 
 // T (+) delta = T * Exp([rho; theta]) (right perturbation, translation-first tangent,
@@ -430,23 +567,41 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
             status = LM_NUMERICAL_FAILURE;
             break;
         }
-        bool solved = sy.ok && chol_solve(sy.S, n, sy.b, dc);
-        if (!solved) {
-            lambda *= nu;
-            nu *= 2.0;
-            if (lambda > 1e32) {
-                status = LM_TRUST_REGION;
+        double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
+        std::vector<double> dp(3 * (size_t)n_lm);
+        if (cfg->linear_solver == 1) {
+            // SparseCholesky fallback: the full damped system, solved densely
+            std::vector<double> H, g, rhs, dx;
+            build_full(pr, poses, pw.data(), lambda, H, g);
+            const int N = n + 3 * n_lm;
+            rhs.resize(N);
+            for (int i = 0; i < N; ++i) rhs[i] = -g[i];
+            if (!chol_solve(H, N, rhs, dx)) {  // Err(LinearSolveFailed): the caller reverts
+                status = LM_LINEAR_SOLVE_FAILED;
                 break;
             }
-            continue;
+            const int m3 = 3 * n_lm;
+            dc.assign(dx.begin() + m3, dx.end());
+            for (int f = 0; f < n; ++f) {
+                dx2 += dc[f] * dc[f];
+                gdx += g[m3 + f] * dc[f];
+            }
+            for (int i = 0; i < m3; ++i) {
+                dp[i] = dx[i];
+                dx2 += dp[i] * dp[i];
+                gdx += g[i] * dp[i];
+            }
+        } else {
+        bool solved = sy.ok && chol_solve(sy.S, n, sy.b, dc);
+        if (!solved) {  // Err(LinearSolveFailed / "Singular matrix"): sliding_window.rs:326-330 retries
+            status = LM_LINEAR_SOLVE_FAILED;
+            break;
         }
         // back substitution dp_l = Vi (-gp - sum_k W_k^T dc_k)
-        double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
         for (int f = 0; f < n; ++f) {
             dx2 += dc[f] * dc[f];
             gdx += sy.gc[f] * dc[f];
         }
-        std::vector<double> dp(3 * (size_t)n_lm);
         for (int l = 0; l < n_lm; ++l) {
             const LmBlock& B = sy.lms[l];
             double rhs[3] = {-B.gp[0], -B.gp[1], -B.gp[2]};
@@ -463,6 +618,7 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
                 dx2 += dp[3 * l + c] * dp[3 * l + c];
                 gdx += B.gp[c] * dp[3 * l + c];
             }
+        }
         }
         for (int k = 0; k < n_kf; ++k)
             if (!kf_fixed[k])
@@ -634,7 +790,7 @@ extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_
     rigid_inverse(T_last, TBW0);
     double R0[9] = {TBW0[0], TBW0[1], TBW0[2], TBW0[4], TBW0[5], TBW0[6], TBW0[8], TBW0[9], TBW0[10]};
     x[0] = TBW0[3]; x[1] = TBW0[7]; x[2] = TBW0[11];
-    orc_quat_from_rotation(R0, x + 3);
+    orc_quat_from_matrix(R0, x + 3);  // UnitQuaternion::from_matrix (:511)
     int status = LM_MAX_ITERS;
     if (obs.empty()) {
         status = LM_SKIPPED;
@@ -654,14 +810,9 @@ extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_
                 A[a * 6 + a] += lambda;
                 b[a] = -g[a];
             }
-            if (!chol_solve(A, 6, b, dx)) {
-                lambda *= nu;
-                nu *= 2.0;
-                if (lambda > 1e32) {
-                    status = LM_TRUST_REGION;
-                    break;
-                }
-                continue;
+            if (!chol_solve(A, 6, b, dx)) {  // Err(LinearSolveFailed) -> Ok(None) (:554-560)
+                status = LM_LINEAR_SOLVE_FAILED;
+                break;
             }
             double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
             for (int a = 0; a < 6; ++a) {
@@ -722,9 +873,15 @@ extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_
             }
         res->translation_norm = std::sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
         double Rr[9] = {Tr[0], Tr[1], Tr[2], Tr[4], Tr[5], Tr[6], Tr[8], Tr[9], Tr[10]};
-        double q7[7] = {0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
-        orc_quat_from_rotation(Rr, q7 + 3);
-        Pose Q = pose_from7(q7);
+        // UnitQuaternion::from_matrix(&R_rel).euler_angles() (estimator.rs:207-212): the unit
+        // quaternion's to_rotation_matrix, no renormalisation
+        double q[4];
+        orc_quat_from_matrix(Rr, q);
+        const double w = q[0], i = q[1], j = q[2], k = q[3];
+        Pose Q;
+        Q.R[0][0] = w * w + i * i - j * j - k * k; Q.R[0][1] = i * j * 2.0 - w * k * 2.0; Q.R[0][2] = w * j * 2.0 + i * k * 2.0;
+        Q.R[1][0] = w * k * 2.0 + i * j * 2.0; Q.R[1][1] = w * w - i * i + j * j - k * k; Q.R[1][2] = j * k * 2.0 - w * i * 2.0;
+        Q.R[2][0] = i * k * 2.0 - w * j * 2.0; Q.R[2][1] = w * i * 2.0 + j * k * 2.0; Q.R[2][2] = w * w - i * i - j * j + k * k;
         res->rotation_norm = euler_norm(Q.R);
         res->is_keyframe = (res->translation_norm > thr_t || res->rotation_norm > thr_r) ? 1 : 0;
     } else {  // estimator.rs:228-234: the frame stays a keyframe with T_W_B = I

@@ -17,7 +17,7 @@ def _orc_cfg(oracle, cfg):
     if cfg is None:
         return None
     return oracle.lm_cfg(cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance, cfg.huber_delta,
-                         cfg.lambda_init)
+                         cfg.lambda_init, cfg.linear_solver)
 
 
 class OracleSolver:

@@ -20,7 +20,7 @@ P = C.c_void_p
 class LmCfg(C.Structure):
     _fields_ = [("max_iterations", C.c_int), ("cost_tolerance", C.c_double),
                 ("parameter_tolerance", C.c_double), ("huber_delta", C.c_double),
-                ("lambda_init", C.c_double)]
+                ("lambda_init", C.c_double), ("linear_solver", C.c_int)]
 
 
 class BaResult(C.Structure):
@@ -90,6 +90,7 @@ _SIG = {
                                C.POINTER(BaResult)]),
     "orc_se3_plus": (None, [P, P, P]),
     "orc_quat_from_rotation": (None, [P, P]),
+    "orc_quat_from_matrix": (None, [P, P]),
 }
 
 _lib = None
@@ -261,8 +262,10 @@ def track_motion(ids_l, uv_l, ids_r, uv_r, map_ids, map_pw, T_W_B_last_kf, T_C_B
     return r
 
 
-def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):
-    return LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init)
+def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4,
+           linear_solver=0):
+    """linear_solver 0: SparseSchurComplement; 1: the SparseCholesky fallback (dense full system here)."""
+    return LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init, linear_solver)
 
 
 def ba_solve(prob, cfg=None):
@@ -309,6 +312,22 @@ def se3_plus(pose7, delta):
     a, d = np.ascontiguousarray(pose7, np.float64), np.ascontiguousarray(delta, np.float64)
     load().orc_se3_plus(_p(a), _p(d), _p(out))
     return out
+
+
+def quat_from_matrix(R):
+    """UnitQuaternion::from_matrix (w, i, j, k) of one row-major 3x3 matrix."""
+    q = np.zeros(4)
+    m = np.ascontiguousarray(R, np.float64)
+    load().orc_quat_from_matrix(_p(m), _p(q))
+    return q
+
+
+def quat_from_rotation(R):
+    """UnitQuaternion::from_rotation_matrix (closed form only), (w, i, j, k)."""
+    q = np.zeros(4)
+    m = np.ascontiguousarray(R, np.float64)
+    load().orc_quat_from_rotation(_p(m), _p(q))
+    return q
 
 
 # ---------------- feature_tracker/ crate (secondary variant) ----------------

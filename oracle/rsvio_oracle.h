@@ -173,6 +173,7 @@ typedef struct {
     double parameter_tolerance;/* :133 -> 1e-9 */
     double huber_delta;        /* :295 -> 2.0 */
     double lambda_init;        /* build's own LM -> 1e-4 */
+    int linear_solver;         /* 0 SparseSchurComplement, 1 SparseCholesky fallback (:334-341) */
 } orc_lm_cfg;
 
 typedef struct {
@@ -221,6 +222,8 @@ int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_l, const ui
 
 /* nalgebra UnitQuaternion::from_matrix restatement (sliding_window.rs:221) */
 void orc_quat_from_rotation(const double* R, double* qwxyz);
+/* UnitQuaternion::from_matrix: nalgebra's iterative from_matrix_eps, then from_rotation_matrix */
+void orc_quat_from_matrix(const double* R, double* qwxyz);
 
 #ifdef __cplusplus
 }

@@ -152,6 +152,7 @@ struct Geometry {
     int n_kf, n_free, n_lm, n_obs, n_slot, n_pb, n_wave, n_chunk;
     Mat4 TCB[2];
     double huber_delta;
+    int chol;  // linear solver: 0 Schur (inv3 landmark blocks), 1 the SparseCholesky fallback (LL^T)
 };
 
 // Structure-of-arrays problem description (device pointers)
@@ -317,12 +318,38 @@ __device__ void store_linearization(const Work& Wk, int buf, int s, int lane, bo
     }
 }
 
+// (V + lambda I)^-1 by its 3x3 Cholesky factor L: (L L^T)^-1 = L^-T L^-1.  This is the
+// landmark block of the SparseCholesky fallback (sliding_window.rs:334-341) with the landmarks
+// eliminated first -- the order a fill-reducing ordering gives the BA arrow matrix -- so the
+// camera block it leaves is the same Schur complement; false unless every pivot is > 0.
+__device__ __forceinline__ bool chol_inv3(const double A[3][3], double X[3][3]) {
+    const double d0 = A[0][0];
+    if (!(d0 > 0.0) || !isfinite(d0)) return false;
+    const double l00 = sqrt(d0), l10 = A[1][0] / l00, l20 = A[2][0] / l00;
+    const double d1 = A[1][1] - l10 * l10;
+    if (!(d1 > 0.0) || !isfinite(d1)) return false;
+    const double l11 = sqrt(d1), l21 = (A[2][1] - l20 * l10) / l11;
+    const double d2 = (A[2][2] - l20 * l20) - l21 * l21;
+    if (!(d2 > 0.0) || !isfinite(d2)) return false;
+    const double l22 = sqrt(d2);
+    const double m00 = 1.0 / l00, m11 = 1.0 / l11, m22 = 1.0 / l22;
+    const double m10 = -(l10 * m00) * m11, m21 = -(l21 * m11) * m22;
+    const double m20 = -(l20 * m00 + l21 * m10) * m22;
+    X[0][0] = (m00 * m00 + m10 * m10) + m20 * m20;
+    X[0][1] = X[1][0] = m10 * m11 + m20 * m21;
+    X[0][2] = X[2][0] = m20 * m22;
+    X[1][1] = m11 * m11 + m21 * m21;
+    X[1][2] = X[2][1] = m21 * m22;
+    X[2][2] = m22 * m22;
+    return true;
+}
+
 // (V + lambda I)^-1 of a landmark from its raw record; the same f64 operations wherever it is
 // needed (K4c lanes, K6 first lanes), so every user sees identical bits.  false if singular
-// (then Vi = 0).
-__device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda, double Vi[3][3]) {
+// (then Vi = 0).  chol: the SparseCholesky fallback's LL^T form (chol_inv3).
+__device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda, double Vi[3][3], int chol) {
     double A[3][3] = {{Vp[0] + lambda, Vp[1], Vp[2]}, {Vp[1], Vp[3] + lambda, Vp[4]}, {Vp[2], Vp[4], Vp[5] + lambda}};
-    const bool ok = inv3(A, Vi);
+    const bool ok = chol ? chol_inv3(A, Vi) : inv3(A, Vi);
     if (!ok)
 #pragma unroll
         for (int a = 0; a < 3; ++a)
@@ -469,7 +496,7 @@ __global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work 
             Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
         }
         double Vi[3][3];
-        if (!landmark_inverse(Lm + LV, lambda, Vi)) *Wk.singular = 1;
+        if (!landmark_inverse(Lm + LV, lambda, Vi, G.chol)) *Wk.singular = 1;
         double Ya[18];  // Y_a = W_a (V + lambda I)^-1
 #pragma unroll
         for (int a = 0; a < 6; ++a)
@@ -1227,12 +1254,11 @@ __device__ void lm_update(LmState& s, double cost, const double tv[4], int max_i
         s.status = RSVIO_LM_NUMERICAL_FAILURE;
         s.done = 1;
     } else if (!s.solve_ok) {
-        s.lambda *= s.nu;
-        s.nu *= 2.0;
-        if (s.lambda > 1e32) {
-            s.status = RSVIO_LM_TRUST_REGION;
-            s.done = 1;
-        }
+        // a singular landmark block or camera system: apex's optimize returns
+        // Err(LinearSolveFailed), which SlidingWindow::optimize answers with the SparseCholesky
+        // retry, then a revert (sliding_window.rs:326-353)
+        s.status = RSVIO_LM_LINEAR_SOLVE_FAILED;
+        s.done = 1;
     } else {
         s.new_cost = tv[0];
         s.dp2 = tv[1];
@@ -1371,7 +1397,7 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int f
     STAMP(22);
     if (act && lane == first) {
         double Vi[3][3];
-        landmark_inverse(Lm + LV, lambda, Vi);
+        landmark_inverse(Lm + LV, lambda, Vi, G.chol);
         double rhs[3] = {-Lm[LG], -Lm[LG + 1], -Lm[LG + 2]};
         for (int k = 0; k < nk; ++k)
 #pragma unroll
@@ -1450,45 +1476,6 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
     __shared__ double shp[3][64];
     __shared__ double shs[4][64];
     k6_body<false>(G, Pr, Wk, fuse_decide, la, blockIdx.x, threadIdx.x, sh, shp, shs);
-}
-
-// K5 + K6 in one launch (single rank, n_free <= 10): block 0 runs the camera solve and raises
-// the K5 flag (reset by K4c) after an agent-scope release; blocks 1.. carry four K6 waves each
-// (one landmark group per wave) that wait on the flag -- one kernel boundary less per LM
-// iteration.  Used only when every block is co-resident (<= kFusedMaxBlocks), so block 0 always
-// runs; the waits are bounded regardless.
-constexpr int kFusedMaxBlocks = 64;
-constexpr int kK6Rows = 17;  // 10 + 3 + 4 rows of 64 doubles per wave
-
-template <int NF>
-__global__ __launch_bounds__(256) void ba_solve_backsub(Geometry G, Prob Pr, Work Wk, LmArgs la) {
-    extern __shared__ __attribute__((aligned(16))) double dsm[];
-    if (blockIdx.x == 0) {
-        k5_body<NF>(G, Pr, Wk, dsm);
-        if ((threadIdx.x >> 6) == 0) {
-            __threadfence();  // wave 0 made every K5 write; release them device-wide
-            if (threadIdx.x == 0)
-                __hip_atomic_store(Wk.cnt + G.n_pb + 1, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    // one poller per block (agent-scope acquire), the block's waves released by the barrier
-    if (threadIdx.x == 0) {
-        int polls = 0;
-        while (__hip_atomic_load(Wk.cnt + G.n_pb + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-            __builtin_amdgcn_s_sleep(4);
-            if (++polls > (1 << 22)) {  // bounded: flag the timeout, never hang the queue
-                __hip_atomic_store(Wk.cnt + G.n_pb + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int w = (blockIdx.x - 1) * 4 + wave;
-    if (w >= G.n_wave) return;
-    double (*sh)[64] = reinterpret_cast<double (*)[64]>(dsm + (size_t)wave * kK6Rows * 64);
-    k6_body<true>(G, Pr, Wk, 1, la, w, lane, sh, sh + 10, sh + 13);
 }
 
 __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
@@ -1593,7 +1580,7 @@ struct BundleAdjuster {
     static bool same_cfg(const rsvio_lm_cfg& a, const rsvio_lm_cfg& b) {
         return a.max_iterations == b.max_iterations && a.cost_tolerance == b.cost_tolerance &&
                a.parameter_tolerance == b.parameter_tolerance && a.huber_delta == b.huber_delta &&
-               a.lambda_init == b.lambda_init;
+               a.lambda_init == b.lambda_init && a.linear_solver == b.linear_solver;
     }
     bool start_graph(const rsvio_lm_cfg& cfg, int k) {
         if (sharded() || !graphs_ok) return false;
@@ -1662,8 +1649,6 @@ struct BundleAdjuster {
         h_state.alloc(1);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
-        const char* fe = std::getenv("RSVIO_BA_FUSE");    // "1": fused K5 + K6 (experiment)
-        fuse_k5k6 = fe && fe[0] == '1';
     }
     ~BundleAdjuster() {
         drop_graph();
@@ -1728,6 +1713,7 @@ struct BundleAdjuster {
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
+        require_idle("set_problem");
         drop_graph();  // kernel arguments (sizes, buffers) change with the problem
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
@@ -1955,38 +1941,11 @@ struct BundleAdjuster {
         RSVIO_HIP(hipGetLastError());
     }
 
-    // RSVIO_BA_FUSE=1: K5 + K6 as one launch (ba_solve_backsub).  Off by default: measured
-    // slower (0.049-0.052 vs 0.044 ms per LM iteration) -- the flag
-    // hand-off's device-scope release/acquire costs more than the kernel boundary it replaces.
-    bool fuse_k5k6 = false;
-    bool fused_ok() const {
-        const int blocks = 1 + (G.n_wave + 3) / 4;
-        return fuse_k5k6 && !sharded() && fuse_combine && G.n_wave > 0 && G.n_free <= 10 &&
-               blocks <= kFusedMaxBlocks;
-    }
-    void launch_solve_backsub(const Prob& pr, const Work& wk, const LmArgs& la) {
-        const dim3 g(1 + (G.n_wave + 3) / 4), b(256);
-        const size_t lds = sizeof(double) * std::max<size_t>((size_t)4 * kK6Rows * 64, 128 + 2 * 6 * 10 * kLcLd);
-        switch (G.n_free) {
-#define RSVIO_FUSED(NF) \
-    case NF: hipLaunchKernelGGL(ba_solve_backsub<NF>, g, b, lds, stream, G, pr, wk, la); break;
-            RSVIO_FUSED(1) RSVIO_FUSED(2) RSVIO_FUSED(3) RSVIO_FUSED(4) RSVIO_FUSED(5)
-            RSVIO_FUSED(6) RSVIO_FUSED(7) RSVIO_FUSED(8) RSVIO_FUSED(9) RSVIO_FUSED(10)
-#undef RSVIO_FUSED
-            default: throw std::logic_error("fused K5+K6 needs n_free <= 10");
-        }
-        RSVIO_HIP(hipGetLastError());
-    }
-
     void enqueue_iteration(const rsvio_lm_cfg& cfg) {
         const Prob pr = prob();
         const Work wk = work();
         enqueue_linear_system();
         const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
-        if (fused_ok()) {
-            launch_solve_backsub(pr, wk, la);
-            return;
-        }
         launch_camera_solve(pr, wk);
         // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
         const int fuse = (!sharded() && G.n_wave) ? 1 : 0;
@@ -2024,6 +1983,7 @@ struct BundleAdjuster {
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         if (pend.active) throw std::logic_error("a solve is already in flight (call finish first)");
         G.huber_delta = cfg.huber_delta;
+        G.chol = cfg.linear_solver == RSVIO_SOLVER_CHOLESKY ? 1 : 0;
         pend = Pending{};
         pend.active = true;
         pend.cfg = cfg;
@@ -2150,7 +2110,14 @@ struct BundleAdjuster {
         finish(res);
     }
 
+    // entry points that read or replace what an in-flight solve uses (rsvio_ba_run_async before
+    // rsvio_ba_wait) are refused, as set_stream is
+    void require_idle(const char* what) const {
+        if (pend.active) throw std::logic_error(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
+    }
+
     void get_state(double* pose7, double* pW) {
+        require_idle("get_state");
         const int cur = h_state.p->cur;
         const Work wk = work();
         RSVIO_HIP(hipMemcpyAsync(pose7, wk.pose[cur], sizeof(double) * 7 * G.n_kf, hipMemcpyDeviceToHost, stream));
@@ -2160,8 +2127,10 @@ struct BundleAdjuster {
     }
 
     void build_system(double lambda, double huber_delta, double* S, double* b, double* cost) {
+        require_idle("build_system");
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
+        G.chol = 0;
         enqueue_start(lambda);
         enqueue_linear_system();
         std::vector<double> sys((size_t)36 * G.n_pb + 12 * G.n_free + 2);
@@ -2187,8 +2156,10 @@ struct BundleAdjuster {
 
     // diagnostic: one reduced system at lambda and its camera solve (K4c + K5) -> dc
     void camera_step(double lambda, double huber_delta, double* dc) {
+        require_idle("camera_step");
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
+        G.chol = 0;
         enqueue_start(lambda);
         enqueue_linear_system();
         launch_camera_solve(prob(), work());

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <stdexcept>
 #include <string>
 
 #include "rsvio_gpu.h"
@@ -36,6 +37,9 @@ int guarded(F&& f) {
     } catch (const std::bad_alloc&) {
         set_last_error("host allocation failed");
         return RSVIO_ERR_NOMEM;
+    } catch (const std::logic_error& e) {  // bad arguments or call order (std::invalid_argument too)
+        set_last_error(e.what());
+        return RSVIO_ERR_INVALID_ARG;
     } catch (const std::exception& e) {
         set_last_error(e.what());
         return RSVIO_ERR_INTERNAL;

@@ -23,6 +23,19 @@ namespace {
 RSVIO_DBG_DECL
 
 constexpr int NP = 52;
+
+// diagnostic phase accumulators (stamps build only): cycles per phase summed over a block's
+// iterations into g_dbg[block][16..20] (tools/lk_stamps.py)
+#ifdef RSVIO_STAMPS
+#define LK_CLK(v)                                  \
+    __builtin_amdgcn_s_waitcnt(0);                 \
+    const unsigned long long v = clock64()
+#define LK_ACC(slot, a, b)                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + (slot)] += (b) - (a)
+#else
+#define LK_CLK(v)
+#define LK_ACC(slot, a, b)
+#endif
 constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dispatched round-robin
 
 // patch.rs:19-72 -- the 52-point pattern (pixel offsets before the 1/2 scale of :126)
@@ -258,6 +271,7 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
 #ifdef RSVIO_STAMPS
         if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] += 1;
 #endif
+        LK_CLK(t0);
         float x = A.m00 * patx;
         x = A.m01 * paty + x;
         float y = A.m10 * patx;
@@ -275,6 +289,8 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
             float p00 = (float)r0[0], p10 = (float)r0[1], p01 = (float)r1[0], p11 = (float)r1[1];
             v = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
         }
+        LK_CLK(t1);
+        LK_ACC(16, t0, t1);
         float sum;
         {
             const float x1[1] = {inb ? v : 0.0f};
@@ -289,17 +305,24 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
         const int nres = __popcll(__ballot(use));
         if (!(nres > NP / 2)) return false;
         float inc[3];
+        LK_CLK(t2);
+        LK_ACC(17, t1, t2);
         {
             const float x3[3] = {(-T.h0) * r, (-T.h1) * r, (-T.h2) * r};
             lane_chains<3, false>(x3, inc, sh, lane);
         }
+        LK_CLK(t3);
+        LK_ACC(18, t2, t3);
         const float i0 = inc[0], i1 = inc[1], i2 = inc[2];
         if (!(isfinite(i0) && isfinite(i1) && isfinite(i2))) return false;
         const float nrm = sqrtf(i0 * i0 + i1 * i1 + i2 * i2);
         if (nrm > 1e6f) return false;
         if (nrm < thresh) break;
         A = mul3(A, se2_exp(i0, i1, i2));
-        if (!inbound(im, A.m02, A.m12, 2)) return false;
+        const bool inb2 = inbound(im, A.m02, A.m12, 2);
+        LK_CLK(t4);
+        LK_ACC(19, t3, t4);
+        if (!inb2) return false;
     }
     return true;
 }
@@ -326,8 +349,11 @@ __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, 
         T1.m02 /= sdn;
         T1.m12 /= sdn;
         Template tp;
-        if (!make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp, sh))
-            return false;
+        LK_CLK(m0);
+        const bool tok = make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp, sh);
+        LK_CLK(m1);
+        LK_ACC(20, m0, m1);
+        if (!tok) return false;
         if (!track_at_level(level_of(pyr1, w, h, i), tp, patx, paty, lane, T1, max_iter, thresh, sh))
             return false;
         T1.m02 *= sdn;
@@ -382,7 +408,8 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
     T0.m20 = 0.0f; T0.m21 = 0.0f; T0.m22 = 1.0f;
     Aff fwd, bwd;
 #ifdef RSVIO_STAMPS
-    if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] = 0;
+    if (lane == 0 && blockIdx.x < 4096)
+        for (int k = 15; k <= 20; ++k) g_dbg[blockIdx.x * 32 + k] = 0;
 #endif
     STAMP(0);
     bool ok = track_one(pyr0, pyr1, L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,

@@ -25,6 +25,7 @@
 #include <stdexcept>
 
 #include "common.hpp"
+#include "rotation.hpp"
 #include "se3.hpp"
 
 namespace rsvio {
@@ -38,7 +39,8 @@ constexpr int kPnpMaxFeatures = 4096; // features per frame (both cameras), obse
 constexpr int kPnpMapLds = 4096;      // map ids staged in LDS (32 KB) up to this size
 constexpr int kRed = 28;          // H upper (21), g (6), cost
 
-enum { LM_COST_TOL = 1, LM_PARAM_TOL = 2, LM_MAX_ITERS = 3, LM_TRUST_REGION = 4, LM_NUMFAIL = -1, LM_SKIPPED = -2 };
+enum { LM_COST_TOL = 1, LM_PARAM_TOL = 2, LM_MAX_ITERS = 3, LM_TRUST_REGION = 4, LM_NUMFAIL = -1, LM_SKIPPED = -2,
+       LM_LINSOLVE = -3 };
 
 struct PnpArgs {
     const uint8_t* ids[2];   // u64 feature ids, `id_stride` bytes apart
@@ -50,6 +52,7 @@ struct PnpArgs {
     const float* map_pw;     // [f32; 3] per map point (sliding_window.rs:466-475)
     int n_map;
     double T_last[16];
+    double q0[4];            // from_matrix(R_B_W) of the last keyframe (host, rotation.hpp)
     double TCB[2][16];
     int max_iter;
     double cost_tol, param_tol, huber_delta, lambda0, thr_t, thr_r;
@@ -302,14 +305,9 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
         double dx[6];
         const bool solved = ldl6(C->H, C->lambda, C->g, dx);
         STAMP(30);
-        if (!solved) {
-            C->lambda *= C->nu;
-            C->nu *= 2.0;
-            if (C->lambda > 1e32) {
-                C->status = LM_TRUST_REGION;
-                break;
-            }
-            continue;
+        if (!solved) {  // Err(LinearSolveFailed) -> track_motion returns Ok(None) (:554-560)
+            C->status = LM_LINSOLVE;
+            break;
         }
         double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
         for (int k = 0; k < 6; ++k) {
@@ -331,26 +329,6 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
     C->run = 0;
 }
 
-// nalgebra Rotation3::euler_angles (roll, pitch, yaw) of a rotation matrix (estimator.rs:207-212)
-__device__ __forceinline__ double euler_norm(const double R[3][3]) {
-    double roll, pitch, yaw;
-    if (fabs(R[2][0]) < 1.0) {
-        pitch = -asin(R[2][0]);
-        const double c = cos(pitch);
-        roll = atan2(R[2][1] / c, R[2][2] / c);
-        yaw = atan2(R[1][0] / c, R[0][0] / c);
-    } else if (R[2][0] <= -1.0) {
-        roll = atan2(R[0][1], R[0][2]);
-        pitch = M_PI_2;
-        yaw = 0.0;
-    } else {
-        roll = -atan2(-R[0][1], -R[0][2]);
-        pitch = -M_PI_2;
-        yaw = 0.0;
-    }
-    return sqrt((roll * roll + pitch * pitch) + yaw * yaw);
-}
-
 __device__ void pnp_finish(const PnpArgs& A, const Ctl& C) {
     rsvio_motion_result r;
     r.status = C.status;
@@ -364,29 +342,16 @@ __device__ void pnp_finish(const PnpArgs& A, const Ctl& C) {
     if (ok) {
         // T_W_B = inv(SE3(F).matrix()) (sliding_window.rs:566-569)
         const Pose P = pose_from7(C.x);
-        double TBW[16], Tl_inv[16];
+        double TBW[16];
         for (int i = 0; i < 3; ++i) {
             for (int j = 0; j < 3; ++j) TBW[4 * i + j] = P.R[i][j];
             TBW[4 * i + 3] = P.t[i];
         }
         TBW[12] = 0.0; TBW[13] = 0.0; TBW[14] = 0.0; TBW[15] = 1.0;
         rigid_inverse(TBW, r.T_W_B);
-        rigid_inverse(A.T_last, Tl_inv);
-        // T_rel = T_W_B * inv(T_W_B_last_kf) (estimator.rs:205)
-        double Tr[16];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) {
-                double s = 0.0;
-                for (int k = 0; k < 4; ++k) s += r.T_W_B[4 * i + k] * Tl_inv[4 * k + j];
-                Tr[4 * i + j] = s;
-            }
-        r.translation_norm = sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
-        const double Rr[9] = {Tr[0], Tr[1], Tr[2], Tr[4], Tr[5], Tr[6], Tr[8], Tr[9], Tr[10]};
-        double q7[7] = {0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0};
-        quat_from_rot(Rr, q7 + 3);
-        const Pose Q = pose_from7(q7);  // UnitQuaternion -> rotation matrix
-        r.rotation_norm = euler_norm(Q.R);
-        r.is_keyframe = (r.translation_norm > A.thr_t || r.rotation_norm > A.thr_r) ? 1 : 0;
+        // the keyframe rule (estimator.rs:204-225) runs on the host after the kernel
+        // (keyframe_rule(): nalgebra's iterative from_matrix is a long serial loop)
+        r.is_keyframe = 0;
     } else {
         for (int k = 0; k < 16; ++k) r.T_W_B[k] = (k % 5 == 0) ? 1.0 : 0.0;
         r.is_keyframe = 1;
@@ -447,11 +412,11 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
         // sliding_window.rs:506-517: F = (t_B_W, from_matrix(R_B_W)) of the last keyframe
         double TBW[16];
         rigid_inverse(A.T_last, TBW);
-        const double R[9] = {TBW[0], TBW[1], TBW[2], TBW[4], TBW[5], TBW[6], TBW[8], TBW[9], TBW[10]};
         C.x[0] = TBW[3];
         C.x[1] = TBW[7];
         C.x[2] = TBW[11];
-        quat_from_rot(R, C.x + 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) C.x[3 + k] = A.q0[k];  // UnitQuaternion::from_matrix(R_B_W) (host)
         const Pose P0 = pose_from7(C.x);  // SE3::from (apex) of the initial 7-vector
 #pragma unroll
         for (int k = 0; k < 9; ++k) C.R[k] = P0.R[k / 3][k % 3];
@@ -615,6 +580,8 @@ struct Pnp {
     DevBuf<uint8_t> feat;            // [ids_l | ids_r | uv_l | uv_r]
     HostBuf<uint8_t> hfeat;
     HostBuf<rsvio_motion_result> hres;
+    double q0_key[16] = {};              // T_W_B_last_kf of the cached initial quaternion
+    double q0[4] = {1.0, 0.0, 0.0, 0.0};
 
     void init(int dev) {
         device = dev;
@@ -627,7 +594,7 @@ struct Pnp {
     }
 };
 
-PnpArgs make_args(const Pnp& p, const double* T_last, const double* TCB2, const rsvio_lm_cfg* cfg,
+PnpArgs make_args(Pnp& p, const double* T_last, const double* TCB2, const rsvio_lm_cfg* cfg,
                   const rsvio_keyframe_rule* rule) {
     PnpArgs A{};
     A.map_ids = p.map_ids.p;
@@ -643,7 +610,39 @@ PnpArgs make_args(const Pnp& p, const double* T_last, const double* TCB2, const 
     A.thr_t = rule->translation_threshold;
     A.thr_r = rule->rotation_threshold;
     A.out = p.hres.p;
+    // sliding_window.rs:506-517: F starts from the last keyframe's T_B_W = inv(T_W_B) with
+    // q = UnitQuaternion::from_matrix(R_B_W); cached per keyframe pose
+    if (std::memcmp(p.q0_key, T_last, sizeof p.q0_key) != 0) {
+        double TBW[16];
+        rigid_inverse(T_last, TBW);
+        const double R[9] = {TBW[0], TBW[1], TBW[2], TBW[4], TBW[5], TBW[6], TBW[8], TBW[9], TBW[10]};
+        rot::quat_from_matrix(R, p.q0);
+        std::memcpy(p.q0_key, T_last, sizeof p.q0_key);
+    }
+    std::memcpy(A.q0, p.q0, sizeof A.q0);
     return A;
+}
+
+// The keyframe rule (estimator.rs:204-225) on the PnP result: T_rel = T_W_B inv(T_W_B_last_kf),
+// keyframe iff |t_rel| > thr_t or |euler(from_matrix(R_rel))| > thr_r.  A failed PnP keeps
+// is_keyframe = 1 and T_W_B = I (written by the kernel, estimator.rs:228-234).
+void keyframe_rule(const PnpArgs& A, rsvio_motion_result* r) {
+    if (r->status <= 0) return;
+    double Tl_inv[16], Tr[16];
+    rigid_inverse(A.T_last, Tl_inv);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 4; ++k) s += r->T_W_B[4 * i + k] * Tl_inv[4 * k + j];
+            Tr[4 * i + j] = s;
+        }
+    r->translation_norm = std::sqrt((Tr[3] * Tr[3] + Tr[7] * Tr[7]) + Tr[11] * Tr[11]);
+    const double Rr[9] = {Tr[0], Tr[1], Tr[2], Tr[4], Tr[5], Tr[6], Tr[8], Tr[9], Tr[10]};
+    double q[4], Q[9];
+    rot::quat_from_matrix(Rr, q);
+    rot::rotation_of_quat(q, Q);
+    r->rotation_norm = rot::euler_norm(Q);
+    r->is_keyframe = (r->translation_norm > A.thr_t || r->rotation_norm > A.thr_r) ? 1 : 0;
 }
 
 int run_pnp(Pnp& p, const PnpArgs& A, hipStream_t stream, rsvio_motion_result* res) {
@@ -651,6 +650,7 @@ int run_pnp(Pnp& p, const PnpArgs& A, hipStream_t stream, rsvio_motion_result* r
     RSVIO_HIP(hipGetLastError());
     RSVIO_HIP(hipStreamSynchronize(stream));
     *res = *p.hres.p;
+    keyframe_rule(A, res);
     if (res->n_observations < 0) {
         set_last_error("track_motion: more than 4096 features in one frame");
         return RSVIO_ERR_CAPACITY;
@@ -667,6 +667,12 @@ struct rsvio_pnp {
 using rsvio::guarded;
 
 extern "C" {
+
+int rsvio_quat_from_matrix(const double* R, size_t n, double* q) {
+    if (n && (!R || !q)) return RSVIO_ERR_INVALID_ARG;
+    for (size_t i = 0; i < n; ++i) rsvio::rot::quat_from_matrix(R + 9 * i, q + 4 * i);
+    return RSVIO_OK;
+}
 
 int rsvio_pnp_create(int32_t device, rsvio_pnp** out) {
     if (!out) return RSVIO_ERR_INVALID_ARG;

@@ -131,7 +131,7 @@ __device__ __forceinline__ double rsqrt_f64(double d) {
 
 // Rigid inverse [R^T | -R^T t] of a row-major 4x4 transform (nalgebra try_inverse of a rigid
 // T up to rounding; the oracle uses the same formula).
-__device__ __forceinline__ void rigid_inverse(const double* T, double* Ti) {
+__host__ __device__ __forceinline__ void rigid_inverse(const double* T, double* Ti) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
 #pragma unroll

@@ -263,10 +263,15 @@ __global__ __launch_bounds__(1024) void append_pack_kernel(
     int pos = block_exclusive_scan(local, sh, &total);
     const int c0 = counts[0], c1 = counts[1];
     const unsigned long long base = *last_id;
+    // Both cameras append the same new points (feature_tracker.rs:162-170), so admit only as many as
+    // the fuller camera has room for: no slot beyond what was written is ever counted, and ids stay
+    // consecutive.  A frame with more new points than room raises the overflow flag (reported by
+    // fetch() as RSVIO_ERR_CAPACITY); the flag is rewritten every frame.
+    const int admit = min(total, max(0, min(capacity - c0, capacity - c1)));
     for (int i = b; i < e; ++i) {
         if (!new_valid[i]) continue;
-        const int d0 = c0 + pos, d1 = c1 + pos;
-        if (d0 < capacity && d1 < capacity) {
+        if (pos < admit) {
+            const int d0 = c0 + pos, d1 = c1 + pos;
             for (int k = 0; k < 6; ++k) {
                 map_aff0[6 * d0 + k] = new_aff0[6 * i + k];
                 map_aff1[6 * d1 + k] = new_aff1[6 * i + k];
@@ -277,17 +282,12 @@ __global__ __launch_bounds__(1024) void append_pack_kernel(
         ++pos;
     }
     __syncthreads();
-    int n0 = c0 + total, n1 = c1 + total;
-    if (n0 > capacity || n1 > capacity) {
-        n0 = min(n0, capacity);
-        n1 = min(n1, capacity);
-        if (threadIdx.x == 0) *overflow = 1;
-    }
-    __syncthreads();
+    const int n0 = c0 + admit, n1 = c1 + admit;
     if (threadIdx.x == 0) {
         counts[0] = n0;
         counts[1] = n1;
-        *last_id = base + (unsigned long long)total;
+        *last_id = base + (unsigned long long)admit;
+        *overflow = total > admit ? 1 : 0;
     }
     // get_track_points packing, both cameras spread over the block; with cameras attached the
     // Frame::add_{left,right}_feature unprojection (frame.rs:118-119,131-132) is fused here
@@ -312,12 +312,14 @@ __global__ __launch_bounds__(1024) void remove_ids_kernel(const uint64_t* __rest
                                                           uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
                                                           float* __restrict__ tmp_aff, uint64_t* __restrict__ tmp_ids,
                                                           int* __restrict__ counts, rsvio_feature* out0,
-                                                          rsvio_feature* out1) {
+                                                          rsvio_feature* out1, float2* und0, float2* und1,
+                                                          float2* __restrict__ tmp_und) {
     __shared__ int sh[1024];
     for (int c = 0; c < 2; ++c) {
         float* ma = c == 0 ? map_aff0 : map_aff1;
         uint64_t* ids = c == 0 ? ids0 : ids1;
         rsvio_feature* out = c == 0 ? out0 : out1;
+        float2* und = c == 0 ? und0 : und1;  // the fused unprojection's output, compacted alike
         const int n = counts[c];
         const int per = (n + blockDim.x - 1) / blockDim.x;
         const int b = threadIdx.x * per, e = min(n, b + per);
@@ -328,6 +330,7 @@ __global__ __launch_bounds__(1024) void remove_ids_kernel(const uint64_t* __rest
             local += drop ? 0 : 1;
             tmp_ids[i] = drop ? ~0ull : ids[i];
             for (int k = 0; k < 6; ++k) tmp_aff[6 * i + k] = ma[6 * i + k];
+            if (und) tmp_und[i] = und[i];
         }
         int total;
         int pos = block_exclusive_scan(local, sh, &total);
@@ -335,6 +338,7 @@ __global__ __launch_bounds__(1024) void remove_ids_kernel(const uint64_t* __rest
             if (tmp_ids[i] == ~0ull) continue;
             for (int k = 0; k < 6; ++k) ma[6 * pos + k] = tmp_aff[6 * i + k];
             ids[pos] = tmp_ids[i];
+            if (und) und[pos] = tmp_und[i];
             ++pos;
         }
         __syncthreads();
@@ -376,6 +380,7 @@ struct Tracker {
     HostBuf<int> h_counts;
     CamPair cams{};                 // T12 unprojection fused into append_pack_kernel when on
     DevBuf<float2> undist;          // 2 x cap
+    DevBuf<float2> tmp_und;         // cap (remove_ids compaction scratch)
     HostBuf<float2> h_undist;       // last process_frame's undistorted coordinates
     HostBuf<rsvio_feature> h_out;   // pinned staging of both packed feature lists (2 x cap)
     size_t last_n[2] = {0, 0};
@@ -496,7 +501,7 @@ struct Tracker {
         }
     }
 
-    void fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
+    int fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
         const size_t bl = std::min((size_t)cap, (size_t)host_count[0] + (size_t)n_cells);
         const size_t br = std::min((size_t)cap, (size_t)host_count[1] + (size_t)n_cells);
         RSVIO_HIP(hipMemcpyAsync(h_counts.p, counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
@@ -517,6 +522,15 @@ struct Tracker {
         last_n[1] = cams.on ? nr : 0;
         *n_l = nl;
         *n_r = nr;
+        if (h_counts.p[2]) {
+            set_last_error("StereoPatchTracker: new points exceed max_features; the excess was dropped");
+            return RSVIO_ERR_CAPACITY;
+        }
+        if (nl < ml || nr < mr) {
+            set_last_error("StereoPatchTracker: feature list exceeds the output capacity (truncated)");
+            return RSVIO_ERR_CAPACITY;
+        }
+        return RSVIO_OK;
     }
 };
 
@@ -628,8 +642,7 @@ int rsvio_tracker_process_frame(rsvio_tracker* t, const uint8_t* left, const uin
         RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p, w, left, stride, w, h, hipMemcpyHostToDevice, T.stream));
         RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p + w * h, w, right, stride, w, h, hipMemcpyHostToDevice, T.stream));
         T.enqueue_frame(T.d_img.p, T.d_img.p + w * h);
-        T.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
-        return (int)RSVIO_OK;
+        return T.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
     });
 }
 
@@ -639,8 +652,7 @@ int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left, 
     if (!t || !d_left || !d_right || !n_l || !n_r) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
         t->t.enqueue_frame(d_left, d_right);
-        t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
-        return (int)RSVIO_OK;
+        return t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
     });
 }
 
@@ -661,6 +673,7 @@ int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const 
         if (!T.undist.p) {
             T.undist.alloc((size_t)2 * T.cap);
             T.h_undist.alloc((size_t)2 * T.cap);
+            T.tmp_und.alloc((size_t)T.cap);
         }
         T.cams.cam[0] = *left;
         T.cams.cam[1] = *right;
@@ -691,12 +704,23 @@ int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n) {
         RSVIO_HIP(hipMemcpyAsync(T.rm_ids.p, ids, n * sizeof(uint64_t), hipMemcpyHostToDevice, T.stream));
         hipLaunchKernelGGL(rsvio::remove_ids_kernel, dim3(1), dim3(1024), 0, T.stream, T.rm_ids.p, (int)n, T.maff(0),
                            T.maff(1), T.mid(0), T.mid(1), T.tmp_aff.p, T.ids_tmp.p, T.counts.p, T.out.p,
-                           T.out.p + T.cap);
+                           T.out.p + T.cap, T.cams.on ? T.undist.p : nullptr,
+                           T.cams.on ? T.undist.p + T.cap : nullptr, T.tmp_und.p);
         RSVIO_HIP(hipGetLastError());
         RSVIO_HIP(hipMemcpyAsync(T.h_counts.p, T.counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, T.stream));
         RSVIO_HIP(hipStreamSynchronize(T.stream));
         T.host_count[0] = T.h_counts.p[0];
         T.host_count[1] = T.h_counts.p[1];
+        if (T.cams.on) {  // undistorted() stays aligned with the compacted feature lists
+            const size_t nl = std::min(T.last_n[0], (size_t)T.host_count[0]);
+            const size_t nr = std::min(T.last_n[1], (size_t)T.host_count[1]);
+            if (nl) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p, T.undist.p, nl * sizeof(float2), hipMemcpyDeviceToHost, T.stream));
+            if (nr) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p + T.cap, T.undist.p + T.cap, nr * sizeof(float2),
+                                             hipMemcpyDeviceToHost, T.stream));
+            RSVIO_HIP(hipStreamSynchronize(T.stream));
+            T.last_n[0] = nl;
+            T.last_n[1] = nr;
+        }
         return (int)RSVIO_OK;
     });
 }

@@ -19,7 +19,7 @@ ERRORS = {
     -5: "RSVIO_ERR_NO_DEVICE", -6: "RSVIO_ERR_INTERNAL", -7: "RSVIO_ERR_RCCL",
 }
 LM_STATUS = {1: "CostToleranceReached", 2: "ParameterToleranceReached", 3: "MaxIterationsReached",
-             4: "TrustRegionRadiusTooSmall", -1: "NumericalFailure", -2: "Skipped"}
+             4: "TrustRegionRadiusTooSmall", -1: "NumericalFailure", -2: "Skipped", -3: "LinearSolveFailed"}
 
 
 class RsvioError(RuntimeError):
@@ -47,7 +47,7 @@ class TrackBatch(C.Structure):
 class LmCfg(C.Structure):
     _fields_ = [("max_iterations", C.c_int32), ("cost_tolerance", C.c_double),
                 ("parameter_tolerance", C.c_double), ("huber_delta", C.c_double),
-                ("lambda_init", C.c_double)]
+                ("lambda_init", C.c_double), ("linear_solver", C.c_int32)]
 
 
 class BaResult(C.Structure):
@@ -105,6 +105,7 @@ SIG = {
     "rsvio_unproject_d": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P, P]),
     "rsvio_tracker_set_cameras": (C.c_int, [P, C.POINTER(Camera), C.POINTER(Camera)]),
     "rsvio_tracker_undistorted": (C.c_int, [P, P, C.c_size_t, P, C.c_size_t]),
+    "rsvio_quat_from_matrix": (C.c_int, [P, C.c_size_t, P]),
     "rsvio_pnp_create": (C.c_int, [C.c_int32, C.POINTER(P)]),
     "rsvio_pnp_destroy": (None, [P]),
     "rsvio_pnp_set_stream": (C.c_int, [P, P]),

@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import math
 from collections import deque
 from dataclasses import dataclass, field
 
@@ -20,9 +21,22 @@ from . import _lib
 from ._lib import check, ptr
 
 
-def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):
-    """sliding_window.rs:126-135 (max 20 iterations, cost tol 1e-6, parameter tol 1e-9) + Huber(2.0)."""
-    return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init)
+SOLVER_SCHUR, SOLVER_CHOLESKY = 0, 1        # LinearSolverType::{SparseSchurComplement, SparseCholesky}
+LINEAR_SOLVE_FAILED = -3                    # RSVIO_LM_LINEAR_SOLVE_FAILED
+
+
+def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4,
+           linear_solver=SOLVER_SCHUR):
+    """sliding_window.rs:126-135 (max 20 iterations, cost tol 1e-6, parameter tol 1e-9) + Huber(2.0);
+    linear_solver SOLVER_CHOLESKY is the fallback configuration of :334-341 (same tolerances)."""
+    return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init, linear_solver)
+
+
+def fallback_cfg(cfg=None):
+    """The SparseCholesky configuration the reference retries with (sliding_window.rs:333-341)."""
+    c = cfg or lm_cfg()
+    return lm_cfg(c.max_iterations, c.cost_tolerance, c.parameter_tolerance, c.huber_delta, c.lambda_init,
+                  SOLVER_CHOLESKY)
 
 
 def _c(a, dt):
@@ -177,15 +191,29 @@ def _feature_arrays(feats):
             np.asarray(uv, np.float64).reshape(-1, 2).astype(np.float32).astype(np.float64))
 
 
-def _quat_from_rot(R):
-    from .synthetic import quat_from_rot
-    return quat_from_rot(R)
+def quat_from_matrix(R) -> np.ndarray:
+    """UnitQuaternion::from_matrix (sliding_window.rs:221,511): nalgebra's iterative
+    Rotation3::from_matrix_eps then from_rotation_matrix, (w, i, j, k); n x 3 x 3 -> n x 4
+    (rsvio_quat_from_matrix, host code of the library)."""
+    R = np.ascontiguousarray(R, np.float64).reshape(-1, 9)
+    q = np.zeros((len(R), 4))
+    check(_lib.load().rsvio_quat_from_matrix(ptr(R), len(R), ptr(q)))
+    return q
 
 
-def _T_from_pose7(p7):
-    from .synthetic import rot_from_quat
+def se3_matrix(p7) -> np.ndarray:
+    """apex SE3::from([t; w, i, j, k]).matrix(): the quaternion normalised, then nalgebra's
+    to_rotation_matrix (the same formula as the kernels' pose_from7, se3.hpp)."""
+    w, x, y, z = (float(v) for v in p7[3:7])
+    n = 1.0 / math.sqrt(w * w + x * x + y * y + z * z)
+    w, x, y, z = w * n, x * n, y * n, z * n
+    ww, xx, yy, zz = w * w, x * x, y * y, z * z
+    xy, wz, wy = x * y * 2.0, w * z * 2.0, w * y * 2.0
+    xz, yz, wx = x * z * 2.0, y * z * 2.0, w * x * 2.0
     T = np.eye(4)
-    T[:3, :3] = rot_from_quat(np.asarray(p7[3:7]))
+    T[:3, :3] = [[ww + xx - yy - zz, xy - wz, wy + xz],
+                 [wz + xy, ww - xx + yy - zz, yz - wx],
+                 [xz - wy, wx + yz, ww - xx - yy + zz]]
     T[:3, 3] = p7[:3]
     return T
 
@@ -198,6 +226,7 @@ class SlidingWindow:
         self.keyframes: deque[Frame] = deque()
         self.map_points: dict[int, np.ndarray] = {}  # feature id -> [f32; 3]
         self.map_version = 0                           # bumped whenever map_points is replaced
+        self.fallbacks = 0                             # SparseCholesky retries (diagnostic)
         self.solver = solver or BundleAdjuster(max_keyframes=max(max_frames, 2), device=device)
         self.last_result = None
         self._pending = None                           # landmark ids of a solve in flight (optimize_async)
@@ -268,9 +297,9 @@ class SlidingWindow:
             p_B = np.matmul(Tbc[:, :3, :3], p_C[:, :, None])[:, :, 0] + Tbc[:, :3, 3]
             p_init[new] = np.matmul(Twb[:, :3, :3], p_B[:, :, None])[:, :, 0] + Twb[:, :3, 3]
         pose7 = np.zeros((len(kfs), 7))
-        for i, T_B_W in enumerate(np.linalg.inv(T_W_B)):
-            pose7[i, :3] = T_B_W[:3, 3]
-            pose7[i, 3:] = _quat_from_rot(T_B_W[:3, :3])
+        T_B_W = np.linalg.inv(T_W_B)  # try_inverse (:218)
+        pose7[:, :3] = T_B_W[:, :3, 3]
+        pose7[:, 3:] = quat_from_matrix(T_B_W[:, :3, :3])  # UnitQuaternion::from_matrix (:221)
         kf_fixed = np.zeros(len(kfs), np.uint8)
         kf_fixed[0] = 1
         T_C_B2 = np.stack([T_Cl_B.reshape(16), T_Cr_B.reshape(16)])
@@ -289,6 +318,11 @@ class SlidingWindow:
             self.last_result = None
             return False
         pose, pw, res = self.solver.solve(pose7, fixed, p_init, lm, kf, cam, uv, tcb, cfg)
+        if res.status == LINEAR_SOLVE_FAILED:
+            # sliding_window.rs:326-353: a singular Schur solve is retried from the same initial
+            # values with SparseCholesky; if that fails too the window reverts (_apply: Ok(false))
+            self.fallbacks += 1
+            pose, pw, res = self.solver.solve(pose7, fixed, p_init, lm, kf, cam, uv, tcb, fallback_cfg(cfg))
         return self._apply(ids, pose, pw, res)
 
     def _apply(self, ids, pose, pw, res) -> bool:
@@ -299,7 +333,7 @@ class SlidingWindow:
         pw32 = pw.astype(np.float32)
         self.map_points = dict(zip(ids, pw32))
         self.map_version += 1
-        T_W_B = np.linalg.inv(np.stack([_T_from_pose7(pose[i]) for i in range(len(self.keyframes))]))
+        T_W_B = np.linalg.inv(np.stack([se3_matrix(pose[i]) for i in range(len(self.keyframes))]))
         for f, T in zip(self.keyframes, T_W_B):
             f.T_W_B = T
         return True
@@ -324,14 +358,17 @@ class SlidingWindow:
             return False
         self.solver.set_problem(pose7, fixed, p_init, lm, kf, cam, uv, tcb)
         self.solver.run_async(cfg)
-        self._pending = ids
+        self._pending = (ids, cfg)
         return None
 
     def finish(self):
         """Complete a solve started by optimize_async (no-op otherwise); returns its bool."""
         if self._pending is None:
             return None
-        ids, self._pending = self._pending, None
+        (ids, cfg), self._pending = self._pending, None
         res = self.solver.wait()
+        if res.status == LINEAR_SOLVE_FAILED:  # the SparseCholesky retry (:326-353), same problem
+            self.fallbacks += 1
+            res = self.solver.run(fallback_cfg(cfg))
         pose, pw = self.solver.state()
         return self._apply(ids, pose, pw, res)

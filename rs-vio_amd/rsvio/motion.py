@@ -17,8 +17,8 @@ from ._lib import check, ptr
 
 
 def pnp_cfg(max_iterations=10, cost_tolerance=1e-6, parameter_tolerance=1e-9, huber_delta=2.0, lambda_init=1e-4):
-    """sliding_window.rs:494-501 (+ HuberLoss::new(2.0) at :538)."""
-    return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init)
+    """sliding_window.rs:494-501 (SparseCholesky; + HuberLoss::new(2.0) at :538)."""
+    return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init, 1)
 
 
 @dataclass

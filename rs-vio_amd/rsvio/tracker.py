@@ -102,17 +102,19 @@ class StereoPatchTracker:
         if left.shape != (self.height, self.width) or right.shape != left.shape:
             raise ValueError(f"expected {self.height}x{self.width} images")
         nl, nr = C.c_size_t(0), C.c_size_t(0)
-        check(_lib.load().rsvio_tracker_process_frame(self._h, ptr(left), ptr(right), self.width,
-                                                      ptr(self._out_l), self.cap, C.byref(nl),
-                                                      ptr(self._out_r), self.cap, C.byref(nr)))
-        self._n = (nl.value, nr.value)
+        rc = _lib.load().rsvio_tracker_process_frame(self._h, ptr(left), ptr(right), self.width,
+                                                     ptr(self._out_l), self.cap, C.byref(nl),
+                                                     ptr(self._out_r), self.cap, C.byref(nr))
+        self._n = (nl.value, nr.value)  # RSVIO_ERR_CAPACITY still leaves consistent (truncated) lists
+        check(rc)
         return self._out_l[:nl.value].copy(), self._out_r[:nr.value].copy()
 
     def process_frame_device(self, d_left: int, d_right: int):
         nl, nr = C.c_size_t(0), C.c_size_t(0)
-        check(_lib.load().rsvio_tracker_process_frame_device(self._h, d_left, d_right, ptr(self._out_l), self.cap,
-                                                             C.byref(nl), ptr(self._out_r), self.cap, C.byref(nr)))
+        rc = _lib.load().rsvio_tracker_process_frame_device(self._h, d_left, d_right, ptr(self._out_l), self.cap,
+                                                            C.byref(nl), ptr(self._out_r), self.cap, C.byref(nr))
         self._n = (nl.value, nr.value)
+        check(rc)
         return nl.value, nr.value
 
     def get_track_points(self):
@@ -140,5 +142,13 @@ class StereoPatchTracker:
         return ul, ur
 
     def remove_id(self, ids):
+        """StereoPatchTracker::remove_id (feature_tracker.rs:201-206): the device lists are
+        compacted in order, so the cached lists are filtered the same way."""
         ids = np.ascontiguousarray(ids, np.uint64)
         check(_lib.load().rsvio_tracker_remove_ids(self._h, ptr(ids), len(ids)))
+        n = []
+        for out, k in ((self._out_l, self._n[0]), (self._out_r, self._n[1])):
+            keep = out[:k][~np.isin(out[:k]["id"], ids)]
+            out[:len(keep)] = keep
+            n.append(len(keep))
+        self._n = tuple(n)

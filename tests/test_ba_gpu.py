@@ -233,6 +233,24 @@ def test_async_solve_equals_run(gpu, cfg3):
     a.close()
 
 
+def test_async_wrong_call_order_refused(gpu, cfg3):
+    """Between rsvio_ba_run_async and rsvio_ba_wait, every entry point that reads or replaces
+    what the solve uses is refused with RSVIO_ERR_INVALID_ARG (the in-flight solve is intact)."""
+    a = _adjuster(gpu, cfg3)
+    ra = a.run()
+    pa, wa = a.state()
+    a.run_async()
+    for call in (lambda: a.state(), lambda: a.set_problem_from(cfg3), lambda: a.run_async()):
+        with pytest.raises(gpu.RsvioError) as e:
+            call()
+        assert e.value.code == -1
+    rb = a.wait()
+    pb, wb = a.state()
+    assert (ra.status, ra.iterations, ra.final_cost) == (rb.status, rb.iterations, rb.final_cost)
+    assert np.array_equal(pa, pb) and np.array_equal(wa, wb)
+    a.close()
+
+
 def _p2p_worker(rank, world, port, out_dir):
     import os
 
@@ -281,3 +299,51 @@ def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
     assert np.abs(r0["pose"] - po).max() < 1e-7
     pw = np.concatenate([r0["pw"], r1["pw"]])
     assert np.abs(pw - pwo).max() < 1e-6
+
+
+def _small_fallback_problem(seed=3):
+    from rsvio import synthetic as S
+    return S.ba_problem(n_kf=4, n_lm=40, kf_per_lm=3, seed=seed, init_seed=seed + 1)
+
+
+def test_cholesky_fallback_matches_oracle(gpu, oracle, cfg3):
+    """B3: the device's SparseCholesky fallback (landmarks eliminated first, 3x3 LL^T blocks) vs
+    the oracle's dense LL^T of the full damped system: same LM path, tolerance parity; and on
+    config 3 it takes the Schur solve's path (the two solvers differ only in rounding)."""
+    from rsvio.ba import SOLVER_CHOLESKY, lm_cfg
+    for prob in (_small_fallback_problem(), cfg3):
+        ba = _adjuster(gpu, prob)
+        r = ba.run(lm_cfg(linear_solver=SOLVER_CHOLESKY))
+        pose, pw = ba.state()
+        rs = ba.run(lm_cfg())
+        ps, ws = ba.state()
+        assert r.status > 0 and (r.status, r.iterations) == (rs.status, rs.iterations)
+        assert np.abs(pose - ps).max() < 1e-9 and np.abs(pw - ws).max() < 1e-8
+        if prob.n_lm <= 100:  # the oracle's dense full-system Cholesky is O(N^3)
+            po, pwo, ro = oracle.ba_solve(prob, oracle.lm_cfg(linear_solver=1))
+            assert (r.status, r.iterations) == (ro.status, ro.iterations)
+            assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6
+        ba.close()
+
+
+def test_singular_landmark_block_linear_solve_failed(gpu, oracle):
+    """B3: a singular landmark block (lambda_init 0, a landmark behind every camera) fails the
+    Schur solve with LinearSolveFailed at iteration 1 and the fallback the same way, as the
+    oracle does; the state is left at the initial values (the caller reverts)."""
+    import dataclasses
+
+    from rsvio.ba import LINEAR_SOLVE_FAILED, SOLVER_CHOLESKY, lm_cfg
+    base = _small_fallback_problem()
+    pw = base.p_W.copy()
+    pw[5] = 2.0 * base.p_W[0] - pw[5] * np.array([1.0, 1.0, -3.0])
+    pw[5, 2] = -abs(pw[5, 2]) - 5.0
+    prob = dataclasses.replace(base, p_W=pw)
+    ba = _adjuster(gpu, prob)
+    for ls in (0, SOLVER_CHOLESKY):
+        r = ba.run(lm_cfg(lambda_init=0.0, linear_solver=ls))
+        _, _, ro = oracle.ba_solve(prob, oracle.lm_cfg(lambda_init=0.0, linear_solver=ls))
+        assert (r.status, r.iterations) == (LINEAR_SOLVE_FAILED, 1) == (ro.status, ro.iterations)
+    r = ba.run(lm_cfg())  # default damping: solvable
+    _, _, ro = oracle.ba_solve(prob, oracle.lm_cfg())
+    assert r.status > 0 and (r.status, r.iterations) == (ro.status, ro.iterations)
+    ba.close()

@@ -289,3 +289,57 @@ def test_track_points_table_batched(gpu, oracle, stereo_frames):
         assert lib.rsvio_track_points_table_d(ctx, None, None, 3, 10, 20, C.c_float(0.01), None) < 0
     finally:
         lib.rsvio_track_ctx_destroy(ctx)
+
+
+def test_stereo_tracker_capacity_overflow(gpu, oracle, stereo_frames):
+    """max_features smaller than one frame's new points: both cameras admit the same leading
+    new points (ids consecutive, no unwritten slot counted), the call reports
+    RSVIO_ERR_CAPACITY, and the lists equal the first `cap` ids of the uncapped oracle."""
+    cap = 20
+    trk = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50, max_features=cap)
+    oracle.set_trig_mode(1)
+    try:
+        ref = oracle.StereoTracker(752, 480, 3, 50, 20, 0.01)
+        l0, r0 = stereo_frames[0]
+        rl, _ = ref.process_frame(l0, r0)
+        assert len(rl) > cap  # the uncapped tracker would exceed the capacity
+        with pytest.raises(gpu.RsvioError) as e:
+            trk.process_frame(l0, r0)
+        assert e.value.code == -4
+        fl, fr = trk.get_track_points()
+        assert sorted(fl) == list(range(cap)) and sorted(fr) == list(range(cap))
+        for k in range(cap):  # the admitted points are the oracle's first cap points
+            assert fl[k] == (rl[k][1], rl[k][2])
+        # the next frame continues from a full, consistent state: ids never exceed those issued
+        l1, r1 = stereo_frames[1]
+        try:
+            gl, gr = trk.process_frame(l1, r1)
+        except gpu.RsvioError as e2:
+            assert e2.code == -4
+        gl, gr = trk.get_track_points()
+        assert len(gl) <= cap and len(gr) <= cap
+        assert max(list(gl) + list(gr)) < 2 * cap
+    finally:
+        oracle.set_trig_mode(0)
+        trk.close()
+
+
+def test_stereo_tracker_remove_ids_undistorted(gpu, stereo_frames):
+    """remove_id keeps the fused unprojection aligned with the compacted feature lists."""
+    from rsvio.camera import EUROC
+    cl, cr = EUROC
+    trk = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50)
+    trk.set_cameras(cl, cr)
+    l0, r0 = stereo_frames[0]
+    l1, r1 = stereo_frames[1]
+    trk.process_frame(l0, r0)
+    fl, fr = trk.process_frame(l1, r1)
+    ul, ur = trk.undistorted()
+    drop = fl["id"][1::4]
+    trk.remove_id(drop)
+    kl, kr = ~np.isin(fl["id"], drop), ~np.isin(fr["id"], drop)
+    ul2, ur2 = trk.undistorted()
+    assert np.array_equal(ul2, ul[kl]) and np.array_equal(ur2, ur[kr])
+    pl, pr = trk.get_track_points()
+    assert sorted(pl) == sorted(fl["id"][kl].tolist()) and sorted(pr) == sorted(fr["id"][kr].tolist())
+    trk.close()

@@ -61,3 +61,8 @@ k = np.argmax(tot)
 print("slowest feature: cycles fwd %d bwd %d iterations %d valid %d" % (fw[k], bw[k], it[k], v[k]))
 span = st[:, 2].max() - st[:, 0].min()
 print("first start -> last end: %d cycles" % span)
+ph = st[:, 16:20].sum(0).astype(float)
+nit = max(it.sum(), 1)
+print("per-iteration phase cycles (mean over all iterations): gather+bilinear %.0f, sum chain + residual %.0f, "
+      "increment chains %.0f, exp/update/inbound %.0f" % tuple(ph / nit))
+print("template cycles (mean per template): %.0f" % (st[:, 20].sum() / max(1, (st[:, 20] > 0).sum() * 2 * L)))
