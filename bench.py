@@ -7,7 +7,9 @@ forward + backward) followed by one full sliding-window BA solve of config 3 (10
 KF_0 fixed, 2000 landmarks per GPU, 24,000 observations per GPU, LM to convergence, <= 20
 iterations) -- i.e. every frame is treated as a keyframe (worst case of estimator.rs:243-246).
 Inputs are resident in HBM before the timed region; nothing crosses PCIe inside a step except
-the LM status word the host loop reads once per iteration.
+the LM status word the host loop reads once per chunk of iterations.  `value_pcie` times the
+same step with its transfers inside (BASELINE.md protocol): image upload, feature lists and
+the BA state downloaded.
 
 Multi-GPU (torchrun, one process per GPU): the tracker runs as independent replicas (each rank
 its own stream); the BA is ONE problem whose landmarks are sharded 2000 per rank (weak scaling)
@@ -347,7 +349,7 @@ class _StageTimer:
         return self.be.set_map(*a)
 
 
-def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_seconds: float = 15.0):
+def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_seconds: float = 40.0):
     """BASELINE config 4 on one GPU: the Estimator (estimator.rs:101-262) over the device backend
     on a rendered stereo stream of textured planes (synthetic.euroc_scene_stream_device, frames
     resident in HBM): per frame the tracker (6 levels, grid 50, fused radtan unprojection), PnP +
@@ -399,10 +401,19 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=ob)
         t0 = time.perf_counter()
         k = 0
+        oerr = 0.0
+        # the whole stream when it fits the budget: the oracle's drift on the same frames is the
+        # correctness anchor of max_position_error_m (the reference's quirks -- identity poses
+        # until the window fills, depth-2.0 initialisation, f32 map -- drift alike)
         while k < len(host) and (time.perf_counter() - t0 < cpu_seconds or k < 30):
-            est.process_frame(*host[k])
+            ro = est.process_frame(*host[k])
+            oerr = max(oerr, float(np.linalg.norm(ro.T_W_B[:3, 3] - s.T_W_B[k][:3, 3])))
             k += 1
         cel = time.perf_counter() - t0
+        gerr_k = max(float(np.linalg.norm(r.T_W_B[:3, 3] - T[:3, 3])) for r, T in zip(out[:k], s.T_W_B[:k]))
+        row["oracle_max_position_error_m"] = round(oerr, 5)
+        row["oracle_frames"] = k
+        row["gpu_max_position_error_m_same_frames"] = round(gerr_k, 5)
         row["cpu_baseline"] = {"value": round(k / cel, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": f"the first {k} frames of the same stream through the same Estimator "
                                          "host logic over the oracle (oracle/estimator.py), 1 thread",
@@ -483,17 +494,29 @@ def measure_ft_row(device: int, cpu: bool, reps: int = 60):
     return row
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per dispatch of `kernel` (FETCH_SIZE + WRITE_SIZE) from the newest committed
-    PMC summary profiles/*_pmc_traffic.json (separate rocprofv3 --pmc passes of this same
-    bench command, tools/gpu_bench.sh + tools/pmc_summary.py), or None."""
+def pmc_traffic(kernel: str, shape: str = "u8_gath"):
+    """HBM bytes per dispatch of `kernel` from the newest committed PMC summary
+    profiles/*_pmc_traffic.json (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the
+    headline bench command, tools/gpu_round.sh + tools/pmc_summary.py), corrected as the
+    MI355X guide's HBM section prescribes: FETCH_SIZE x the multiplier measured for this access
+    shape by tools/fetch_calib.hip (profiles/*_fetch_calib.json; the guide's x2 for wide
+    16-B-per-lane reads when no calibration is committed), + WRITE_SIZE.  Returns
+    (corrected bytes, details) or (None, None)."""
     files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
     if not files:
         return None, None
     k = json.load(open(files[-1]))["kernels"].get(kernel)
     if not k:
         return None, None
-    return k["fetch_size_bytes_per_dispatch"] + k["write_size_bytes_per_dispatch"], files[-1].name
+    mult, msrc = 2.0, "guide x2 (wide reads)"
+    cal = sorted((ROOT / "profiles").glob("*_fetch_calib.json"))
+    if cal:
+        c = json.load(open(cal[-1]))["kernels"].get(shape)
+        if c and c.get("multiplier"):
+            mult, msrc = float(c["multiplier"]), f"{cal[-1].name}:{shape}"
+    f, w = k["fetch_size_bytes_per_dispatch"], k["write_size_bytes_per_dispatch"]
+    return f * mult + w, {"source": files[-1].name, "fetch_raw": round(f), "write_raw": round(w),
+                          "fetch_multiplier": round(mult, 4), "multiplier_source": msrc}
 
 
 def setup_dist(same_device: bool = False):
@@ -605,18 +628,35 @@ class TrackerWorkload:
         # prime: pyramids of the first frame
         self._pyramids(self.seq[0], self.slot)
 
-    def _pyramids(self, t, slot):
+    def _pyramids(self, t, slot, src=None):
         s = self.stream.cuda_stream
-        self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, self.imgs[t].data_ptr(), 2,
-                                                     self.pyr[slot].data_ptr(), s))
+        src = self.imgs[t] if src is None else src
+        self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, src.data_ptr(), 2, self.pyr[slot].data_ptr(), s))
 
-    def step(self, timed: bool):
-        """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches."""
+    def enable_pcie(self):
+        """Host-side buffers of the PCIe-inclusive step (GPU frames/sec includes the
+        image upload and the feature-list download): the frames in pinned host memory, a device
+        staging pair, pinned outputs."""
+        torch = self.torch
+        self.h_imgs = self.imgs.cpu().pin_memory()
+        self.d_stage = torch.empty_like(self.imgs[0])
+        self.h_out = torch.empty(self.out.shape, dtype=self.out.dtype).pin_memory()
+        self.h_valid = torch.empty(self.valid.shape, dtype=self.valid.dtype).pin_memory()
+
+    def step(self, timed: bool, pcie: bool = False):
+        """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches.  pcie:
+        the two images are uploaded from pinned host memory first and the three tracked
+        feature lists (+ valid flags) are downloaded before the step returns."""
         C = self.C
         t = self.seq[self.k % len(self.seq)]
         t2 = self.seq[(self.k + 1) % len(self.seq)]
         prev, cur = self.slot, 1 - self.slot
-        self._pyramids(t2, cur)
+        if pcie:
+            with self.torch.cuda.stream(self.stream):
+                self.d_stage.copy_(self.h_imgs[t2], non_blocking=True)
+            self._pyramids(t2, cur, self.d_stage)
+        else:
+            self._pyramids(t2, cur)
         b = (self.L.TrackBatch * 3)()
         spec = [(self.pyr[prev, 0], self.pyr[cur, 0], self.aff0[t]),
                 (self.pyr[prev, 1], self.pyr[cur, 1], self.aff1[t]),
@@ -632,10 +672,23 @@ class TrackerWorkload:
         if timed:
             e1.record(self.stream)
             self.ev.append((e0, e1))
+        if pcie:
+            with self.torch.cuda.stream(self.stream):
+                self.h_out.copy_(self.out, non_blocking=True)
+                self.h_valid.copy_(self.valid, non_blocking=True)
+            self.stream.synchronize()
         self.slot = cur
         self.k += 1
 
     def close(self):
+        # pinned blocks carry events recorded on the tracker stream: drain and release them while
+        # that stream exists (it is destroyed with the CU-mask streams after this)
+        self.torch.cuda.synchronize()
+        for k in ("h_imgs", "h_out", "h_valid", "d_stage"):
+            self.__dict__.pop(k, None)
+        host_empty = getattr(self.torch._C, "_host_emptyCache", None)
+        if host_empty:
+            host_empty()
         if self.ctx:
             self.lib.rsvio_track_ctx_destroy(self.ctx)
             self.ctx = None
@@ -812,8 +865,20 @@ class BAWorkload:
         return r
 
 
-def cpu_baseline(frames_budget_s: float):
-    """The oracle (C++ restatement of the reference) on the host: same tracker frame + BA solve."""
+def host_cores() -> int:
+    """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS, set per GPU on
+    the pool) or the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(frames_budget_s: float, threads: int = 1):
+    """The oracle (C++ restatement of the reference) on the host: same tracker frame + BA solve.
+    threads > 1 mirrors the reference's rayon parallelism: per-level pyramids
+    (feature_tracker.rs:213) and per-feature track_points (:260) over `threads` threads; the BA
+    solve stays single-threaded like apex's per-block loop."""
     from oracle import oracle as O
     from rsvio import synthetic as S
     frames = list(S.stereo_sequence(2, W, H))
@@ -827,10 +892,10 @@ def cpu_baseline(frames_budget_s: float):
     t_start = time.perf_counter()
     while time.perf_counter() - t_start < frames_budget_s or n < 2:
         t0 = time.perf_counter()
-        pc = [O.build_pyramid(frames[1][c], LEVELS) for c in range(2)]
-        O.track_points(pyr_prev[0], pc[0], W, H, LEVELS, aff0, MAX_IT, THRESH)
-        O.track_points(pyr_prev[1], pc[1], W, H, LEVELS, aff1, MAX_IT, THRESH)
-        O.track_points(pc[0], pc[1], W, H, LEVELS, affn, MAX_IT, THRESH)
+        pc = [O.build_pyramid(frames[1][c], LEVELS, threads) for c in range(2)]
+        O.track_points(pyr_prev[0], pc[0], W, H, LEVELS, aff0, MAX_IT, THRESH, threads)
+        O.track_points(pyr_prev[1], pc[1], W, H, LEVELS, aff1, MAX_IT, THRESH, threads)
+        O.track_points(pc[0], pc[1], W, H, LEVELS, affn, MAX_IT, THRESH, threads)
         t1 = time.perf_counter()
         _, _, r = O.ba_solve(prob)
         t2 = time.perf_counter()
@@ -838,9 +903,11 @@ def cpu_baseline(frames_budget_s: float):
         t_ba += t2 - t1
         n += 1
     fps = n / (t_track + t_ba)
-    return {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+    return {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{n} frames of config 2 (2 pyramids + 3x300 track_points) each followed by one config-3 "
-                      f"BA solve ({r.iterations} LM iterations), oracle/ C++ restatement, 1 thread",
+                      f"BA solve ({r.iterations} LM iterations), oracle/ C++ restatement, "
+                      + ("1 thread" if threads == 1 else
+                         f"{threads} threads (pyramid levels and features in parallel, BA 1 thread)"),
             "tracker_ms_per_frame": round(1e3 * t_track / n, 3), "ba_ms_per_solve": round(1e3 * t_ba / n, 3),
             "ba_ms_per_iter": round(1e3 * t_ba / n / max(r.iterations, 1), 3)}
 
@@ -902,6 +969,23 @@ def main():
     barrier(world)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world)
+    # the same step with its PCIe traffic inside (BASELINE.md protocol): images uploaded from
+    # pinned host memory, the three feature lists and the BA's optimised state downloaded
+    trk.enable_pcie()
+    for _ in range(2):
+        ba.start()
+        trk.step(False, pcie=True)
+        ba.finish(False)
+        ba.ba.state()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ba.start()
+        trk.step(False, pcie=True)
+        ba.finish(False)
+        ba.ba.state()
+    barrier(world)
+    elapsed_pcie = max_over_ranks(time.perf_counter() - t0, world)
 
     frames = world * args.steps
     value = frames / elapsed
@@ -923,6 +1007,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "value_pcie": round(world * args.steps / elapsed_pcie, 3),
+        "ms_per_step_pcie": round(1e3 * elapsed_pcie / args.steps, 4),
+        "pcie_note": "value_pcie: the same step with 2 x 361 KB image H2D (pinned), 3 x 300 feature "
+                     "states + valid flags D2H and the BA state (48.6 KB) D2H inside the timed region",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -945,7 +1033,7 @@ def main():
         "roofline": {"kernel": "lk_track_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": None if traffic is None else round(traffic),
-                     "traffic_source": traffic_src,
+                     "traffic_detail": traffic_src,
                      "algorithmic_bytes_per_launch": lk_bytes, "launch_ms": round(lk_ms, 4),
                      "note": "latency-bound: 900 one-wave workgroups (fwd+bwd chains) on 256 CUs"},
         "ba_roofline": {"bound": "fp64", "flop_per_iter": flops,
@@ -960,10 +1048,16 @@ def main():
         out.setdefault("rows", {})["pipeline_config4"] = measure_pipeline_row(
             local, cpu=(world == 1 and not args.no_cpu), n_frames=args.pipeline_frames)
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(args.cpu_seconds)
-        cb["cores"] = 1
+        # two legs -- all host cores (the reported baseline, rayon's parallelism) and
+        # one thread -- each a bounded sample of the same per-frame work
+        cores = host_cores()
+        cb = cpu_baseline(args.cpu_seconds, cores)
+        cb1 = cpu_baseline(args.cpu_seconds / 2, 1)
+        cb["single_thread"] = {k: cb1[k] for k in ("value", "cores", "sample", "tracker_ms_per_frame",
+                                                   "ba_ms_per_solve", "ba_ms_per_iter")}
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 2)
+        out["speedup_vs_cpu_single_thread"] = round(value / cb1["value"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -72,6 +72,7 @@ _SIG = {
     "orc_pyramid_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "orc_pyramid_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "orc_build_pyramid": (None, [P, C.c_int, C.c_int, C.c_int, P]),
+    "orc_build_pyramid_mt": (None, [P, C.c_int, C.c_int, C.c_int, P, C.c_int]),
     "orc_resize_triangle": (None, [P, C.c_int, C.c_int, P, C.c_int, C.c_int]),
     "orc_pattern52_new": (C.c_int, [P, C.c_int, C.c_int, C.c_float, C.c_float, P, P, P]),
     "orc_track_one_point": (C.c_int, [P, P, C.c_int, C.c_int, C.c_int, P, C.c_int, C.c_float, P]),
@@ -137,11 +138,14 @@ def pyramid_bytes(w, h, levels):
     return int(load().orc_pyramid_bytes(w, h, levels))
 
 
-def build_pyramid(img: np.ndarray, levels: int) -> np.ndarray:
+def build_pyramid(img: np.ndarray, levels: int, n_threads: int = 1) -> np.ndarray:
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     out = np.empty(pyramid_bytes(w, h, levels), np.uint8)
-    load().orc_build_pyramid(_p(img), w, h, levels, _p(out))
+    if n_threads > 1:
+        load().orc_build_pyramid_mt(_p(img), w, h, levels, _p(out), n_threads)
+    else:
+        load().orc_build_pyramid(_p(img), w, h, levels, _p(out))
     return out
 
 

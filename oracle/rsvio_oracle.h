@@ -45,6 +45,7 @@ size_t orc_pyramid_offset(int w, int h, int level);
 size_t orc_pyramid_bytes(int w, int h, int levels);
 
 /* feature_tracker.rs:209-220 (imageops::resize Triangle from full resolution per level) */
+void orc_build_pyramid_mt(const uint8_t* img, int w, int h, int levels, uint8_t* out, int n_threads);
 void orc_build_pyramid(const uint8_t* img, int w, int h, int levels, uint8_t* out);
 
 /* image 0.25 imageops::resize(.., FilterType::Triangle), u8 luma */

@@ -607,6 +607,22 @@ void orc_build_pyramid(const uint8_t* img, int w, int h, int levels, uint8_t* ou
     }
 }
 
+// build_image_pyramid with rayon's par_iter over levels (feature_tracker.rs:213): one thread
+// per level (the all-cores CPU baseline); the same bytes as orc_build_pyramid
+void orc_build_pyramid_mt(const uint8_t* img, int w, int h, int levels, uint8_t* out, int n_threads) {
+    if (n_threads <= 1 || levels < 2) {
+        orc_build_pyramid(img, w, h, levels, out);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int i = 0; i < levels; ++i)
+        th.emplace_back([=] {
+            int nw = (int)((uint32_t)w / (1u << i)), nh = (int)((uint32_t)h / (1u << i));
+            orc_resize_triangle(img, w, h, out + orc_pyramid_offset(w, h, i), nw, nh);
+        });
+    for (auto& t : th) t.join();
+}
+
 int orc_pattern52_new(const uint8_t* img, int w, int h, float px, float py, float* out_data,
                       float* out_hinvjt, float* out_mean) {
     Img im{img, (uint32_t)w, (uint32_t)h};

@@ -202,64 +202,110 @@ struct Template {
     float h0, h1, h2;  // this lane's column of H^-1 J^T
 };
 
-// Pattern52::new (patch.rs:124-162) + set_data_jac_se2 (:75-123)
-__device__ bool make_template(const LevelImg& im, float posx, float posy, int lane, float patx,
-                              float paty, Template& T, float* sh) {
+__device__ __forceinline__ LevelImg level_of(const uint8_t* pyr, uint32_t w, uint32_t h, int i) {
+    LevelImg L;
+    L.p = pyr + level_offset(w, h, i);
+    L.w = level_w(w, i);
+    L.h = level_h(h, i);
+    return L;
+}
+
+// Pattern52::new (patch.rs:124-162 + set_data_jac_se2 :75-123) for every level of a pyramid at
+// once, level i at (posx, posy) / 2^i -- the templates track_one_point builds level by level
+// (feature_tracker.rs:310-314).  They are independent, so one pass overlaps them: the 12-pixel
+// image_grad crosses of all levels are in flight together, the 4L normalisation sums run as one
+// lane_chains<4L> (chain j in lane j, each in the reference's order) and the 6L entries of H
+// as one lane_chains<6L>; the L 3x3 Cholesky solves interleave.  Every value is the one the
+// per-level build computes (same f32 operations), so tracks stay bit-exact.
+// Levels [L0, L0 + K) of the L templates (K <= 4 keeps the chain values within the VGPR file).
+template <int L, int L0, int K>
+__device__ void make_templates_part(const uint8_t* pyr, uint32_t w, uint32_t h, float posx, float posy, int lane,
+                                    Template (&T)[L], bool (&ok)[L], float* sh) {
     const bool act = lane < NP;
     const float ox = act ? (float)kPattern[lane][0] : 0.0f;
     const float oy = act ? (float)kPattern[lane][1] : 0.0f;
-    const float qx = posx + ox / 2.0f, qy = posy + oy / 2.0f;
     const float jw02 = -oy / 2.0f, jw12 = ox / 2.0f;
-    const bool in = act && inbound(im, qx, qy, 2);
-    float v = 0.0f, J0 = 0.0f, J1 = 0.0f, J2 = 0.0f;
-    if (in) {
-        float vg[3];
-        image_grad(im, qx, qy, vg);
-        v = vg[0];
-        J0 = vg[1] * 1.0f + vg[2] * 0.0f;
-        J1 = vg[1] * 0.0f + vg[2] * 1.0f;
-        J2 = vg[1] * jw02 + vg[2] * jw12;
+    float v[K], J0[K], J1[K], J2[K];
+    bool in[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float sdn = (float)(1 << (L0 + i));
+        const LevelImg im = level_of(pyr, w, h, L0 + i);
+        const float qx = posx / sdn + ox / 2.0f, qy = posy / sdn + oy / 2.0f;
+        in[i] = act && inbound(im, qx, qy, 2);
+        // every lane samples (an out-of-bound one at a safe dummy spot, its values discarded):
+        // no branch around the loads, so all levels' gathers are in flight together
+        // (levels under 5 x 5 have no in-bound point and are not sampled at all)
+        float vg[3] = {0.0f, 0.0f, 0.0f};
+        if (im.w >= 5 && im.h >= 5) image_grad(im, in[i] ? qx : 2.0f, in[i] ? qy : 2.0f, vg);
+        v[i] = in[i] ? vg[0] : 0.0f;
+        J0[i] = in[i] ? vg[1] * 1.0f + vg[2] * 0.0f : 0.0f;
+        J1[i] = in[i] ? vg[1] * 0.0f + vg[2] * 1.0f : 0.0f;
+        J2[i] = in[i] ? vg[1] * jw02 + vg[2] * jw12 : 0.0f;
     }
-    float data = in ? v : -1.0f;
-    float s4[4];
-    {
-        const float x4[4] = {in ? v : 0.0f, in ? J0 : 0.0f, in ? J1 : 0.0f, in ? J2 : 0.0f};
-        lane_chains<4, true>(x4, s4, sh, lane);
+    float x4[4 * K], s4[4 * K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        x4[4 * i] = in[i] ? v[i] : 0.0f;
+        x4[4 * i + 1] = in[i] ? J0[i] : 0.0f;
+        x4[4 * i + 2] = in[i] ? J1[i] : 0.0f;
+        x4[4 * i + 3] = in[i] ? J2[i] : 0.0f;
     }
-    const float sum = s4[0], gs0 = s4[1], gs1 = s4[2], gs2 = s4[3];
-    const int nvalid = __popcll(__ballot(in));
-    const float mean = sum / (float)nvalid;
-    const float mean_inv = (float)nvalid / sum;
-    if (data >= 0.0f) {
-        J0 = J0 + (-(gs0 * data / sum));
-        J1 = J1 + (-(gs1 * data / sum));
-        J2 = J2 + (-(gs2 * data / sum));
-        data *= mean_inv;
-    } else {
-        J0 = J1 = J2 = 0.0f;
+    lane_chains<4 * K, true>(x4, s4, sh, lane);
+    float x6[6 * K], h6[6 * K], mean[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float sum = s4[4 * i], gs0 = s4[4 * i + 1], gs1 = s4[4 * i + 2], gs2 = s4[4 * i + 3];
+        const int nvalid = __popcll(__ballot(in[i]));
+        mean[i] = sum / (float)nvalid;
+        const float mean_inv = (float)nvalid / sum;
+        float data = in[i] ? v[i] : -1.0f;
+        float a0 = J0[i], a1 = J1[i], a2 = J2[i];
+        if (data >= 0.0f) {
+            a0 = a0 + (-(gs0 * data / sum));
+            a1 = a1 + (-(gs1 * data / sum));
+            a2 = a2 + (-(gs2 * data / sum));
+            data *= mean_inv;
+        } else {
+            a0 = a1 = a2 = 0.0f;
+        }
+        J0[i] = a0 * mean_inv;
+        J1[i] = a1 * mean_inv;
+        J2[i] = a2 * mean_inv;
+        T[L0 + i].data = data;
+        x6[6 * i] = J0[i] * J0[i];
+        x6[6 * i + 1] = J0[i] * J1[i];
+        x6[6 * i + 2] = J0[i] * J2[i];
+        x6[6 * i + 3] = J1[i] * J1[i];
+        x6[6 * i + 4] = J1[i] * J2[i];
+        x6[6 * i + 5] = J2[i] * J2[i];
     }
-    J0 *= mean_inv;
-    J1 *= mean_inv;
-    J2 *= mean_inv;
-    float H[3][3];
-    {
-        const float x6[6] = {J0 * J0, J0 * J1, J0 * J2, J1 * J1, J1 * J2, J2 * J2};
-        float h6[6];
-        lane_chains<6, false>(x6, h6, sh, lane);
-        H[0][0] = h6[0]; H[0][1] = h6[1]; H[0][2] = h6[2]; H[1][1] = h6[3]; H[1][2] = h6[4]; H[2][2] = h6[5];
+    lane_chains<6 * K, false>(x6, h6, sh, lane);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        float H[3][3], Hi[3][3];
+        H[0][0] = h6[6 * i]; H[0][1] = h6[6 * i + 1]; H[0][2] = h6[6 * i + 2];
+        H[1][1] = h6[6 * i + 3]; H[1][2] = h6[6 * i + 4]; H[2][2] = h6[6 * i + 5];
+        H[1][0] = H[0][1];
+        H[2][0] = H[0][2];
+        H[2][1] = H[1][2];
+        Template& t = T[L0 + i];
+        ok[L0 + i] = chol_inv3(H, Hi);
+        if (!ok[L0 + i]) continue;
+        t.h0 = Hi[0][2] * J2[i] + (Hi[0][1] * J1[i] + Hi[0][0] * J0[i]);
+        t.h1 = Hi[1][2] * J2[i] + (Hi[1][1] * J1[i] + Hi[1][0] * J0[i]);
+        t.h2 = Hi[2][2] * J2[i] + (Hi[2][1] * J1[i] + Hi[2][0] * J0[i]);
+        const bool fin = !act || (isfinite(t.h0) && isfinite(t.h1) && isfinite(t.h2) && isfinite(t.data));
+        const bool all_fin = __ballot(!fin) == 0ull;
+        ok[L0 + i] = (mean[i] > __FLT_EPSILON__) && all_fin;
     }
-    H[1][0] = H[0][1];
-    H[2][0] = H[0][2];
-    H[2][1] = H[1][2];
-    float Hi[3][3];
-    T.data = data;
-    if (!chol_inv3(H, Hi)) return false;
-    T.h0 = Hi[0][2] * J2 + (Hi[0][1] * J1 + Hi[0][0] * J0);
-    T.h1 = Hi[1][2] * J2 + (Hi[1][1] * J1 + Hi[1][0] * J0);
-    T.h2 = Hi[2][2] * J2 + (Hi[2][1] * J1 + Hi[2][0] * J0);
-    const bool fin = !act || (isfinite(T.h0) && isfinite(T.h1) && isfinite(T.h2) && isfinite(data));
-    const bool all_fin = __ballot(!fin) == 0ull;
-    return (mean > __FLT_EPSILON__) && all_fin;
+}
+
+template <int L>
+__device__ void make_templates(const uint8_t* pyr, uint32_t w, uint32_t h, float posx, float posy, int lane,
+                               Template (&T)[L], bool (&ok)[L], float* sh) {
+    make_templates_part<L, 0, (L < 4 ? L : 4)>(pyr, w, h, posx, posy, lane, T, ok, sh);
+    if constexpr (L > 4) make_templates_part<L, 4, L - 4>(pyr, w, h, posx, posy, lane, T, ok, sh);
 }
 
 // track_point_at_level (feature_tracker.rs:344-395) with Pattern52::residual (patch.rs:163-232)
@@ -327,33 +373,47 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
     return true;
 }
 
-__device__ __forceinline__ LevelImg level_of(const uint8_t* pyr, uint32_t w, uint32_t h, int i) {
-    LevelImg L;
-    L.p = pyr + level_offset(w, h, i);
-    L.w = level_w(w, i);
-    L.h = level_h(h, i);
-    return L;
-}
-
-// track_one_point (feature_tracker.rs:292-342)
-__device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, uint32_t h, int levels,
-                          const Aff& T0, int lane, float patx, float paty, int max_iter, float thresh,
-                          Aff& out, float* sh) {
+// track_one_point (feature_tracker.rs:292-342): the L templates first (make_templates), then
+// the levels coarse to fine; an invalid template fails the call when its level is reached, as
+// the reference's level-by-level build does.
+template <int L>
+__device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, uint32_t h, const Aff& T0, int lane,
+                          float patx, float paty, int max_iter, float thresh, Aff& out, float* sh, float* tsh) {
+    uint32_t tok_mask = 0;
+    {
+        Template tp[L];
+        bool tok[L];
+        LK_CLK(m0);
+        make_templates<L>(pyr0, w, h, T0.m02, T0.m12, lane, tp, tok, sh);
+        LK_CLK(m1);
+        LK_ACC(20, m0, m1);
+        // park the templates in LDS so the level loop below is not unrolled (one inlined
+        // track_at_level per direction; tsh: [level][4][64] floats of this wave)
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            tsh[(4 * i + 0) * 64 + lane] = tp[i].data;
+            tsh[(4 * i + 1) * 64 + lane] = tp[i].h0;
+            tsh[(4 * i + 2) * 64 + lane] = tp[i].h1;
+            tsh[(4 * i + 3) * 64 + lane] = tp[i].h2;
+            tok_mask |= tok[i] ? (1u << i) : 0u;
+        }
+    }
     Aff T1;
     T1.m00 = 1.0f; T1.m01 = 0.0f; T1.m10 = 0.0f; T1.m11 = 1.0f;
     T1.m20 = 0.0f; T1.m21 = 0.0f; T1.m22 = 1.0f;
     T1.m02 = T0.m02;
     T1.m12 = T0.m12;
-    for (int i = levels - 1; i >= 0; --i) {
+#pragma unroll 1
+    for (int i = L - 1; i >= 0; --i) {
         const float sdn = (float)(1 << i);
         T1.m02 /= sdn;
         T1.m12 /= sdn;
+        if (!((tok_mask >> i) & 1u)) return false;
         Template tp;
-        LK_CLK(m0);
-        const bool tok = make_template(level_of(pyr0, w, h, i), T0.m02 / sdn, T0.m12 / sdn, lane, patx, paty, tp, sh);
-        LK_CLK(m1);
-        LK_ACC(20, m0, m1);
-        if (!tok) return false;
+        tp.data = tsh[(4 * i + 0) * 64 + lane];
+        tp.h0 = tsh[(4 * i + 1) * 64 + lane];
+        tp.h1 = tsh[(4 * i + 2) * 64 + lane];
+        tp.h2 = tsh[(4 * i + 3) * 64 + lane];
         if (!track_at_level(level_of(pyr1, w, h, i), tp, patx, paty, lane, T1, max_iter, thresh, sh))
             return false;
         T1.m02 *= sdn;
@@ -368,37 +428,39 @@ __device__ bool track_one(const uint8_t* pyr0, const uint8_t* pyr1, uint32_t w, 
     return true;
 }
 
-__global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
+template <int L>
+__global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch P) {
     // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of jobs (whole
     // batches, i.e. 2 of the 4 pyramids) so its L2 fetches only what its features read
-    const int per = (L.njobs + kXcds - 1) / kXcds;
+    const int per = (P.njobs + kXcds - 1) / kXcds;
     const int job = (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
-    if (job >= L.njobs) return;
+    if (job >= P.njobs) return;
     const uint8_t* pyr0;
     const uint8_t* pyr1;
     const float* ain;
     float* aout;
     uint8_t* valid;
     int idx;
-    if (L.table != nullptr) {
+    if (P.table != nullptr) {
         // largest b with tstart[b] <= job (binary search over the device prefix)
-        int lo = 0, hi = L.nb - 1;
+        int lo = 0, hi = P.nb - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (L.tstart[mid] <= job) lo = mid; else hi = mid - 1;
+            if (P.tstart[mid] <= job) lo = mid; else hi = mid - 1;
         }
-        const rsvio_track_batch& d = L.table[lo];
-        idx = job - L.tstart[lo];
+        const rsvio_track_batch& d = P.table[lo];
+        idx = job - P.tstart[lo];
         if (idx < 0 || idx >= d.n) return;  // a malformed caller prefix never indexes out of a batch
         pyr0 = d.d_pyr0; pyr1 = d.d_pyr1; ain = d.d_aff_in; aout = d.d_aff_out; valid = d.d_valid;
     } else {
         int b = 0;
-        while (b + 1 < L.nb && job >= L.start[b + 1]) ++b;
-        idx = job - L.start[b];
-        if (L.dcount[b] != nullptr && idx >= *L.dcount[b]) return;
-        pyr0 = L.pyr0[b]; pyr1 = L.pyr1[b]; ain = L.ain[b]; aout = L.aout[b]; valid = L.valid[b];
+        while (b + 1 < P.nb && job >= P.start[b + 1]) ++b;
+        idx = job - P.start[b];
+        if (P.dcount[b] != nullptr && idx >= *P.dcount[b]) return;
+        pyr0 = P.pyr0[b]; pyr1 = P.pyr1[b]; ain = P.ain[b]; aout = P.aout[b]; valid = P.valid[b];
     }
-    __shared__ __attribute__((aligned(16))) float sh[6 * kChainLd];
+    __shared__ __attribute__((aligned(16))) float sh[6 * (L < 4 ? L : 4) * kChainLd];
+    __shared__ float tsh[4 * L * 64];
     const int lane = threadIdx.x;
     const float patx = lane < NP ? (float)kPattern[lane][0] / 2.0f : 0.0f;
     const float paty = lane < NP ? (float)kPattern[lane][1] / 2.0f : 0.0f;
@@ -412,12 +474,9 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch L) {
         for (int k = 15; k <= 20; ++k) g_dbg[blockIdx.x * 32 + k] = 0;
 #endif
     STAMP(0);
-    bool ok = track_one(pyr0, pyr1, L.w, L.h, L.levels, T0, lane, patx, paty, L.max_iter,
-                        L.thresh, fwd, sh);
+    bool ok = track_one<L>(pyr0, pyr1, P.w, P.h, T0, lane, patx, paty, P.max_iter, P.thresh, fwd, sh, tsh);
     STAMP(1);
-    if (ok)
-        ok = track_one(pyr1, pyr0, L.w, L.h, L.levels, fwd, lane, patx, paty, L.max_iter,
-                       L.thresh, bwd, sh);
+    if (ok) ok = track_one<L>(pyr1, pyr0, P.w, P.h, fwd, lane, patx, paty, P.max_iter, P.thresh, bwd, sh, tsh);
     STAMP(2);
     if (ok) {
         // feature_tracker.rs:277-281: squared translation distance < 0.4
@@ -445,7 +504,13 @@ void enqueue_track(const TrackLaunch& L0, hipStream_t s) {
     if (total <= 0) return;
     L.njobs = total;
     const int grid = ((total + kXcds - 1) / kXcds) * kXcds;
-    hipLaunchKernelGGL(lk_track_kernel, dim3(grid), dim3(64), 0, s, L);
+    switch (L.levels) {  // one instantiation per pyramid depth (make_templates<L>)
+#define RSVIO_LK(NL) \
+    case NL: hipLaunchKernelGGL(lk_track_kernel<NL>, dim3(grid), dim3(64), 0, s, L); break;
+        RSVIO_LK(1) RSVIO_LK(2) RSVIO_LK(3) RSVIO_LK(4) RSVIO_LK(5) RSVIO_LK(6) RSVIO_LK(7) RSVIO_LK(8)
+#undef RSVIO_LK
+        default: throw std::invalid_argument("track_points: levels must be in [1, 8]");
+    }
     RSVIO_HIP(hipGetLastError());
 }
 

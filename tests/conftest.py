@@ -38,7 +38,16 @@ def stereo_frames():
 
 
 @pytest.fixture(scope="session")
-def scene_stream():
-    """Config 4's rendered stereo stream, shortened: 24 frames, window 5."""
+def scene_stream_long():
+    """Config 4's rendered stereo stream at the reference window: 72 frames,
+    config/euroc_vio.yaml's keyframe_window_size 10 (30 keyframes, 21 full-window solves)."""
     from rsvio import synthetic as S
-    return S.euroc_scene_stream(24), 5
+    return S.euroc_scene_stream(72), 10
+
+
+@pytest.fixture(scope="session")
+def scene_stream(scene_stream_long):
+    """The same stream shortened: its first 24 frames, window 5."""
+    import dataclasses
+    s, _ = scene_stream_long
+    return dataclasses.replace(s, frames=s.frames[:24], T_W_B=s.T_W_B[:24]), 5

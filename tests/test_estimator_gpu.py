@@ -3,9 +3,13 @@ with fused unprojection, PnP + keyframe rule, BA -- against the same host logic 
 backend (oracle/estimator.py), frame by frame on the rendered stream.
 
 Parity: features (ids, f32 undistorted coordinates) bit-exact every frame (trig mode 1, the
-oracle's device-matched sin/cos); integer outcomes (keyframe flag, PnP status, BA status) equal;
-poses within 1e-6 m / rad -- BA and PnP agree to 1e-7 per solve (test_ba_gpu, test_motion_gpu)
-and map points are narrowed to f32 between solves, so differences may carry over frames.
+oracle's device-matched sin/cos); keyframe flags equal; PnP and BA outcomes equal in class
+(ran / success / failure); poses within 1e-6 m / rad -- BA and PnP agree to 1e-7 per solve
+(test_ba_gpu, test_motion_gpu) and map points are narrowed to f32 between solves, so
+differences may carry over frames.  The termination REASON of a converged LM (cost tolerance 1
+vs parameter tolerance 2) is a threshold test on values the GPU reduces in a different fixed
+order, so it may flip on a frame whose last step sits at the threshold: such flips are counted
+and must stay rare (<= 1 in 20 frames), and the poses still agree to the tolerance.
 """
 import numpy as np
 import pytest
@@ -31,11 +35,10 @@ class _Spy:
         return getattr(self.be, k)
 
 
-def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
+def _compare_with_oracle(oracle, s, win):
     from oracle.estimator import OracleBackend
     from rsvio.camera import Camera
     from rsvio.estimator import DeviceBackend, Estimator
-    s, win = scene_stream
     h, w = s.frames[0][0].shape
     cams = [Camera.opencv5(*p) for p in s.intrinsics]
     oracle.set_trig_mode(1)
@@ -44,7 +47,7 @@ def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
         orc = _Spy(OracleBackend(oracle, w, h, cams))
         ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev)
         eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=orc)
-        n_kf = 0
+        n_kf = flips = 0
         for k, (l, r) in enumerate(s.frames):
             rd = ed.process_frame(l, r)
             ro = eo.process_frame(l, r)
@@ -52,10 +55,13 @@ def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
                 assert np.array_equal(ids_d, ids_o), f"frame {k}"
                 assert np.array_equal(np.asarray(uv_d, np.float32).view(np.uint32),
                                       np.asarray(uv_o, np.float32).view(np.uint32)), f"frame {k}"
-            assert (rd.is_keyframe, rd.pnp_status, rd.ba_status) == (ro.is_keyframe, ro.pnp_status, ro.ba_status), \
-                f"frame {k}"
+            assert rd.is_keyframe == ro.is_keyframe, f"frame {k}"
+            for a, b in ((rd.pnp_status, ro.pnp_status), (rd.ba_status, ro.ba_status)):
+                assert (a is None) == (b is None) and (a is None or (a > 0) == (b > 0)), f"frame {k}: {a} vs {b}"
+            flips += (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)
             assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
             n_kf += rd.is_keyframe
+        assert flips <= max(1, len(s.frames) // 20), flips
         for Td, To in zip(ed.trajectory(), eo.trajectory()):
             assert np.abs(Td - To).max() <= POSE_TOL
         assert win < n_kf < len(s.frames)
@@ -63,8 +69,25 @@ def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
         assert sorted(md) == sorted(mo)
         assert max(np.abs(md[i].astype(np.float64) - mo[i]).max() for i in md) <= 1e-5
         dev.be.close()
+        return n_kf, ed.window.fallbacks + eo.window.fallbacks
     finally:
         oracle.set_trig_mode(0)
+
+
+def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
+    s, win = scene_stream
+    _compare_with_oracle(oracle, s, win)
+
+
+def test_estimator_matches_oracle_window10(gpu, oracle, scene_stream_long):
+    """config/euroc_vio.yaml's values -- L = 6, grid 50, 20 iterations, threshold 0.01,
+    keyframe_window_size 10, keyframe thresholds 0.05 / 0.05 -- over 72 frames: the first 10
+    keyframes fill the window (pose I, estimator.rs:195), then PnP every frame and a full-window
+    BA at every keyframe (21 solves), frame by frame against the oracle backend."""
+    s, win = scene_stream_long
+    assert win == 10 and len(s.frames) >= 60
+    n_kf, _ = _compare_with_oracle(oracle, s, win)
+    assert n_kf >= win + 15
 
 
 def test_estimator_pipelined_matches_sequential(gpu, scene_stream):
