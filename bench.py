@@ -512,7 +512,9 @@ def pmc_traffic(kernel: str, shape: str = "u8_gath"):
     cal = sorted((ROOT / "profiles").glob("*_fetch_calib.json"))
     if cal:
         c = json.load(open(cal[-1]))["kernels"].get(shape)
-        if c and c.get("multiplier"):
+        # a calibration outside [1, 8] is a broken measurement (e.g. loads the compiler deleted),
+        # never a counter correction: keep the guide's x2 then
+        if c and c.get("multiplier") and 1.0 <= float(c["multiplier"]) <= 8.0:
             mult, msrc = float(c["multiplier"]), f"{cal[-1].name}:{shape}"
     f, w = k["fetch_size_bytes_per_dispatch"], k["write_size_bytes_per_dispatch"]
     return f * mult + w, {"source": files[-1].name, "fetch_raw": round(f), "write_raw": round(w),

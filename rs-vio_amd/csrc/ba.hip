@@ -40,12 +40,18 @@
 
 #include "common.hpp"
 #include "se3.hpp"
+#include "wave.hpp"
+
+// HP-B is f64 with tolerance parity: multiply-adds contract to FMAs
+// here, unlike the tracker's bit-exact f32 code (built with -ffp-contract=off)
+#pragma clang fp contract(fast)
 
 namespace rsvio {
 
 namespace {
 
 RSVIO_DBG_DECL
+RSVIO_RT_DECL
 
 constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
 constexpr int kMaxN = 6 * kMaxFree;
@@ -56,6 +62,12 @@ enum { LV = 0, LG = 6, kLmF = 12 };
 constexpr int kBlockF = 48;             // 36 S + 6 b + 6 g_c per camera block workgroup
 constexpr int kPartA = 2;               // cost of the initial linearisation, 0 (per wave)
 constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per wave
+// Landmark groups of the Schur reduction: wave w (K4 / K6 workgroup w, dispatched round robin to
+// XCD w % 8) belongs to group w % kGrp, and K4c workgroup 4 pb + g (on XCD g or g + 4) reduces
+// block pb over group g -- each slot record is fetched into at most two XCDs' L2 per launch,
+// and K5 sums kGrp partial systems (fewer copies: less to pull across the fabric into one CU)
+constexpr int kGrp = 4;
+constexpr int kSchurThreads = 512;      // K4c workgroup: one pair per thread per pass
 
 struct Mat4 {
     double m[16];
@@ -139,17 +151,21 @@ __device__ __forceinline__ int utri(int a, int c) {  // index of (min, max) in a
     return i * 6 - i * (i - 1) / 2 + (j - i);
 }
 
-// LM bookkeeping that lives on the device (read back once per chunk of iterations)
+// LM bookkeeping that lives on the device.  Two copies alternate by iteration: iteration i's
+// K4c reads copy i & 1 (the state left by iteration i-1, with its trial pending), takes the
+// pending decision and writes the decided state to copy (i+1) & 1, which K5 / K6 of iteration i
+// then use -- so no workgroup ever reads a copy another workgroup of the same launch writes.
 struct LmState {
     double lambda, nu, cost, initial_cost;
     double dc2, gcdc;
     double new_cost, dp2, gpdp, x2;
     int iter, status, done, solve_ok;
     int accepted, cur;                      // cur: which of the two state buffers is current
+    int pending;                            // K5 produced a step (or failed) not yet decided
 };
 
 struct Geometry {
-    int n_kf, n_free, n_lm, n_obs, n_slot, n_pb, n_wave, n_chunk;
+    int n_kf, n_free, n_lm, n_obs, n_slot, n_pb, n_wave, n_chunk, pair_stride;
     Mat4 TCB[2];
     double huber_delta;
     int chol;  // linear solver: 0 Schur (inv3 landmark blocks), 1 the SparseCholesky fallback (LL^T)
@@ -161,16 +177,15 @@ struct Geometry {
 //   {free block of kf or -1, observations (0 = padding, <= 2), camera bits, 0}
 // and its observations' normalised coordinates inline (2 double2): everything a lane needs
 // before the pose / point loads arrives in one round trip.
+// Schur chunks: chunk c = 8 pb + x (workgroup c of K4c, dispatched to XCD c % 8 = x) holds all
+// slot pairs of camera block pb among the landmarks of XCD group x (the landmarks of the K6 / K4
+// waves w with w % 8 == x, which run on that XCD too).  Its partial goes to slot x of the
+// partial systems (cpart: 8 copies of the sys layout), which K5 sums in slot order.
 struct Prob {
     const int* free_idx;     // kf -> free block or -1
     const int4* slot_hdr;    // 2 per padded slot
     const double2* slot_uv;  // 2 per padded slot
-    const int* chunk_pb;     // n_chunk: camera block of each chunk
-    const int* chunk_pair;   // n_chunk + 1: slot-pair range of each chunk
-    const int* pb_chunk;     // n_pb + 1: chunk range of each camera block
-    const int* pair_a;
-    const int* pair_b;
-    const int* pair_l;       // landmark of each pair
+    const int4* pairs;       // n_chunk x pair_stride: {slot a, slot b, landmark, 0}, padding a = -1
     const int* pb_fa;
     const int* pb_fb;
 };
@@ -185,12 +200,12 @@ struct Work {
     int* singular;           // set by K4c when a landmark block (V + lambda I) is singular
     double* partA;           // n_wave x kPartA
     double* partD;           // n_wave x kPartD
-    int* cnt;                // K6 arrival counter (fused LM decision)
-    double* cpart;           // n_chunk x kBlockF chunk partials
+    double* cpart;           // kGrp x sys_len partial systems (slot g: landmark group g)
     double* sys;             // n_pb * 36 + 12 n_free + 2
     double* dc;              // 6 n_free
     double* trial4;          // 4 (sharded: reduced trial scalars)
-    LmState* st;
+    const LmState* st_prev;  // K4c: the state left by the previous iteration (read only)
+    LmState* st;             // this iteration's state (K4c's owner block writes it; K5, K6 use it)
 };
 
 __device__ __forceinline__ size_t sys_len(const Geometry& G) { return (size_t)G.n_pb * 36 + 12 * G.n_free + 2; }
@@ -206,7 +221,6 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[0][i] = Wk.pw_init[i];
         Wk.pw[1][i] = Wk.pw_init[i];
     }
-    if (i < G.n_pb + 3) Wk.cnt[i] = 0;
     if (i == 0) {
         *Wk.singular = 0;
         LmState s{};
@@ -379,7 +393,6 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk,
             Wk.pw[0][i] = Wk.pw_init[i];
             Wk.pw[1][i] = Wk.pw_init[i];
         }
-        for (int i = s; i < G.n_pb + 3; i += nt) Wk.cnt[i] = 0;
         if (s == 0) {
             *Wk.singular = 0;
             LmState st{};
@@ -417,223 +430,374 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk,
     STAMP(14);
 }
 
-// Deterministic sum of n values in global memory: thread t adds elements t, t + T, t + 2T, ...
-// (independent loads, all in flight), then thread 0 adds the T per-thread sums in thread order.
-// The order is fixed by (n, T) alone, so results are run-to-run identical.  Valid in thread 0;
-// every thread of the block must call it.
-template <int T>
-__device__ double block_ordered_sum(const double* __restrict__ v, int n, int stride, double* sh) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int i = threadIdx.x; i < n; i += T) acc += v[(size_t)i * stride];
-    __syncthreads();
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    double s = 0.0;
-    if (threadIdx.x == 0)
-        for (int k = 0; k < T; ++k) s += sh[k];
-    __syncthreads();
+// Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
+// owner rank), per-lane strided sums then a fixed-pairing wave reduction; every load is issued
+// before the state is read (the free-pose squares of both buffers; the current one is picked
+// afterwards).  Result on every lane.  Used by every decision (K4c blocks, K7, K6r), so the
+// sharded and single-rank paths reduce in the same order.
+__device__ void trial_scalars_wave(const Geometry& G, const Prob& Pr, const Work& Wk, const LmState& s,
+                                   int include_poses, double out[4]) {
+    const int lane = threadIdx.x & 63;
+    // all loads in flight together, branch-free (clamped indices, zeroed after the load): up to
+    // 8 wave partials per lane (a tail loop past 512 waves), then the <= 3 pose entries per
+    // lane of both state buffers
+    constexpr int kU = 8;
+    double4 pv[kU];
+    const int wl = max(G.n_wave - 1, 0), el = 7 * G.n_kf - 1;
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+        pv[k] = *reinterpret_cast<const double4*>(Wk.partD + (size_t)min(lane + 64 * k, wl) * kPartD);
+    double p0[3], p1[3];
+    int fi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int e = min(lane + 64 * k, el);
+        fi[k] = Pr.free_idx[e / 7];
+        p0[k] = Wk.pose[0][e];
+        p1[k] = Wk.pose[1][e];
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+        if (lane + 64 * k >= G.n_wave) pv[k] = make_double4(0.0, 0.0, 0.0, 0.0);
+    bool fr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fr[k] = include_poses && lane + 64 * k <= el && fi[k] >= 0;
+    double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+        acc[0] += pv[k].x;
+        acc[1] += pv[k].y;
+        acc[2] += pv[k].z;
+        acc[3] += pv[k].w;
+    }
+    for (int i = lane + 64 * kU; i < G.n_wave; i += 64) {
+        const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
+        acc[0] += v.x;
+        acc[1] += v.y;
+        acc[2] += v.z;
+        acc[3] += v.w;
+    }
+    double sq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (fr[k]) {
+            sq[0] += p0[k] * p0[k];
+            sq[1] += p1[k] * p1[k];
+        }
+    if (!s.solve_ok)
+#pragma unroll
+        for (int k = 0; k < kPartD; ++k) acc[k] = 0.0;
+    acc[3] += sq[s.cur];
+#pragma unroll
+    for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
+}
+
+// The build's LM decision (DESIGN.md section 5) for one iteration: cost = cost at the current
+// state, tv = trial cost, |dp|^2, g_p.dp, |x|^2.  Flips the state buffers on acceptance.
+__device__ void lm_update(LmState& s, double cost, const double tv[4], int max_iter, double cost_tol,
+                          double param_tol) {
+    if (s.iter == 0) s.initial_cost = cost;
+    s.cost = cost;
+    s.iter += 1;
+    s.accepted = 0;
+    if (!isfinite(cost)) {
+        s.status = RSVIO_LM_NUMERICAL_FAILURE;
+        s.done = 1;
+    } else if (!s.solve_ok) {
+        // a singular landmark block or camera system: apex's optimize returns
+        // Err(LinearSolveFailed), which SlidingWindow::optimize answers with the SparseCholesky
+        // retry, then a revert (sliding_window.rs:326-353)
+        s.status = RSVIO_LM_LINEAR_SOLVE_FAILED;
+        s.done = 1;
+    } else {
+        s.new_cost = tv[0];
+        s.dp2 = tv[1];
+        s.gpdp = tv[2];
+        s.x2 = tv[3];
+        const double dx2 = s.dc2 + s.dp2;
+        const double dxn = sqrt(dx2), xn = sqrt(s.x2);
+        if (dxn <= param_tol * (xn + param_tol)) {
+            s.status = RSVIO_LM_PARAMETER_TOLERANCE;
+            s.done = 1;
+        } else {
+            const double pred = 0.5 * (s.lambda * dx2 - (s.gcdc + s.gpdp));
+            const double rho = (cost - s.new_cost) / pred;
+            if (isfinite(s.new_cost) && rho > 0.0) {
+                const double dcost = cost - s.new_cost;
+                s.accepted = 1;
+                s.cur = 1 - s.cur;  // the trial buffers become current
+                const double f = 2.0 * rho - 1.0;
+                s.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
+                s.nu = 2.0;
+                s.cost = s.new_cost;
+                if (dcost <= cost_tol * (s.cost + dcost)) {
+                    s.status = RSVIO_LM_COST_TOLERANCE;
+                    s.done = 1;
+                }
+            } else {
+                s.lambda *= s.nu;
+                s.nu *= 2.0;
+                if (s.lambda > 1e32) {
+                    s.status = RSVIO_LM_TRUST_REGION;
+                    s.done = 1;
+                }
+            }
+        }
+    }
+    if (!s.done && s.iter >= max_iter) {
+        s.status = RSVIO_LM_MAX_ITERATIONS;
+        s.done = 1;
+    }
+}
+
+// LM configuration passed to the kernels that decide
+struct LmArgs {
+    int max_iter;
+    double cost_tol, param_tol;
+};
+
+// The pending decision (the previous iteration's trial), by one whole wave: returns the decided
+// state on every lane.  pre_reduced: the trial scalars come from trial4 (all-reduced over ranks),
+// else they are this rank's.  The cost of the initial state is sys[SC0] (K5's combine, or the
+// sharded combine + all-reduce, wrote it in iteration 0).  Every caller runs the same
+// operations on the same data, so every workgroup that decides gets identical bits.
+__device__ LmState lm_decide(const Geometry& G, const Prob& Pr, const Work& Wk, const LmState* src, int pre_reduced,
+                             const LmArgs& la) {
+    LmState s = *src;
+    // the trial scalars are gathered whether or not a decision is pending, so their loads are
+    // in flight together with the state's (one round trip)
+    double tv[4];
+    if (pre_reduced) {
+        for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
+    } else {
+        trial_scalars_wave(G, Pr, Wk, s, 1, tv);
+    }
+    const double cost0 = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];
+    // keep the compiler from sinking the gathers under the branch below (the state's load and
+    // theirs then overlap instead of running back to back)
+    __asm__ volatile("" ::"v"(tv[0]), "v"(tv[1]), "v"(tv[2]), "v"(tv[3]), "v"(cost0));
+    STAMP(29);
+    if (s.pending && !s.done) {
+        // cost at the current state: the initial linearisation's at the first iteration, then
+        // the cost of the last accepted trial state (K6 evaluated it while linearising it)
+        const double cost = s.iter == 0 ? cost0 : s.cost;
+        lm_update(s, cost, tv, la.max_iter, la.cost_tol, la.param_tol);
+        s.pending = 0;
+    }
     return s;
 }
 
 // ---------------------------------------------------------------------------------------
-// K4c: one wave per chunk of <= 64 slot pairs of one upper-triangular 6x6 camera block
-// (fa <= fb).  Lane = pair:  S_ab -= Y_a W_b^T  (+ U_a, b_a, g_c,a on diagonal blocks).
-// The lane partials are transposed through LDS and summed in lane order; the chunk partial
-// (48 values) goes to cpart.  No atomics: K4d combines the chunks of each block in order.
+// K4c: one 128-thread workgroup per (XCD group x, upper-triangular 6x6 camera block fa <= fb),
+// one slot pair per thread (more passes past 128 pairs).  It first takes the pending LM
+// decision (every wave redundantly, identical bits; block 0 stores it as this iteration's
+// state), then per pair  S_ab -= Y_a W_b^T  with Y = W (V + lambda I)^-1 formed on the fly
+// (+ U_a, b_a, g_c,a on diagonal blocks), reduce-scattered over each wave and summed over the
+// two waves in a fixed order into slot x of the partial systems.  No atomics and no last
+// arriver: K5 (or K4d when sharded) sums the 8 slots.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, int fused) {
-    __shared__ double sh[kBlockF * 65];
-    const int c = blockIdx.x, lane = threadIdx.x;
-    if (fused && c == 0 && lane == 0) Wk.cnt[G.n_pb + 1] = 0;  // the K5 flag of this iteration's K5+K6
-    if (c == G.n_chunk) {  // fused: the initial cost of this rank for the first decision
-        if (Wk.st->done) return;
-        const int SC0 = G.n_pb * 36 + 12 * G.n_free;
-        double v = 0.0;
-        for (int w = lane; w < G.n_wave; w += 64) v += Wk.partA[w * kPartA];
-        v = wave_sum_det(v);
-        if (lane == 0) {
-            Wk.sys[SC0] = v;
-            Wk.sys[SC0 + 1] = 0.0;  // the singular flag stays in Wk.singular (read by K5)
-        }
-        return;
-    }
-    const int pb = Pr.chunk_pb[c];
-    const bool diag = Pr.pb_fa[pb] == Pr.pb_fb[pb];
-    const int p0 = Pr.chunk_pair[c], np = Pr.chunk_pair[c + 1] - p0;
-    const bool act = lane < np;
-    int sa = 0, sb = 0, l = 0;
-    if (act) {
-        const int p = p0 + lane;
-        sa = Pr.pair_a[p];
-        sb = Pr.pair_b[p];
-        l = Pr.pair_l[p];
-    }
-    const LmState* st = Wk.st;
-    if (st->done) return;
-    STAMP(16);
-    const int cur = st->cur;
-    const double lambda = st->lambda;
-    double acc[36], bg[12];
+// One slot pair of a camera block.  DIAG: a diagonal block's pairs are (s, s) (a landmark has
+// one slot per keyframe), so W is loaded once and U, g_c join; off-diagonal blocks touch only
+// the 36 S entries -- two instantiations keep each one's register footprint to its own needs.
+template <bool DIAG>
+__device__ __forceinline__ void schur_pair(const Work& Wk, int cur, double lambda, int chol, int sa, int sb, int l,
+                                           double (&acc)[kBlockF]) {
+    const double2* ra = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sa * kRawF);
+    const double2* rb = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sb * kRawF);
+    const double2* rl = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)l * kLmF);
+    double Wa[18], Wb[18], Lm[10];
 #pragma unroll
-    for (int i = 0; i < 36; ++i) acc[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) bg[i] = 0.0;
-    if (act) {
-        const double2* ra = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sa * kRawF);
-        const double2* rb = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sb * kRawF);
-        const double2* rl = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)l * kLmF);
-        double Wa[18], Wb[18], Lm[10];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const double2 x = ra[RW / 2 + i], y = rb[RW / 2 + i];
-            Wa[2 * i] = x.x; Wa[2 * i + 1] = x.y;
+    for (int i = 0; i < 9; ++i) {
+        const double2 x = ra[RW / 2 + i];
+        Wa[2 * i] = x.x; Wa[2 * i + 1] = x.y;
+        if constexpr (!DIAG) {
+            const double2 y = rb[RW / 2 + i];
             Wb[2 * i] = y.x; Wb[2 * i + 1] = y.y;
         }
+    }
+    if constexpr (DIAG)
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const double2 x = rl[i];
-            Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
+        for (int i = 0; i < 18; ++i) Wb[i] = Wa[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const double2 x = rl[i];
+        Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
+    }
+    double r[28];  // record entries 18..45: U (21), g_c (6), pad -- diagonal blocks only
+    if constexpr (DIAG)
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const double2 v = ra[RU / 2 + i];
+            r[2 * i] = v.x; r[2 * i + 1] = v.y;
         }
-        double Vi[3][3];
-        if (!landmark_inverse(Lm + LV, lambda, Vi, G.chol)) *Wk.singular = 1;
-        double Ya[18];  // Y_a = W_a (V + lambda I)^-1
+    double Vi[3][3];
+    if (!landmark_inverse(Lm + LV, lambda, Vi, chol)) *Wk.singular = 1;
+    double Ya[18];  // Y_a = W_a (V + lambda I)^-1
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            Ya[a * 3 + k] = fma(Wa[a * 3 + 2], Vi[2][k], fma(Wa[a * 3 + 1], Vi[1][k], Wa[a * 3] * Vi[0][k]));
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            acc[a * 6 + k] -= fma(Ya[a * 3 + 2], Wb[k * 3 + 2], fma(Ya[a * 3 + 1], Wb[k * 3 + 1], Ya[a * 3] * Wb[k * 3]));
+    if constexpr (DIAG) {
+        int u = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
-                Ya[a * 3 + k] = (Wa[a * 3] * Vi[0][k] + Wa[a * 3 + 1] * Vi[1][k]) + Wa[a * 3 + 2] * Vi[2][k];
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int k = 0; k < 6; ++k)
-                acc[a * 6 + k] = -((Ya[a * 3] * Wb[k * 3] + Ya[a * 3 + 1] * Wb[k * 3 + 1]) + Ya[a * 3 + 2] * Wb[k * 3 + 2]);
-        if (diag) {
-            double r[28];  // record entries 18..45: U (21), g_c (6), pad
-#pragma unroll
-            for (int i = 0; i < 14; ++i) {
-                const double2 v = ra[RU / 2 + i];
-                r[2 * i] = v.x; r[2 * i + 1] = v.y;
+            for (int k = a; k < 6; ++k) {
+                const double v = r[u++];
+                acc[a * 6 + k] += v;
+                if (k != a) acc[k * 6 + a] += v;
             }
-            int u = 0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a)
-#pragma unroll
-                for (int k = a; k < 6; ++k) {
-                    const double v = r[u++];
-                    acc[a * 6 + k] += v;
-                    if (k != a) acc[k * 6 + a] += v;
-                }
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const double gca = r[RG - RU + a];
-                const double yg = (Ya[a * 3] * Lm[LG] + Ya[a * 3 + 1] * Lm[LG + 1]) + Ya[a * 3 + 2] * Lm[LG + 2];
-                bg[a] = yg - gca;  // b = -g_c + sum Y g_p
-                bg[6 + a] = gca;
-            }
-        }
-    }
-    STAMP(17);
-#pragma unroll
-    for (int i = 0; i < 36; ++i) sh[i * 65 + lane] = acc[i];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) sh[(36 + i) * 65 + lane] = bg[i];
-    __syncthreads();
-    const int nf = diag ? kBlockF : 36;
-    if (lane < nf) {
-        const double* row = sh + lane * 65;
-        double s = 0.0;
-#pragma unroll 16
-        for (int k = 0; k < 64; ++k) s += row[k];  // lanes >= np hold zeros
-        if (fused)  // device-coherent (sc1): the block's last chunk reads it in this launch
-            __hip_atomic_store(Wk.cpart + (size_t)c * kBlockF + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            Wk.cpart[(size_t)c * kBlockF + lane] = s;
-    }
-    STAMP(18);
-    if (!fused) return;
-    // K4d folded in (single rank): drain the sc1 partials, count the block's arrivals; the last
-    // chunk of the block sums the block's chunk partials in chunk order (+ lambda on the
-    // diagonal) and writes the block of S, b, g_c for K5
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
-    int last = 0;
-    if (lane == 0) {
-        const int old = __hip_atomic_fetch_add(Wk.cnt + 1 + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == c1 - c0 - 1;
-    }
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (!last) return;
-    if (lane == 0) __hip_atomic_store(Wk.cnt + 1 + pb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane < nf) {
-        double v = 0.0;
-#pragma unroll 8
-        for (int cc = c0; cc < c1; ++cc)
-            v += __hip_atomic_load(Wk.cpart + (size_t)cc * kBlockF + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int fa = Pr.pb_fa[pb];
-        const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free;
-        if (lane < 36) {
-            if (diag && lane / 6 == lane % 6) v += lambda;
-            Wk.sys[pb * 36 + lane] = v;
-        } else if (lane < 42) {
-            Wk.sys[SB0 + 6 * fa + (lane - 36)] = v;   // b = -g_c + sum Y g_p
-        } else {
-            Wk.sys[SG0 + 6 * fa + (lane - 42)] = v;   // g_c
+        for (int a = 0; a < 6; ++a) {
+            const double gca = r[RG - RU + a];
+            const double yg = fma(Ya[a * 3 + 2], Lm[LG + 2], fma(Ya[a * 3 + 1], Lm[LG + 1], Ya[a * 3] * Lm[LG]));
+            acc[36 + a] += yg - gca;  // b = -g_c + sum Y g_p
+            acc[42 + a] += gca;
         }
     }
 }
 
-// Cost of the initial linearisation of this rank (K4 wave partials, one wave, fixed order) and
-// the singular-landmark flag of this iteration's K4c (consumed and cleared here): written to
-// sys[SC0], sys[SC0 + 1].
-__device__ void cost_partials(const Geometry& G, const Work& Wk, int lane, int SC0) {
-    double c = 0.0;
-    for (int w = lane; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
-    c = wave_sum_det(c);
-    if (lane == 0) {
-        Wk.sys[SC0] = c;
-        Wk.sys[SC0 + 1] = *Wk.singular ? 1.0 : 0.0;
-        *Wk.singular = 0;
+template <bool DIAG>
+__device__ __forceinline__ void schur_chunk_pairs(const Geometry& G, const Work& Wk, const LmState& s, const int4* pr,
+                                                  int4 p1, int tid, double (&acc)[kBlockF]) {
+    if (p1.x >= 0) schur_pair<DIAG>(Wk, s.cur, s.lambda, G.chol, p1.x, p1.y, p1.z, acc);
+    for (int p = tid + kSchurThreads; p < G.pair_stride; p += kSchurThreads) {  // > 512 pairs per group
+        const int4 q = pr[p];
+        if (q.x >= 0) schur_pair<DIAG>(Wk, s.cur, s.lambda, G.chol, q.x, q.y, q.z, acc);
     }
 }
 
-// Entry k (< 48) of camera block pb: its chunk partials in chunk order (+ lambda on the
-// diagonal of S on the owner rank).
-__device__ __forceinline__ double block_entry(const Prob& Pr, const Work& Wk, int pb, int k, bool diag,
-                                              int lambda_owner) {
-    const int c0 = Pr.pb_chunk[pb], c1 = Pr.pb_chunk[pb + 1];
-    double v = 0.0;
-#pragma unroll 8
-    for (int cc = c0; cc < c1; ++cc) v += Wk.cpart[(size_t)cc * kBlockF + k];
-    if (k < 36 && diag && lambda_owner && k / 6 == k % 6) v += Wk.st->lambda;
-    return v;
-}
-
-// K4d: one wave per camera block: S, b, g_c from the block's chunk partials in chunk order
-// (+ lambda on the diagonal on the owner rank); one extra wave for the cost and the
-// singular-landmark count of this rank.
-__global__ __launch_bounds__(64) void ba_schur_combine(Geometry G, Prob Pr, Work Wk, int lambda_owner) {
-    if (Wk.st->done) return;
-    const int pb = blockIdx.x, lane = threadIdx.x;
-    double* sys = Wk.sys;
-    const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free, SC0 = SG0 + 6 * G.n_free;
-    if (pb == G.n_pb) {
-        cost_partials(G, Wk, lane, SC0);
-        return;
-    }
-    STAMP(19);
+__global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, LmArgs la,
+                                                                  int pre_reduced) {
+    __shared__ double red[kSchurThreads / 64][kBlockF];
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pb = c / kGrp, x = c % kGrp;
+    RTSTAMP(0);
+    STAMP(26);
+    // this chunk's pairs sit at a fixed stride: the first pair of every thread is one load,
+    // issued together with the decision's loads
+    const int4* pr = Pr.pairs + (size_t)c * G.pair_stride;
+    const int4 p1 = tid < G.pair_stride ? pr[tid] : make_int4(-1, 0, 0, 0);
     const int fa = Pr.pb_fa[pb];
     const bool diag = fa == Pr.pb_fb[pb];
-    const int nf = diag ? kBlockF : 36;
-    if (lane >= nf) return;
-    const double v = block_entry(Pr, Wk, pb, lane, diag, lambda_owner);
-    if (lane < 36) {
-        sys[pb * 36 + lane] = v;
-    } else if (lane < 42) {
-        sys[SB0 + 6 * fa + (lane - 36)] = v;   // b = -g_c + sum Y g_p
-    } else {
-        sys[SG0 + 6 * fa + (lane - 42)] = v;   // g_c
+    // the decision by wave 0, handed to the other waves through LDS (a quarter of the loads)
+    __shared__ LmState sd;
+    STAMP(27);
+    if (wave == 0) {
+        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la);
+        STAMP(28);
+        if (lane == 0) {
+            sd = d;
+            if (c == 0) *Wk.st = d;
+        }
     }
+    __syncthreads();
+    const LmState s = sd;
+    if (s.done) return;
+    STAMP(16);
+    RTSTAMP(1);
+    double acc[kBlockF];
+#pragma unroll
+    for (int i = 0; i < kBlockF; ++i) acc[i] = 0.0;
+    if (diag)
+        schur_chunk_pairs<true>(G, Wk, s, pr, p1, tid, acc);
+    else
+        schur_chunk_pairs<false>(G, Wk, s, pr, p1, tid, acc);
+    STAMP(17);
+    wave_reduce_scatter<3>(acc, lane);
+    if ((lane & 3) == 0)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) red[wave][3 * (lane >> 2) + j] = acc[j];
+    __syncthreads();
+    if (tid < (diag ? kBlockF : 36)) {
+        double v = red[0][tid];
+#pragma unroll
+        for (int w = 1; w < kSchurThreads / 64; ++w) v += red[w][tid];
+        const int SB0 = G.n_pb * 36, SG0 = SB0 + 6 * G.n_free;
+        const int e = tid < 36 ? pb * 36 + tid : (tid < 42 ? SB0 + 6 * fa + tid - 36 : SG0 + 6 * fa + tid - 42);
+        Wk.cpart[(size_t)x * sys_len(G) + e] = v;
+    }
+    STAMP(18);
+    RTSTAMP(2);
+}
+
+// The reduced system of this rank into dst (sys layout): S, b, g_c summed over the kGrp partial
+// systems in slot order (+ lambda on the diagonal of diagonal blocks when add_lambda), then the
+// cost of the initial linearisation (K4 wave partials, fixed order) and the singular-landmark
+// flag of this iteration's K4c.  Every load is coalesced and independent of any other.  Whole
+// block (T threads).
+template <int T>
+__device__ void combine_system(const Geometry& G, const Prob& Pr, const Work& Wk, double* dst, double lambda,
+                               bool add_lambda) {
+    const int n_e = G.n_pb * 36 + 12 * G.n_free;
+    const size_t L = sys_len(G);
+    // the K4 wave partials (initial cost) and the singular flag are loaded first, with the
+    // partial systems: one round trip for everything
+    constexpr int kU = 16;  // all in flight (a tail loop past 1024 waves)
+    const int lane = threadIdx.x;
+    double pa[kU];
+    int sing = 0;
+    if (lane < 64) {
+#pragma unroll
+        for (int k = 0; k < kU; ++k) pa[k] = lane + 64 * k < G.n_wave ? Wk.partA[(lane + 64 * k) * kPartA] : 0.0;
+        sing = *Wk.singular;
+    }
+    // rounds of kE entries per thread, every load of a round issued before any is consumed
+    constexpr int kE = 8;
+    for (int e0 = 0; e0 < n_e; e0 += T * kE) {
+        double v[kE][kGrp];
+#pragma unroll
+        for (int i = 0; i < kE; ++i) {
+            const int e = e0 + threadIdx.x + T * i;
+#pragma unroll
+            for (int x = 0; x < kGrp; ++x) v[i][x] = e < n_e ? Wk.cpart[(size_t)x * L + e] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < kE; ++i) {
+            const int e = e0 + threadIdx.x + T * i;
+            if (e >= n_e) break;
+            double a = v[i][0];
+#pragma unroll
+            for (int x = 1; x < kGrp; ++x) a += v[i][x];
+            dst[e] = a;
+        }
+    }
+    if (add_lambda) {  // + lambda on the diagonal of each diagonal block (f, f), after its sum
+        __syncthreads();
+        for (int t = threadIdx.x; t < 6 * G.n_free; t += T) {
+            const int f = t / 6, k = t % 6;
+            dst[(f * G.n_free - f * (f - 1) / 2) * 36 + 7 * k] += lambda;
+        }
+    }
+    if (lane < 64) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < kU; ++k) c += pa[k];
+        for (int w = lane + 64 * kU; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+        c = wave_sum_det(c);
+        if (lane == 0) {
+            dst[n_e] = c;
+            dst[n_e + 1] = sing ? 1.0 : 0.0;
+            Wk.sys[n_e] = c;  // the decision of iteration 0 reads the initial cost here
+        }
+    }
+}
+
+// K4d (sharded path, and build_system): the rank's reduced system into sys (+ lambda on the
+// owner rank), ready for the all-reduce; clears the singular flag.
+__global__ __launch_bounds__(256) void ba_schur_combine(Geometry G, Prob Pr, Work Wk, int lambda_owner) {
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    STAMP(19);
+    combine_system<256>(G, Pr, Wk, Wk.sys, st->lambda, lambda_owner != 0);
+    __syncthreads();
+    if (threadIdx.x == 0) *Wk.singular = 0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -658,7 +822,7 @@ constexpr int kLcLd = 65;
 
 template <int NP, int CW, int WV, int K>
 __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double* Lc, double* Uc, int* progress,
-                                               int& seen, bool& bad, double inv) {
+                                               int& seen, bool& bad, double inv, double (&uq)[CW], double lp) {
     constexpr int c0 = WV * CW;
     constexpr int c1 = (c0 + CW < NP) ? c0 + CW : NP;
     constexpr int KN = (K + 1 < c0) ? K + 2 : K + 1;  // consume columns in pairs
@@ -703,9 +867,13 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
 #ifdef RSVIO_STAMPS
         if (K == c0 && lane == 0) g_dbg[28 + WV] = (unsigned long long)clock64();
 #endif
-        // publish column K-1 now: its LDS writes have long landed, so the release does not
-        // stall this column's pivot chain (the last column is published at the end)
-        if constexpr (K > c0) __hip_atomic_store(progress, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // publish column K-1: a relaxed store behind a compiler barrier -- a wave's LDS operations
+        // are performed in order, so a consumer that reads the counter reads the column after
+        // it, and no wait for this wave's outstanding LDS operations stalls the pivot chain
+        if constexpr (K > c0) {
+            __asm__ volatile("" ::: "memory");
+            __hip_atomic_store(progress, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         const double uk = a[j];
         const double l = uk * inv;
         a[j] = l;
@@ -717,16 +885,34 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
             a[j + 1] = fma(-l, rl64(uk, K + 1), a[j + 1]);
             piv = rl64(a[j + 1], K + 1);
         }
-        // the rest of the own block: U[c0 + jj][K] straight from its lane (no LDS round trip
-        // on the next pivots' path)
-#pragma unroll
-        for (int jj = j + 2; jj < CW; ++jj)
-            if (c0 + jj < NP) a[jj] = fma(-l, rl64(uk, c0 + jj), a[jj]);
+        // column K+2 by readlane too: it is the next step's pivot-path column
+        if constexpr (j + 2 < CW && K + 2 < NP) a[j + 2] = fma(-l, rl64(uk, K + 2), a[j + 2]);
         if constexpr (j + 1 < CW && K + 1 < NP) {
             bad |= !(piv > 0.0) || !isfinite(piv);
             inv = rcp_f64(piv);
         }
-        if constexpr (K + 1 == c1) __hip_atomic_store(progress, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the next reciprocal is issued before anything below touches LDS results
+        __builtin_amdgcn_sched_barrier(0);
+        // software-pipelined rest of the own block: the previous column's updates of columns
+        // >= j + 2, from U values read from LDS one step ago (landed by now), then this column's
+        // U values for columns >= j + 3 are read for the next step -- a readlane pair per value
+        // plus its SGPR hazard wait cost ~4x the issue slots, and an LDS read consumed in the
+        // same step puts its latency on the chain
+        if constexpr (K > c0) {
+#pragma unroll
+            for (int jj = j + 2; jj < CW; ++jj)
+                if (c0 + jj < NP) a[jj] = fma(-lp, uq[jj], a[jj]);
+        }
+        {
+            const double* uK = Uc + K * kLcLd;
+#pragma unroll
+            for (int jj = j + 3; jj < CW; ++jj) uq[jj] = c0 + jj < NP ? uK[c0 + jj] : 0.0;
+        }
+        lp = l;
+        if constexpr (K + 1 == c1) {
+            __asm__ volatile("" ::: "memory");
+            __hip_atomic_store(progress, K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     // consume steps: materialise the updates here (keeps the compiler from sinking the FMAs
     // past the next wait loop, which would keep every loaded column alive)
@@ -735,7 +921,7 @@ __device__ __forceinline__ void chol_pipe_step(double (&a)[CW], int lane, double
         for (int jj = 0; jj < CW; ++jj) __asm__ volatile("" : "+v"(a[jj]));
     }
     constexpr int KNEXT = (K < c0) ? KN : K + 1;
-    if constexpr (KNEXT < c1) chol_pipe_step<NP, CW, WV, KNEXT>(a, lane, Lc, Uc, progress, seen, bad, inv);
+    if constexpr (KNEXT < c1) chol_pipe_step<NP, CW, WV, KNEXT>(a, lane, Lc, Uc, progress, seen, bad, inv, uq, lp);
 }
 
 // Element (r, c), c <= r < n, of the lower triangle of S in the packed block layout of sys
@@ -771,7 +957,10 @@ __device__ void chol_pipe(const double* sys, double* Lc, double* Uc, int* progre
             inv = rcp_f64(piv);
         }
         int seen = 0;
-        chol_pipe_step<NP, CW, WV, 0>(a, lane, Lc, Uc, progress, seen, bad, inv);
+        double uq[CW];
+#pragma unroll
+        for (int jj = 0; jj < CW; ++jj) uq[jj] = 0.0;
+        chol_pipe_step<NP, CW, WV, 0>(a, lane, Lc, Uc, progress, seen, bad, inv, uq, 0.0);
     }
     if (lane == 0) badw[WV] = bad ? 1 : 0;
 #ifdef RSVIO_STAMPS
@@ -779,29 +968,34 @@ __device__ void chol_pipe(const double* sys, double* Lc, double* Uc, int* progre
 #endif
 }
 
+// K5's result in this iteration's state: the step (or its failure) is pending a decision
+__device__ __forceinline__ void k5_result(LmState* st, int ok, double d2, double gd) {
+    st->solve_ok = ok;
+    st->dc2 = d2;
+    st->gcdc = gd;
+    st->pending = 1;
+}
+
 template <int NF>
-__device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
+__device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, const double* sys, double* A,
+                                int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
     constexpr int NP = 6 * NF, CW = (NP + 3) / 4;
     const int lane = tid & 63, wave = tid >> 6;
     LmState* st = Wk.st;
-    const double gcl_v = (wave == 0 && lane < n) ? Wk.sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
+    const double gcl_v = (wave == 0 && lane < n) ? sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
     // Lc / Uc in A's LDS past its first 128 doubles (A[0..n) holds dc for the pose updates)
     double* Lc = A + 128;
     double* Uc = Lc + NP * kLcLd;
     switch (wave) {
-        case 0: chol_pipe<NP, CW, 0>(Wk.sys, Lc, Uc, progress, badw, lane); break;
-        case 1: chol_pipe<NP, CW, 1>(Wk.sys, Lc, Uc, progress, badw, lane); break;
-        case 2: chol_pipe<NP, CW, 2>(Wk.sys, Lc, Uc, progress, badw, lane); break;
-        default: chol_pipe<NP, CW, 3>(Wk.sys, Lc, Uc, progress, badw, lane); break;
+        case 0: chol_pipe<NP, CW, 0>(sys, Lc, Uc, progress, badw, lane); break;
+        case 1: chol_pipe<NP, CW, 1>(sys, Lc, Uc, progress, badw, lane); break;
+        case 2: chol_pipe<NP, CW, 2>(sys, Lc, Uc, progress, badw, lane); break;
+        default: chol_pipe<NP, CW, 3>(sys, Lc, Uc, progress, badw, lane); break;
     }
     __syncthreads();
     if (wave != 0) return;
     if (badw[0] | badw[1] | badw[2] | badw[3]) {
-        if (lane == 0) {
-            st->solve_ok = 0;
-            st->dc2 = 0.0;
-            st->gcdc = 0.0;
-        }
+        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
     STAMP(7);
@@ -842,21 +1036,21 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
         }
     }
     STAMP(5);
-    if (lane == 0) {
-        st->solve_ok = 1;
-        st->dc2 = d2;
-        st->gcdc = gd;
-    }
+    if (lane == 0) k5_result(st, 1, d2, gd);
     STAMP(6);
 }
 
 template <int NF>
 constexpr size_t k5_lds_doubles() { return 128 + 2 * 6 * NF * kLcLd; }
-
-// K5 body (one 256-thread block); A: k5_lds_doubles<NF>() of LDS.  Every write of its results
-// (dc, trial poses, st->solve_ok/dc2/gcdc) is made by wave 0.
 template <int NF>
-__device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, double* A) {
+constexpr size_t k5_sys_doubles() { return (size_t)(NF * (NF + 1) / 2) * 36 + 12 * NF + 2; }
+
+// K5 body (one 256-thread block); A: k5_lds_doubles<NF>() of LDS, Ls: k5_sys_doubles<NF>().
+// combine (single rank): the reduced system is first summed from K4c's chunk partials into Ls
+// (+ lambda on the diagonal); sharded: it is the all-reduced sys.  Every write of its results
+// (dc, trial poses, the state's solve_ok/dc2/gcdc/pending) is made by wave 0.
+template <int NF>
+__device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* Ls, int combine) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
     __shared__ int badw[4];
     __shared__ int progress;
@@ -865,7 +1059,6 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
     if (st->done) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nF = G.n_free, n = 6 * nF;
-    const double* sys = Wk.sys;
     const int SC0 = G.n_pb * 36 + 12 * nF;
     const int cur = st->cur;
     // the trial-pose inputs of wave 0 are fetched now, behind the fill
@@ -877,6 +1070,12 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
         for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
     }
     STAMP(0);
+    const double* sys = Wk.sys;
+    if (combine) {
+        combine_system<256>(G, Pr, Wk, Ls, st->lambda, true);
+        sys = Ls;
+    }
+    __syncthreads();
     if (tid == 0) {
         // a landmark block was singular (sharded: summed over ranks by K4d + all-reduce;
         // single rank: K4c's flag, cleared here for the next iteration)
@@ -886,26 +1085,22 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
     }
     __syncthreads();
     STAMP(1);
-    {
-        if (fail) {
-            if (tid == 0) {
-                st->solve_ok = 0;
-                st->dc2 = 0.0;
-                st->gcdc = 0.0;
-            }
-            return;
-        }
-        STAMP(2);
-        camera_solve_w4<NF>(G, Pr, Wk, A, badw, &progress, n, tid, p7, fidx);
+    if (fail) {
+        if (tid == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
+    STAMP(2);
+    camera_solve_w4<NF>(G, Pr, Wk, sys, A, badw, &progress, n, tid, p7, fidx);
 }
 
 template <int NF>
-__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk) {
+__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk, int combine) {
     // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
     __shared__ __attribute__((aligned(16))) double A[k5_lds_doubles<NF>()];
-    k5_body<NF>(G, Pr, Wk, A);
+    __shared__ double Ls[k5_sys_doubles<NF>()];
+    RTSTAMP(4);
+    k5_body<NF>(G, Pr, Wk, A, Ls, combine);
+    RTSTAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1066,7 +1261,7 @@ __device__ __forceinline__ void chol2_pipe(const double* sys, int nf, double* Uc
 }
 
 template <int NF>
-__global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, Prob Pr, Work Wk) {
+__global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, Prob Pr, Work Wk, int combine) {
     constexpr int NP = 6 * NF, CW = (NP + kX2Waves - 1) / kX2Waves;
     static_assert(NP <= kMaxN && NP + 1 <= kUcLd && NP < 128, "padded system too large");
     __shared__ double Uc[NP * kUcLd];
@@ -1086,16 +1281,20 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
     double p7[7] = {0, 0, 0, 1, 0, 0, 0};
     int fidx = -1;
     double gcl[2] = {0.0, 0.0};
-    if (wave == 0) {
-        if (lane < G.n_kf) {
-            fidx = Pr.free_idx[lane];
+    if (wave == 0 && lane < G.n_kf) {
+        fidx = Pr.free_idx[lane];
 #pragma unroll
-            for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
-        }
+        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
+    }
+    if (combine) {  // single rank: the reduced system from K4c's chunk partials into sys
+        combine_system<64 * kX2Waves>(G, Pr, Wk, Wk.sys, st->lambda, true);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+    if (wave == 0)
 #pragma unroll
         for (int q = 0; q < 2; ++q)
             if (lane + 64 * q < n) gcl[q] = sys[SG0 + lane + 64 * q];
-    }
     if (tid == 0) {
         fail = (sys[SC0 + 1] != 0.0 || *Wk.singular) ? 1 : 0;
         *Wk.singular = 0;
@@ -1103,11 +1302,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
     }
     __syncthreads();
     if (fail) {
-        if (tid == 0) {
-            st->solve_ok = 0;
-            st->dc2 = 0.0;
-            st->gcdc = 0.0;
-        }
+        if (tid == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
     switch (wave) {
@@ -1126,11 +1321,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
 #pragma unroll
     for (int w = 0; w < kX2Waves; ++w) anybad |= badw[w] != 0;
     if (anybad) {
-        if (lane == 0) {
-            st->solve_ok = 0;
-            st->dc2 = 0.0;
-            st->gcdc = 0.0;
-        }
+        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
     // L^T x = z (unit diagonal), z = row NP of the factor: lane holds rows i = lane, lane + 64;
@@ -1191,140 +1382,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
             for (int i = 0; i < 7; ++i) qd[i] = qv[i];
         }
     }
-    if (lane == 0) {
-        st->solve_ok = 1;
-        st->dc2 = d2;
-        st->gcdc = gd;
-    }
-}
-
-// Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
-// owner rank), per-lane strided sums then a fixed-pairing wave reduction; every load is issued
-// before the state is read (the free-pose squares of both buffers; the current one is picked
-// afterwards).  Result on every lane.  Used by the fused K6 tail, K6r and K7 alike, so the
-// sharded and single-rank paths reduce in the same order.
-template <bool COHERENT = false>
-__device__ void trial_scalars_wave(const Geometry& G, const Prob& Pr, const Work& Wk, int include_poses,
-                                   double out[4]) {
-    const LmState* st = Wk.st;
-    const int lane = threadIdx.x & 63;
-    double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
-    double sq[2] = {0.0, 0.0};
-    for (int i = lane; i < G.n_wave; i += 64) {
-        if constexpr (COHERENT) {  // partials of this launch: device-coherent (sc1) loads
-#pragma unroll
-            for (int k = 0; k < kPartD; ++k)
-                acc[k] += __hip_atomic_load(Wk.partD + (size_t)i * kPartD + k, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const double4 v = *reinterpret_cast<const double4*>(Wk.partD + (size_t)i * kPartD);
-            acc[0] += v.x;
-            acc[1] += v.y;
-            acc[2] += v.z;
-            acc[3] += v.w;
-        }
-    }
-    if (include_poses)
-        for (int e = lane; e < 7 * G.n_kf; e += 64) {
-            const bool fr = Pr.free_idx[e / 7] >= 0;
-            const double p0 = Wk.pose[0][e], p1 = Wk.pose[1][e];
-            if (fr) {
-                sq[0] += p0 * p0;
-                sq[1] += p1 * p1;
-            }
-        }
-    const int solve_ok = st->solve_ok, cur = st->cur;
-    if (!solve_ok)
-#pragma unroll
-        for (int k = 0; k < kPartD; ++k) acc[k] = 0.0;
-    acc[3] += sq[cur];
-#pragma unroll
-    for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
-}
-
-// The build's LM decision (DESIGN.md section 5) for one iteration: cost = cost at the current
-// state, tv = trial cost, |dp|^2, g_p.dp, |x|^2.  Flips the state buffers on acceptance.
-__device__ void lm_update(LmState& s, double cost, const double tv[4], int max_iter, double cost_tol,
-                          double param_tol) {
-    if (s.iter == 0) s.initial_cost = cost;
-    s.cost = cost;
-    s.iter += 1;
-    s.accepted = 0;
-    if (!isfinite(cost)) {
-        s.status = RSVIO_LM_NUMERICAL_FAILURE;
-        s.done = 1;
-    } else if (!s.solve_ok) {
-        // a singular landmark block or camera system: apex's optimize returns
-        // Err(LinearSolveFailed), which SlidingWindow::optimize answers with the SparseCholesky
-        // retry, then a revert (sliding_window.rs:326-353)
-        s.status = RSVIO_LM_LINEAR_SOLVE_FAILED;
-        s.done = 1;
-    } else {
-        s.new_cost = tv[0];
-        s.dp2 = tv[1];
-        s.gpdp = tv[2];
-        s.x2 = tv[3];
-        const double dx2 = s.dc2 + s.dp2;
-        const double dxn = sqrt(dx2), xn = sqrt(s.x2);
-        if (dxn <= param_tol * (xn + param_tol)) {
-            s.status = RSVIO_LM_PARAMETER_TOLERANCE;
-            s.done = 1;
-        } else {
-            const double pred = 0.5 * (s.lambda * dx2 - (s.gcdc + s.gpdp));
-            const double rho = (cost - s.new_cost) / pred;
-            if (isfinite(s.new_cost) && rho > 0.0) {
-                const double dcost = cost - s.new_cost;
-                s.accepted = 1;
-                s.cur = 1 - s.cur;  // the trial buffers become current
-                const double f = 2.0 * rho - 1.0;
-                s.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
-                s.nu = 2.0;
-                s.cost = s.new_cost;
-                if (dcost <= cost_tol * (s.cost + dcost)) {
-                    s.status = RSVIO_LM_COST_TOLERANCE;
-                    s.done = 1;
-                }
-            } else {
-                s.lambda *= s.nu;
-                s.nu *= 2.0;
-                if (s.lambda > 1e32) {
-                    s.status = RSVIO_LM_TRUST_REGION;
-                    s.done = 1;
-                }
-            }
-        }
-    }
-    if (!s.done && s.iter >= max_iter) {
-        s.status = RSVIO_LM_MAX_ITERATIONS;
-        s.done = 1;
-    }
-}
-
-// LM configuration passed to the kernels that decide
-struct LmArgs {
-    int max_iter;
-    double cost_tol, param_tol;
-};
-
-// Decision by one wave (lane 0 writes the state).  pre_reduced: the trial scalars come from
-// trial4 (all-reduced over ranks); else they are this rank's.
-template <bool COHERENT = false>
-__device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced, const LmArgs& la) {
-    LmState* stp = Wk.st;
-    const double cost0 = Wk.sys[(size_t)G.n_pb * 36 + 12 * G.n_free];  // cost of the initial state
-    double tv[4];
-    if (pre_reduced) {
-        for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
-    } else {
-        trial_scalars_wave<COHERENT>(G, Pr, Wk, 1, tv);
-    }
-    if ((threadIdx.x & 63) != 0) return;
-    LmState s = *stp;
-    // cost at the current state: the initial linearisation's at the first iteration, then the
-    // cost of the last accepted trial state (K6 evaluated it while linearising it)
-    const double cost = s.iter == 0 ? cost0 : s.cost;
-    lm_update(s, cost, tv, la.max_iter, la.cost_tol, la.param_tol);
-    *stp = s;
+    if (lane == 0) k5_result(st, 1, d2, gd);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1333,23 +1391,20 @@ __device__ void lm_decide_wave(const Geometry& G, const Prob& Pr, const Work& Wk
 // the trial cost).  Accepted: the next iteration starts from that linearisation; rejected:
 // from the current one, untouched.
 // ---------------------------------------------------------------------------------------
-// FUSED: one wave of a ba_solve_backsub block; its inputs from K5 (dc, trial poses, st) are
-// awaited on the K5 flag (agent-scope acquire) instead of a kernel boundary.
+// The wave partials (trial cost, |dp|^2, g_p.dp, |p|^2) go out as plain stores: the decision
+// is taken by the next iteration's K4c blocks (or K7 at the end of a chunk), after the boundary.
 template <bool FUSED>
-__device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int fuse_decide, const LmArgs& la, int w,
-                        int lane, double (*sh)[64], double (*shp)[64], double (*shs)[64]) {
+__device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w, int lane, double (*sh)[64],
+                        double (*shp)[64], double (*shs)[64]) {
     // sh: W_s^T dc_f per slot, then the linearisation scratch; shp: trial point at the
     // landmark's first lane; shs: per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int s = 64 * w + lane;
     const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
     const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
     const LmState* st = Wk.st;
-    if (st->done) return;
-    if (!st->solve_ok) {  // no step: the decision (lambda up) is all there is
-        if (fuse_decide && w == 0) lm_decide_wave(G, Pr, Wk, 0, la);
-        return;
-    }
+    if (st->done || !st->solve_ok) return;  // no step: the decision (lambda up) is all there is
     STAMP(20);
+    RTSTAMP(7);
     const bool act = h1.y > 0;
     const int cur = st->cur;
     const double lambda = st->lambda;
@@ -1441,58 +1496,42 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int f
         double v[kPartD];
 #pragma unroll
         for (int i = 0; i < kPartD; ++i) v[i] = wave_sum_det(shs[i][lane]);
-        if (lane == 0) {
-            if (fuse_decide) {  // device-coherent (sc1) stores: the last wave reads them below
+        if (lane == 0)
 #pragma unroll
-                for (int i = 0; i < kPartD; ++i)
-                    __hip_atomic_store(Wk.partD + w * kPartD + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-#pragma unroll
-                for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
-            }
-        }
+            for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
     }
     STAMP(21);
-    if (fuse_decide) {
-        // K7 folded in: the partials go out with sc1 stores, drained before the arrival counter
-        // (no L2 write-back fence); the last wave to arrive reads them with sc1 loads and takes
-        // the LM decision
-        int last = 0;
-        if (lane == 0) {
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int old = __hip_atomic_fetch_add(Wk.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = old == G.n_wave - 1;
-        }
-        last = __builtin_amdgcn_readfirstlane(last);
-        if (!last) return;
-        if (lane == 0) __hip_atomic_store(Wk.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lm_decide_wave<true>(G, Pr, Wk, 0, la);
-    }
+    RTSTAMP(8);
 }
 
-__global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr, Work Wk, int fuse_decide,
-                                                             LmArgs la) {
+__global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr, Work Wk) {
     __shared__ double sh[10][64];
     __shared__ double shp[3][64];
     __shared__ double shs[4][64];
-    k6_body<false>(G, Pr, Wk, fuse_decide, la, blockIdx.x, threadIdx.x, sh, shp, shs);
+    RTSTAMP(6);
+    k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs);
+    RTSTAMP(9);
 }
 
+// K6r (sharded): this rank's trial scalars (|x|^2 of the poses on the owner rank) -> trial4,
+// ready for the all-reduce
 __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
-    if (Wk.st->done) return;
+    const LmState s = *Wk.st;
+    if (s.done) return;
     double v[4];
-    trial_scalars_wave(G, Pr, Wk, include_poses, v);
+    trial_scalars_wave(G, Pr, Wk, s, include_poses, v);
     if (threadIdx.x == 0)
         for (int k = 0; k < 4; ++k) Wk.trial4[k] = v[k];
 }
 
 // ---------------------------------------------------------------------------------------
-// K7: LM decision (sharded path, or no landmark wave to fold it into).
+// K7: the pending decision at the end of a chunk of iterations (one wave, in place: the state
+// the host reads back, and the next chunk's K4c finds nothing pending).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la) {
-    if (Wk.st->done) return;
     STAMP(8);
-    lm_decide_wave(G, Pr, Wk, pre_reduced, la);
+    const LmState s = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
+    if (threadIdx.x == 0) *Wk.st = s;
     STAMP(10);
 }
 
@@ -1553,6 +1592,7 @@ __global__ __launch_bounds__(256) void ba_p2p_allreduce(double* buf, int n, P2P 
 }  // namespace
 
 RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
+RSVIO_RT_READER(rsvio_dbg_ba_rt)
 
 // ======================================================================================
 struct BundleAdjuster {
@@ -1562,7 +1602,6 @@ struct BundleAdjuster {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Geometry G{};
     bool has_problem = false;
-    bool fuse_combine = true;  // single rank: K4d folded into K4c
     int iter_chunk = 2;       // LM iterations enqueued per status read-back after the first chunk
     // Single rank: the start of a solve (K0 + K4 + the first chunk of k LM iterations, ~17
     // kernels) captured once as a HIP graph and replayed by one hipGraphLaunch -- the host
@@ -1594,7 +1633,8 @@ struct BundleAdjuster {
             bool ok = true;
             try {
                 enqueue_start(cfg.lambda_init);
-                for (int i = 0; i < k; ++i) enqueue_iteration(cfg);
+                for (int i = 0; i < k; ++i) enqueue_iteration(cfg, i);
+                enqueue_decide(cfg, k);
             } catch (...) {
                 ok = false;
             }
@@ -1619,13 +1659,11 @@ struct BundleAdjuster {
     int last_iterations = 3;  // first chunk = previous solve's iteration count
     DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_slot_uv;
     DevBuf<int> d_slot_hdr;
-    DevBuf<int> d_free, d_chunk_pb,
-        d_chunk_pair, d_pb_chunk, d_pair_a, d_pair_b, d_pb_fa, d_pb_fb;
+    DevBuf<int> d_free, d_pairs, d_pb_fa, d_pb_fb;
     DevBuf<double> d_raws, d_rawl, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
-    DevBuf<int> d_pair_l, d_singular;
+    DevBuf<int> d_singular;
     size_t n_pad = 0;
-    DevBuf<int> d_cnt;
-    DevBuf<LmState> d_state;
+    DevBuf<LmState> d_state;  // two copies, alternating by iteration (LmState)
     HostBuf<LmState> h_state;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -1692,11 +1730,18 @@ struct BundleAdjuster {
         p.free_idx = d_free.p;
         p.slot_hdr = reinterpret_cast<const int4*>(d_slot_hdr.p);
         p.slot_uv = reinterpret_cast<const double2*>(d_slot_uv.p);
-        p.chunk_pb = d_chunk_pb.p; p.chunk_pair = d_chunk_pair.p; p.pb_chunk = d_pb_chunk.p;
-        p.pair_a = d_pair_a.p; p.pair_b = d_pair_b.p; p.pair_l = d_pair_l.p; p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
+        p.pairs = reinterpret_cast<const int4*>(d_pairs.p);
+        p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
         return p;
     }
-    Work work() const {
+    // the kernels of LM iteration `it` read state copy it & 1 and work on copy (it + 1) & 1
+    Work work(int it) const {
+        Work w = work_at((it + 1) & 1);
+        w.st_prev = d_state.p + (it & 1);
+        return w;
+    }
+    // every kernel on one state copy (reset, K4, K7, build_system's combine)
+    Work work_at(int si) const {
         Work w;
         w.pose[0] = d_pose2.p; w.pose[1] = d_pose2.p + 7 * (size_t)G.n_kf;
         w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
@@ -1704,9 +1749,11 @@ struct BundleAdjuster {
         w.raws[0] = d_raws.p; w.raws[1] = d_raws.p + (size_t)kRawF * std::max<size_t>(n_pad, 1);
         w.rawl[0] = d_rawl.p; w.rawl[1] = d_rawl.p + (size_t)kLmF * std::max(G.n_lm, 1);
         w.singular = d_singular.p;
-        w.partA = d_partA.p; w.partD = d_partD.p; w.cnt = d_cnt.p;
+        w.partA = d_partA.p; w.partD = d_partD.p;
         w.cpart = d_cpart.p;
-        w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p; w.st = d_state.p;
+        w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p;
+        w.st = d_state.p + si;
+        w.st_prev = w.st;
         return w;
     }
 
@@ -1793,7 +1840,7 @@ struct BundleAdjuster {
                 }
             }
         for (size_t ps = 0; ps < n_pad; ++ps) hdr[8 * ps + 4] = hdr[8 * ps + 5] ? hdr[8 * ps + 4] : -1;
-        // camera blocks (fa <= fb) and their slot pairs (ascending landmark)
+        // camera blocks (fa <= fb)
         std::vector<int> pb_fa, pb_fb, pb_of((size_t)n_free * n_free, -1);
         for (int a = 0; a < n_free; ++a)
             for (int b = a; b < n_free; ++b) {
@@ -1802,7 +1849,14 @@ struct BundleAdjuster {
                 pb_fb.push_back(b);
             }
         const int n_pb = (int)pb_fa.size();
-        std::vector<std::vector<std::pair<int, int>>> pairs(n_pb);
+        // XCD groups: wave w (K4 / K6 workgroup w, whole landmarks) is dispatched to XCD w % 8, so
+        // the landmarks of group x are those of the waves w % 8 == x; their Schur chunks run on
+        // XCD x too (chunk c on XCD c % 8) and re-read the slot records K6 wrote there
+        std::vector<int> lm_group(n_lm, 0);
+        for (int w = 0; w < n_wave; ++w)
+            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) lm_group[slot_lm[sl]] = w % kGrp;
+        // slot pairs of each (group, camera block), ascending landmark
+        std::vector<std::vector<std::pair<int, int>>> pairs((size_t)kGrp * std::max(n_pb, 1));
         for (int l = 0; l < n_lm; ++l)
             for (int sa = lm_slot[l]; sa < lm_slot[l + 1]; ++sa) {
                 const int fa = free_idx[slot_kf[sa]];
@@ -1810,38 +1864,37 @@ struct BundleAdjuster {
                 for (int sb = sa; sb < lm_slot[l + 1]; ++sb) {
                     const int fb = free_idx[slot_kf[sb]];
                     if (fb < 0) continue;
-                    pairs[pb_of[fa * n_free + fb]].push_back({sa, sb});
+                    pairs[(size_t)lm_group[l] * n_pb + pb_of[fa * n_free + fb]].push_back({sa, sb});
                 }
             }
-        // chunks of <= 64 pairs; a block with no pair still gets one (empty) chunk so that its
-        // entries are written
-        std::vector<int> pa, pbv, pl, chunk_pb, chunk_pair{0}, pb_chunk{0};
-        for (int b = 0; b < n_pb; ++b) {
-            const int np = (int)pairs[b].size();
-            for (int c0 = 0; c0 < std::max(np, 1); c0 += 64) {
-                chunk_pb.push_back(b);
-                chunk_pair.push_back(chunk_pair.back() + std::min(64, np - c0));
+        // chunk 8 pb + x: the pairs of block pb in group x, padded to a common stride
+        const int n_chunk = kGrp * n_pb;
+        size_t stride = 1;
+        for (const auto& pv : pairs) stride = std::max(stride, pv.size());
+        std::vector<int> pq(4 * (size_t)n_chunk * stride, 0);
+        for (size_t i = 0; i < pq.size(); i += 4) pq[i] = -1;
+        for (int b = 0; b < n_pb; ++b)
+            for (int x = 0; x < kGrp; ++x) {
+                const auto& pv = pairs[(size_t)x * n_pb + b];
+                int* d = pq.data() + 4 * ((size_t)(kGrp * b + x) * stride);
+                for (size_t q = 0; q < pv.size(); ++q) {
+                    d[4 * q] = pslot[pv[q].first];
+                    d[4 * q + 1] = pslot[pv[q].second];
+                    d[4 * q + 2] = slot_lm[pv[q].first];
+                }
             }
-            pb_chunk.push_back((int)chunk_pb.size());
-            for (auto& pr : pairs[b]) {
-                pa.push_back(pslot[pr.first]);
-                pbv.push_back(pslot[pr.second]);
-                pl.push_back(slot_lm[pr.first]);
-            }
-        }
         {
             // every DMA of the previous set_problem finished (it ends with a stream sync) and no
             // kernel reads the stage, so it can be refilled (or regrown) now
             size_t need = stage_bytes(sizeof(double) * 7 * (size_t)n_kf) + stage_bytes(sizeof(double) * 3 * (size_t)n_lm);
-            for (size_t b : {free_idx.size(), hdr.size(), chunk_pb.size(), chunk_pair.size(), pb_chunk.size(), pa.size(),
-                             pbv.size(), pl.size(), pb_fa.size(), pb_fb.size()})
+            for (size_t b : {free_idx.size(), hdr.size(), pq.size(), pb_fa.size(), pb_fb.size()})
                 need += stage_bytes(sizeof(int) * b);
             need += stage_bytes(sizeof(double) * huv.size());
             if (h_stage.n < need) h_stage.alloc(need + need / 2);
             stage_off = 0;
         }
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
-        G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = (int)chunk_pb.size();
+        G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = (int)stride;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
         up(d_pose_init, pose7, 7 * (size_t)n_kf);
@@ -1851,13 +1904,12 @@ struct BundleAdjuster {
         up(d_free, free_idx);
         up(d_slot_hdr, hdr);
         up(d_slot_uv, huv);
-        up(d_chunk_pb, chunk_pb);
-        up(d_chunk_pair, chunk_pair);
-        up(d_pb_chunk, pb_chunk);
-        grow(d_cpart, (size_t)kBlockF * G.n_chunk);
-        up(d_pair_a, pa);
-        up(d_pair_b, pbv);
-        up(d_pair_l, pl);
+        up(d_pairs, pq);
+        {  // partial systems: slots nobody writes (a block without pairs in a group) stay zero
+            const size_t nc = (size_t)kGrp * ((size_t)36 * n_pb + 12 * n_free + 2);
+            grow(d_cpart, nc);
+            RSVIO_HIP(hipMemsetAsync(d_cpart.p, 0, sizeof(double) * nc, stream));
+        }
         up(d_pb_fa, pb_fa);
         up(d_pb_fb, pb_fb);
         grow(d_raws, (size_t)2 * kRawF * std::max<size_t>(n_pad, 1));
@@ -1868,8 +1920,7 @@ struct BundleAdjuster {
         grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
-        grow(d_cnt, (size_t)n_pb + 3);  // K6 arrivals, K4c block arrivals, K5 flag, wait timeout
-        grow(d_state, 1);
+        grow(d_state, 2);
         enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
         RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
@@ -1890,73 +1941,80 @@ struct BundleAdjuster {
     }
 
     void enqueue_reset(double lambda0) {
-        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), G.n_pb + 3);
-        hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work(), lambda0);
+        const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), 1);
+        hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work_at(0), lambda0);
         RSVIO_HIP(hipGetLastError());
     }
 
-    // K0 + K4: initial state and its linearisation (buffer 0)
+    // K0 + K4: initial state and its linearisation (buffer 0); the LM state in copy 0
     void enqueue_start(double lambda0) {
         if (G.n_wave)  // K0 folded into K4
-            hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work(), 1, lambda0);
+            hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work_at(0), 1, lambda0);
         else
             enqueue_reset(lambda0);
         RSVIO_HIP(hipGetLastError());
     }
 
-    // K4c + K4d: this rank's reduced camera system (current linearisation, current lambda) in
-    // d_sys, summed over ranks when sharded
-    void enqueue_linear_system() {
+    // K4c of iteration `it` (the pending decision, then this rank's chunk partials); sharded (or
+    // materialise): K4d sums them into d_sys (+ lambda on rank 0), all-reduced over the ranks
+    void enqueue_linear_system(int it, const LmArgs& la, bool materialise) {
         const Prob pr = prob();
-        const Work wk = work();
-        if (!sharded() && fuse_combine) {  // K4d folded into K4c (last chunk of each block)
-            hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk + 1), dim3(64), 0, stream, G, pr, wk, 1);
-            RSVIO_HIP(hipGetLastError());
-            return;
-        }
-        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(64), 0, stream, G, pr, wk, 0);
+        const Work wk = work(it);
+        hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk, la,
+                           sharded() ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(ba_schur_combine, dim3(G.n_pb + 1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+        if (!sharded() && !materialise) return;  // single rank: K5 sums the partials itself
+        hipLaunchKernelGGL(ba_schur_combine, dim3(1), dim3(256), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
         allreduce(d_sys.p, (size_t)36 * G.n_pb + 12 * G.n_free + 2);
     }
 
-    // register-resident factorisation for n_free <= 10, blocked LDS factorisation otherwise
-    void launch_camera_solve(const Prob& pr, const Work& wk) {
+    // register-resident factorisation for n_free <= 10, two rows per lane otherwise; combine:
+    // the reduced system is summed from the chunk partials in K5's prologue (single rank)
+    void launch_camera_solve(const Prob& pr, const Work& wk, int combine) {
         const dim3 g(1), b(256);
         switch (G.n_free <= 10 ? G.n_free : 0) {
 #define RSVIO_CAM(NF) \
-    case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk); break;
+    case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk, combine); break;
             RSVIO_CAM(1) RSVIO_CAM(2) RSVIO_CAM(3) RSVIO_CAM(4) RSVIO_CAM(5)
             RSVIO_CAM(6) RSVIO_CAM(7) RSVIO_CAM(8) RSVIO_CAM(9) RSVIO_CAM(10)
 #undef RSVIO_CAM
             default: {
                 const dim3 b2(64 * kX2Waves);
-                if (G.n_free <= 13) hipLaunchKernelGGL(ba_camera_solve_x2<13>, g, b2, 0, stream, G, pr, wk);
-                else if (G.n_free <= 16) hipLaunchKernelGGL(ba_camera_solve_x2<16>, g, b2, 0, stream, G, pr, wk);
-                else hipLaunchKernelGGL(ba_camera_solve_x2<20>, g, b2, 0, stream, G, pr, wk);
+                if (G.n_free <= 13) hipLaunchKernelGGL(ba_camera_solve_x2<13>, g, b2, 0, stream, G, pr, wk, combine);
+                else if (G.n_free <= 16) hipLaunchKernelGGL(ba_camera_solve_x2<16>, g, b2, 0, stream, G, pr, wk, combine);
+                else hipLaunchKernelGGL(ba_camera_solve_x2<20>, g, b2, 0, stream, G, pr, wk, combine);
                 break;
             }
         }
         RSVIO_HIP(hipGetLastError());
     }
 
-    void enqueue_iteration(const rsvio_lm_cfg& cfg) {
+    static LmArgs lm_args(const rsvio_lm_cfg& cfg) {
+        return LmArgs{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
+    }
+
+    // LM iteration `it`: K4c (decision of it - 1 + Schur partials), [K4d + all-reduce], K5, K6,
+    // [K6r + all-reduce of the trial scalars].  Its own decision is taken by iteration it + 1's
+    // K4c or by enqueue_decide at the end of the chunk.
+    void enqueue_iteration(const rsvio_lm_cfg& cfg, int it) {
         const Prob pr = prob();
-        const Work wk = work();
-        enqueue_linear_system();
-        const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
-        launch_camera_solve(pr, wk);
-        // single rank: the last K6 wave takes the decision; sharded: reduce, all-reduce, K7
-        const int fuse = (!sharded() && G.n_wave) ? 1 : 0;
-        if (G.n_wave)
-            hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, fuse, la);
+        const Work wk = work(it);
+        enqueue_linear_system(it, lm_args(cfg), false);
+        launch_camera_solve(pr, wk, sharded() ? 0 : 1);
+        if (G.n_wave) hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
+        RSVIO_HIP(hipGetLastError());
         if (sharded()) {
             hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
+            RSVIO_HIP(hipGetLastError());
             allreduce(d_trial4.p, 4);
         }
-        if (!fuse)
-            hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, pr, wk, sharded() ? 1 : 0, la);
+    }
+
+    // K7: the decision pending after `it` iterations, in place in state copy it & 1
+    void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
+        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, prob(), work_at(it & 1), sharded() ? 1 : 0,
+                           lm_args(cfg));
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -1973,10 +2031,12 @@ struct BundleAdjuster {
     } pend;
 
     void enqueue_chunk(int k) {
-        for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg);
+        for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg, pend.enq + i);
         pend.enq += k;
+        enqueue_decide(pend.cfg, pend.enq);
         RSVIO_HIP(hipEventRecord(ev1, stream));
-        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p + (pend.enq & 1), sizeof(LmState), hipMemcpyDeviceToHost,
+                                 stream));
     }
 
     void start(const rsvio_lm_cfg& cfg) {
@@ -1998,7 +2058,8 @@ struct BundleAdjuster {
         if (start_graph(cfg, k)) {
             pend.enq += k;
             RSVIO_HIP(hipEventRecord(ev1, stream));
-            RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+            RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p + (pend.enq & 1), sizeof(LmState), hipMemcpyDeviceToHost,
+                                     stream));
         } else {
             enqueue_start(cfg.lambda_init);
             enqueue_chunk(k);
@@ -2119,7 +2180,7 @@ struct BundleAdjuster {
     void get_state(double* pose7, double* pW) {
         require_idle("get_state");
         const int cur = h_state.p->cur;
-        const Work wk = work();
+        const Work wk = work_at(0);
         RSVIO_HIP(hipMemcpyAsync(pose7, wk.pose[cur], sizeof(double) * 7 * G.n_kf, hipMemcpyDeviceToHost, stream));
         if (G.n_lm)
             RSVIO_HIP(hipMemcpyAsync(pW, wk.pw[cur], sizeof(double) * 3 * G.n_lm, hipMemcpyDeviceToHost, stream));
@@ -2132,10 +2193,10 @@ struct BundleAdjuster {
         G.huber_delta = huber_delta;
         G.chol = 0;
         enqueue_start(lambda);
-        enqueue_linear_system();
+        enqueue_linear_system(0, LmArgs{1, 0.0, 0.0}, true);
         std::vector<double> sys((size_t)36 * G.n_pb + 12 * G.n_free + 2);
         RSVIO_HIP(hipMemcpyAsync(sys.data(), d_sys.p, sizeof(double) * sys.size(), hipMemcpyDeviceToHost, stream));
-        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
+        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p + 1, sizeof(LmState), hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
         const int n = 6 * G.n_free;
         std::vector<int> fa, fb;
@@ -2161,8 +2222,8 @@ struct BundleAdjuster {
         G.huber_delta = huber_delta;
         G.chol = 0;
         enqueue_start(lambda);
-        enqueue_linear_system();
-        launch_camera_solve(prob(), work());
+        enqueue_linear_system(0, LmArgs{1, 0.0, 0.0}, false);
+        launch_camera_solve(prob(), work(0), sharded() ? 0 : 1);
         RSVIO_HIP(hipMemcpyAsync(dc, d_dc.p, sizeof(double) * 6 * G.n_free, hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
     }

@@ -63,7 +63,25 @@ int guarded(F&& f) {
         if (n > 4096 * 32) n = 4096 * 32;                                                  \
         return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(unsigned long long) * n); \
     }
+// wall-clock stamps (s_memrealtime, 100 MHz, one clock for every CU): slot k of row blockIdx,
+// taken at issue (no drain), so kernel entry / exit spreads and boundary gaps can be read
+#define RSVIO_RT_DECL static __device__ unsigned long long g_rt[4096 * 16];
+#define RTSTAMP(k)                                                                              \
+    do {                                                                                        \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                              \
+            g_rt[blockIdx.x * 16 + (k)] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  \
+    } while (0)
+#define RSVIO_RT_READER(name)                                                              \
+    extern "C" int name(unsigned long long* out, int n) {                                  \
+        if (n > 4096 * 16) n = 4096 * 16;                                                  \
+        return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt), sizeof(unsigned long long) * n); \
+    }
 #else
+#define RSVIO_RT_DECL
+#define RTSTAMP(k) \
+    do {           \
+    } while (0)
+#define RSVIO_RT_READER(name)
 #define RSVIO_DBG_DECL
 #define STAMP(k) \
     do {         \

@@ -56,3 +56,7 @@ report("linearize (initial)", [11, 12, 14], ["obs linearize", "store + partials"
 report("schur_chunks", [16, 17, 18], ["pair products", "lane-ordered chunk sum"])
 report("backsub_relinearize", [20, 22, 23, 24, 25, 21],
        ["W^T dc", "dp (first lanes)", "trial linearise", "store linearisation", "partials"])
+
+r = T[1]
+print("schur_chunks block 1 (cycles): pairs+block ids loaded %d, decision gathers+sums %d, lm_update %d, "
+      "records+products %d, reduce+store %d" % (r[27] - r[26], r[29] - r[27], r[28] - r[29], r[17] - r[16], r[18] - r[17]))

@@ -53,7 +53,10 @@ __global__ void u16_stride(const uint8_t* __restrict__ p, size_t n_loads, size_t
 
 // one wave per patch: lanes < 52 read 4 bytes (2 rows x 2 columns, like a bilinear sample)
 // around a pattern point inside an 11 x 11 window of a 752-wide image
-__global__ void u8_gath(const uint8_t* __restrict__ img, const int* __restrict__ base, unsigned* __restrict__ sink) {
+// `never` is a kernel argument (not a constant the compiler can bound the sum against), so the
+// loads are kept: a constant test that the 4-byte sum provably never meets lets them be deleted
+__global__ void u8_gath(const uint8_t* __restrict__ img, const int* __restrict__ base, unsigned* __restrict__ sink,
+                        unsigned never) {
     const int lane = threadIdx.x;
     const int b = base[blockIdx.x];
     unsigned acc = 0;
@@ -62,7 +65,7 @@ __global__ void u8_gath(const uint8_t* __restrict__ img, const int* __restrict__
         const uint8_t* q = img + b + dy * 752 + dx;
         acc = q[0] + q[1] + q[752] + q[753];
     }
-    if (acc == 0xFFFFFFFFu) sink[0] = acc;
+    if (acc == never) sink[0] = acc;
 }
 
 int main() {
@@ -108,7 +111,7 @@ int main() {
     CK(hipMalloc(&d_base, n_patch * sizeof(int)));
     CK(hipMemcpy(d_base, base.data(), n_patch * sizeof(int), hipMemcpyHostToDevice));
     CK(hipMemset(flush, 7, size_t(512) << 20));
-    hipLaunchKernelGGL(u8_gath, dim3(n_patch), dim3(64), 0, 0, bufs[4], d_base, sink);
+    hipLaunchKernelGGL(u8_gath, dim3(n_patch), dim3(64), 0, 0, bufs[4], d_base, sink, 0xFFFFFFFFu);
     CK(hipDeviceSynchronize());
     printf("expected line bytes: wide16 %zu byte1 %zu u16_l128 %zu u16_l64 %zu u8_gath %zu (distinct 128-B lines x 128)\n",
            kBytes, kBytes, kBytes, kBytes, lines.size() * 128);
