@@ -55,19 +55,26 @@ RSVIO_RT_DECL
 
 constexpr int kMaxFree = 20;            // camera system up to 120 x 120 in LDS
 constexpr int kMaxN = 6 * kMaxFree;
-// raw linearisation per slot, one contiguous 384-B record (AoS): W (6x3), U (6x6 packed upper),
-// g_c (6), pad; and per landmark (96 B): V (3x3 packed upper), g_p (3), pad
-enum { RW = 0, RU = 18, RG = 39, kRawF = 48 };
+// Raw linearisation per slot, one contiguous 224-B record (AoS).  factors.rs:437-441: the
+// translation columns of the 2x9 Jacobian equal the point columns (J = [Jp | Jp | Jr]), so of a
+// slot's W = Jc^T Jp (6x3), U = Jc^T Jc (6x6) and g_c = Jc^T r only the rotation parts are new:
+//   W = [Vs; Wr],  U = [[Vs, Wr^T], [Wr, Ur]],  g_c = [gp_s; gr]
+// with Vs, gp_s the slot's own landmark-block contribution.  Record: Vs (3x3 packed upper, 6),
+// gp_s (3), Wr (3x3, rotation row x point column, 9), Ur (3x3 packed upper, 6), gr (3), pad --
+// 27 values instead of 48, and half the multiply-adds of the linearisation.  Per landmark
+// (96 B): V (3x3 packed upper), g_p (3), pad.
+enum { RV = 0, RGP = 6, RWR = 9, RUR = 18, RGR = 24, kRawF = 28 };
 enum { LV = 0, LG = 6, kLmF = 12 };
 constexpr int kBlockF = 48;             // 36 S + 6 b + 6 g_c per camera block workgroup
 constexpr int kPartA = 2;               // cost of the initial linearisation, 0 (per wave)
 constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per wave
 // Landmark groups of the Schur reduction: wave w (K4 / K6 workgroup w, dispatched round robin to
-// XCD w % 8) belongs to group w % kGrp, and K4c workgroup 4 pb + g (on XCD g or g + 4) reduces
-// block pb over group g -- each slot record is fetched into at most two XCDs' L2 per launch,
-// and K5 sums kGrp partial systems (fewer copies: less to pull across the fabric into one CU)
-constexpr int kGrp = 4;
-constexpr int kSchurThreads = 512;      // K4c workgroup: one pair per thread per pass
+// XCD w % 8) belongs to group w % kGrp, and K4c workgroup 8 pb + g (on XCD g) reduces block pb
+// over group g -- each slot record is fetched into one XCD's L2 per launch; K5 sums the kGrp
+// partial systems.  (4 groups of 512-thread workgroups: 42 vs 39 us per LM iteration -- two
+// waves per SIMD then share the FP64 pipe -- although K5's combine moved half the bytes.)
+constexpr int kGrp = 8;
+constexpr int kSchurThreads = 256;      // K4c workgroup: one pair per thread per pass
 
 struct Mat4 {
     double m[16];
@@ -237,7 +244,7 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
 // (camera blocks, free keyframes only), cost.
 // ---------------------------------------------------------------------------------------
 struct SlotLin {
-    double V[6], gp[3], W[18], U[21], gc[6], cost;
+    double V[6], gp[3], Wr[9], Ur[6], gr[3], cost;
 };
 
 __device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P, const double p[3], int nobs,
@@ -247,11 +254,11 @@ __device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P,
 #pragma unroll
     for (int i = 0; i < 3; ++i) L.gp[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 18; ++i) L.W[i] = 0.0;
+    for (int i = 0; i < 9; ++i) L.Wr[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 21; ++i) L.U[i] = 0.0;
+    for (int i = 0; i < 6; ++i) L.Ur[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) L.gc[i] = 0.0;
+    for (int i = 0; i < 3; ++i) L.gr[i] = 0.0;
     L.cost = 0.0;
     // unrolled over the <= 2 observations of a slot: a runtime-indexed uvq[o] was lowered to a
     // scratch-memory array (a store + reload on the linearisation's critical path)
@@ -275,12 +282,12 @@ __device__ __forceinline__ void slot_linearize(const Geometry& G, const Pose& P,
         if (fr) {
             int u = 0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) {
+            for (int a = 0; a < 3; ++a) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) L.W[a * 3 + c] += wt * (J[0][3 + a] * J[0][c] + J[1][3 + a] * J[1][c]);
+                for (int c = 0; c < 3; ++c) L.Wr[a * 3 + c] += wt * (J[0][6 + a] * J[0][c] + J[1][6 + a] * J[1][c]);
 #pragma unroll
-                for (int c = a; c < 6; ++c) L.U[u++] += wt * (J[0][3 + a] * J[0][3 + c] + J[1][3 + a] * J[1][3 + c]);
-                L.gc[a] += J[0][3 + a] * wr0 + J[1][3 + a] * wr1;
+                for (int c = a; c < 3; ++c) L.Ur[u++] += wt * (J[0][6 + a] * J[0][6 + c] + J[1][6 + a] * J[1][6 + c]);
+                L.gr[a] += J[0][6 + a] * wr0 + J[1][6 + a] * wr1;
             }
         }
     }
@@ -302,12 +309,16 @@ __device__ void store_linearization(const Work& Wk, int buf, int s, int lane, bo
     if (act && fr) {
         double rec[kRawF];
 #pragma unroll
-        for (int i = 0; i < 18; ++i) rec[RW + i] = L.W[i];
+        for (int i = 0; i < 6; ++i) rec[RV + i] = L.V[i];
 #pragma unroll
-        for (int i = 0; i < 21; ++i) rec[RU + i] = L.U[i];
+        for (int i = 0; i < 3; ++i) rec[RGP + i] = L.gp[i];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) rec[RG + i] = L.gc[i];
-        rec[45] = rec[46] = rec[47] = 0.0;
+        for (int i = 0; i < 9; ++i) rec[RWR + i] = L.Wr[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) rec[RUR + i] = L.Ur[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) rec[RGR + i] = L.gr[i];
+        rec[27] = 0.0;
         double2* dst = reinterpret_cast<double2*>(Wk.raws[buf] + (size_t)s * kRawF);
 #pragma unroll
         for (int i = 0; i < kRawF / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
@@ -599,37 +610,49 @@ __device__ LmState lm_decide(const Geometry& G, const Prob& Pr, const Work& Wk, 
 // One slot pair of a camera block.  DIAG: a diagonal block's pairs are (s, s) (a landmark has
 // one slot per keyframe), so W is loaded once and U, g_c join; off-diagonal blocks touch only
 // the 36 S entries -- two instantiations keep each one's register footprint to its own needs.
+// W (6x3) of a slot from its record: rows 0-2 = Vs (symmetric), rows 3-5 = Wr
+__device__ __forceinline__ void slot_w(const double* rec, double W[18]) {
+    const double* v = rec + RV;
+    const double Vs[9] = {v[0], v[1], v[2], v[1], v[3], v[4], v[2], v[4], v[5]};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) W[i] = Vs[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) W[9 + i] = rec[RWR + i];
+}
+
 template <bool DIAG>
 __device__ __forceinline__ void schur_pair(const Work& Wk, int cur, double lambda, int chol, int sa, int sb, int l,
                                            double (&acc)[kBlockF]) {
     const double2* ra = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sa * kRawF);
     const double2* rb = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)sb * kRawF);
     const double2* rl = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)l * kLmF);
-    double Wa[18], Wb[18], Lm[10];
+    // record a: all 28 values on a diagonal block (Ur, gp_s, gr join), else Vs, gp_s, Wr (18)
+    constexpr int NA = DIAG ? kRawF / 2 : 9;
+    double Ra[2 * NA], Rb[18], Lm[10];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        const double2 x = ra[RW / 2 + i];
-        Wa[2 * i] = x.x; Wa[2 * i + 1] = x.y;
-        if constexpr (!DIAG) {
-            const double2 y = rb[RW / 2 + i];
-            Wb[2 * i] = y.x; Wb[2 * i + 1] = y.y;
-        }
+    for (int i = 0; i < NA; ++i) {
+        const double2 x = ra[i];
+        Ra[2 * i] = x.x; Ra[2 * i + 1] = x.y;
     }
-    if constexpr (DIAG)
+    if constexpr (!DIAG)
 #pragma unroll
-        for (int i = 0; i < 18; ++i) Wb[i] = Wa[i];
+        for (int i = 0; i < 9; ++i) {
+            const double2 y = rb[i];
+            Rb[2 * i] = y.x; Rb[2 * i + 1] = y.y;
+        }
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         const double2 x = rl[i];
         Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
     }
-    double r[28];  // record entries 18..45: U (21), g_c (6), pad -- diagonal blocks only
-    if constexpr (DIAG)
+    double Wa[18], Wb[18];
+    slot_w(Ra, Wa);
+    if constexpr (DIAG) {
 #pragma unroll
-        for (int i = 0; i < 14; ++i) {
-            const double2 v = ra[RU / 2 + i];
-            r[2 * i] = v.x; r[2 * i + 1] = v.y;
-        }
+        for (int i = 0; i < 18; ++i) Wb[i] = Wa[i];  // a diagonal block's pairs are (s, s)
+    } else {
+        slot_w(Rb, Wb);
+    }
     double Vi[3][3];
     if (!landmark_inverse(Lm + LV, lambda, Vi, chol)) *Wk.singular = 1;
     double Ya[18];  // Y_a = W_a (V + lambda I)^-1
@@ -644,18 +667,27 @@ __device__ __forceinline__ void schur_pair(const Work& Wk, int cur, double lambd
         for (int k = 0; k < 6; ++k)
             acc[a * 6 + k] -= fma(Ya[a * 3 + 2], Wb[k * 3 + 2], fma(Ya[a * 3 + 1], Wb[k * 3 + 1], Ya[a * 3] * Wb[k * 3]));
     if constexpr (DIAG) {
-        int u = 0;
+        // U = [[Vs, Wr^T], [Wr, Ur]] and g_c = [gp_s; gr]
+        double U[36];
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
+        for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int k = a; k < 6; ++k) {
-                const double v = r[u++];
-                acc[a * 6 + k] += v;
-                if (k != a) acc[k * 6 + a] += v;
+            for (int c = 0; c < 3; ++c) {
+                U[a * 6 + c] = Wa[a * 3 + c];              // Vs
+                U[(3 + a) * 6 + c] = Wa[(3 + a) * 3 + c];  // Wr
+                U[c * 6 + 3 + a] = Wa[(3 + a) * 3 + c];    // Wr^T
             }
+        const double* ur = Ra + RUR;
+        const double Ur[9] = {ur[0], ur[1], ur[2], ur[1], ur[3], ur[4], ur[2], ur[4], ur[5]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) U[(3 + a) * 6 + 3 + c] = Ur[a * 3 + c];
+#pragma unroll
+        for (int i = 0; i < 36; ++i) acc[i] += U[i];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const double gca = r[RG - RU + a];
+            const double gca = a < 3 ? Ra[RGP + a] : Ra[RGR + a - 3];
             const double yg = fma(Ya[a * 3 + 2], Lm[LG + 2], fma(Ya[a * 3 + 1], Lm[LG + 1], Ya[a * 3] * Lm[LG]));
             acc[36 + a] += yg - gca;  // b = -g_c + sum Y g_p
             acc[42 + a] += gca;
@@ -1415,12 +1447,14 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w
     const int kfc = act ? kf : 0, lc = act ? l : 0, fc = (act && fr) ? h1.x : 0;
     double Wv[18], d6[6], Lm[10], pc[3], p7[7];
     {
-        const double2* wr = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)s * kRawF + RW);
+        const double2* wr = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)s * kRawF);
+        double rec[18];  // Vs, gp_s, Wr
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             const double2 x = wr[i];
-            Wv[2 * i] = x.x; Wv[2 * i + 1] = x.y;
+            rec[2 * i] = x.x; rec[2 * i + 1] = x.y;
         }
+        slot_w(rec, Wv);
         const double2* lr = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)lc * kLmF);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
