@@ -1590,12 +1590,22 @@ __device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
     return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
 }
 
-__global__ __launch_bounds__(256) void ba_p2p_allreduce(double* buf, int n, P2P P, unsigned long long gen,
-                                                        int* err) {
-    const int tid = threadIdx.x, nr = P.nranks, me = P.rank, par = (int)(gen & 1);
+// One exchange by a whole 256-thread block: this rank's message msg[0..n) (LDS or global) is
+// pushed into slot [parity][rank] of every peer's buffer, the flags are raised (system-scope
+// release), the block waits for every peer's flag in its own buffer (bounded: an error flag the
+// host checks), and out[i] = the slots summed in rank order -- identical bits on every rank.
+// The generation lives in device memory (xgen, advanced by each exchange): every rank runs the
+// same exchange sequence, so the counters agree, and a captured graph replays correctly.
+__device__ void p2p_exchange(const double* msg, int n, const P2P& P, unsigned long long* xgen, int* err, double* out) {
+    __shared__ unsigned long long sgen;
+    const int tid = threadIdx.x, nr = P.nranks, me = P.rank;
+    if (tid == 0) sgen = *xgen + 1;
+    __syncthreads();
+    const unsigned long long gen = sgen;
+    const int par = (int)(gen & 1);
     for (int r = 0; r < nr; ++r) {
         double* dst = P.peer[r] + (size_t)(par * kP2PMax + me) * kP2PMsg;
-        for (int i = tid; i < n; i += 256) dst[i] = buf[i];
+        for (int i = tid; i < n; i += 256) dst[i] = msg[i];
     }
     __threadfence_system();
     __syncthreads();
@@ -1619,8 +1629,46 @@ __global__ __launch_bounds__(256) void ba_p2p_allreduce(double* buf, int n, P2P 
         double v = 0.0;
         for (int r = 0; r < nr; ++r)
             v += __hip_atomic_load(mine + (size_t)r * kP2PMsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        buf[i] = v;
+        out[i] = v;
     }
+    if (tid == 0) *xgen = gen;
+}
+
+// generic exchange of buf[0..n) in place (the attach self-test)
+__global__ __launch_bounds__(256) void ba_p2p_allreduce(double* buf, int n, P2P P, unsigned long long* xgen,
+                                                        int* err) {
+    p2p_exchange(buf, n, P, xgen, err, buf);
+}
+
+// X1 (sharded, P2P): K4d folded into the exchange -- this rank's reduced system from its chunk
+// partials (+ lambda on rank 0; its initial cost and singular flag) is built in LDS, exchanged,
+// and the rank-ordered sum lands in sys.  One launch instead of combine + all-reduce.
+__global__ __launch_bounds__(256) void ba_p2p_sys(Geometry G, Prob Pr, Work Wk, P2P P, unsigned long long* xgen,
+                                                  int* err) {
+    __shared__ double msg[kP2PMsg];
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    combine_system<256>(G, Pr, Wk, msg, st->lambda, P.rank == 0);
+    __syncthreads();
+    if (threadIdx.x == 0) *Wk.singular = 0;
+    p2p_exchange(msg, (int)sys_len(G), P, xgen, err, Wk.sys);
+}
+
+// X2 (sharded, P2P): K6r folded into the exchange -- this rank's trial scalars (|x|^2 of the
+// poses on rank 0), exchanged and summed into trial4 for the next decision.
+__global__ __launch_bounds__(256) void ba_p2p_trial(Geometry G, Prob Pr, Work Wk, P2P P, unsigned long long* xgen,
+                                                    int* err) {
+    __shared__ double msg[4];
+    const LmState s = *Wk.st;
+    if (s.done) return;
+    if (threadIdx.x < 64) {
+        double v[4];
+        trial_scalars_wave(G, Pr, Wk, s, P.rank == 0 ? 1 : 0, v);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; ++k) msg[k] = v[k];
+    }
+    __syncthreads();
+    p2p_exchange(msg, 4, P, xgen, err, Wk.trial4);
 }
 
 }  // namespace
@@ -1655,8 +1703,10 @@ struct BundleAdjuster {
                a.parameter_tolerance == b.parameter_tolerance && a.huber_delta == b.huber_delta &&
                a.lambda_init == b.lambda_init && a.linear_solver == b.linear_solver;
     }
+    // (single rank, or sharded over the P2P exchange, whose generation counter lives on the
+    // device; RCCL calls stay out of the graph)
     bool start_graph(const rsvio_lm_cfg& cfg, int k) {
-        if (sharded() || !graphs_ok) return false;
+        if (coll == 1 || !graphs_ok) return false;
         if (!(gexec && g_k == k && same_cfg(g_cfg, cfg))) {
             drop_graph();
             if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
@@ -1707,8 +1757,8 @@ struct BundleAdjuster {
     double* xbuf = nullptr;               // P2P exchange buffer (uncached, IPC-exported)
     P2P p2p{};
     bool p2p_opened[kP2PMax] = {};
-    unsigned long long p2p_gen = 0;
     DevBuf<int> d_p2p_err;
+    DevBuf<unsigned long long> d_xgen;  // P2P exchange generation (advanced on the device)
 
     void init(const rsvio_ba_params& p) {
         P = p;
@@ -1965,7 +2015,7 @@ struct BundleAdjuster {
         if (!sharded() || n == 0) return;
         if (coll == 2) {
             if (n > kP2PMsg) throw std::runtime_error("message exceeds the P2P slot");
-            hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, buf, (int)n, p2p, ++p2p_gen,
+            hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, buf, (int)n, p2p, d_xgen.p,
                                d_p2p_err.p);
             RSVIO_HIP(hipGetLastError());
             return;
@@ -1998,6 +2048,11 @@ struct BundleAdjuster {
                            sharded() ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
         if (!sharded() && !materialise) return;  // single rank: K5 sums the partials itself
+        if (coll == 2) {  // P2P: combine + exchange in one launch (X1)
+            hipLaunchKernelGGL(ba_p2p_sys, dim3(1), dim3(256), 0, stream, G, pr, wk, p2p, d_xgen.p, d_p2p_err.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
         hipLaunchKernelGGL(ba_schur_combine, dim3(1), dim3(256), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
         allreduce(d_sys.p, (size_t)36 * G.n_pb + 12 * G.n_free + 2);
@@ -2038,7 +2093,10 @@ struct BundleAdjuster {
         launch_camera_solve(pr, wk, sharded() ? 0 : 1);
         if (G.n_wave) hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
         RSVIO_HIP(hipGetLastError());
-        if (sharded()) {
+        if (coll == 2) {  // P2P: trial scalars + exchange in one launch (X2)
+            hipLaunchKernelGGL(ba_p2p_trial, dim3(1), dim3(256), 0, stream, G, pr, wk, p2p, d_xgen.p, d_p2p_err.p);
+            RSVIO_HIP(hipGetLastError());
+        } else if (sharded()) {
             hipLaunchKernelGGL(ba_reduce_trial, dim3(1), dim3(64), 0, stream, G, pr, wk, rank == 0 ? 1 : 0);
             RSVIO_HIP(hipGetLastError());
             allreduce(d_trial4.p, 4);
@@ -2136,6 +2194,8 @@ struct BundleAdjuster {
             RSVIO_HIP(hipMemset(xbuf, 0, bytes));
             d_p2p_err.alloc(1);
             RSVIO_HIP(hipMemset(d_p2p_err.p, 0, sizeof(int)));
+            d_xgen.alloc(1);
+            RSVIO_HIP(hipMemset(d_xgen.p, 0, sizeof(unsigned long long)));
         }
         RSVIO_HIP(hipIpcGetMemHandle(h, xbuf));
     }
@@ -2168,7 +2228,7 @@ struct BundleAdjuster {
         DevBuf<double> t(2);
         const double tv[2] = {(double)(rk + 1), 1.0};
         RSVIO_HIP(hipMemcpy(t.p, tv, sizeof tv, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, 2, P, ++p2p_gen, d_p2p_err.p);
+        hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, 2, P, d_xgen.p, d_p2p_err.p);
         RSVIO_HIP(hipGetLastError());
         double out[2] = {0.0, 0.0};
         RSVIO_HIP(hipMemcpyAsync(out, t.p, sizeof out, hipMemcpyDeviceToHost, stream));
@@ -2180,10 +2240,12 @@ struct BundleAdjuster {
         nranks = nr;
         rank = rk;
         coll = 2;
+        drop_graph();  // the iteration's launch sequence changes with the collective
     }
 
     void p2p_detach() {
         if (coll == 2) coll = comm ? 1 : 0;
+        drop_graph();
     }
 
     // run on a caller-owned stream (e.g. one restricted to a CU subset); nullptr = own stream
@@ -2408,6 +2470,7 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
         B.nranks = nranks;
         B.rank = rank;
         B.coll = 1;
+        B.drop_graph();
         return (int)RSVIO_OK;
     });
 }

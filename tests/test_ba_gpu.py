@@ -251,7 +251,7 @@ def test_async_wrong_call_order_refused(gpu, cfg3):
     a.close()
 
 
-def _p2p_worker(rank, world, port, out_dir):
+def _p2p_worker(rank, world, port, out_dir, n_lm=2000):
     import os
 
     import torch.distributed as dist
@@ -261,7 +261,7 @@ def _p2p_worker(rank, world, port, out_dir):
     try:
         from rsvio import synthetic as S
         from rsvio.ba import BundleAdjuster
-        full = S.ba_problem()
+        full = S.ba_problem(n_lm=n_lm)
         shard = full.shard(rank, world)
         ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
         mine = ba.p2p_export(world)
@@ -299,6 +299,29 @@ def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
     assert np.abs(r0["pose"] - po).max() < 1e-7
     pw = np.concatenate([r0["pw"], r1["pw"]])
     assert np.abs(pw - pwo).max() < 1e-6
+
+
+def test_sharded_p2p_weak_scaling_size_matches_oracle(gpu, oracle, tmp_path):
+    """The weak-scaling configuration of the bench at N = 2: 2,000 landmarks per rank (4,000 in
+    all, 48,000 observations), the fused P2P path (K4c, combine+exchange, K5, K6,
+    trial+exchange: 5 launches per LM iteration), against the oracle's single 4,000-landmark
+    solve within the config-3 tolerances."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from rsvio import synthetic as S
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_p2p_worker, args=(2, port, str(tmp_path), 4000), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = np.load(tmp_path / "r0.npz"), np.load(tmp_path / "r1.npz")
+    assert np.array_equal(r0["pose"], r1["pose"]) and np.array_equal(r0["res"], r1["res"])
+    full = S.ba_problem(n_lm=4000)
+    po, pwo, ro = oracle.ba_solve(full)
+    assert int(r0["res"][0]) == ro.status and int(r0["res"][1]) == ro.iterations
+    assert abs(r0["res"][2] - ro.final_cost) <= 1e-8 * ro.initial_cost
+    assert np.abs(r0["pose"] - po).max() < 1e-7
+    assert np.abs(np.concatenate([r0["pw"], r1["pw"]]) - pwo).max() < 1e-6
 
 
 def _small_fallback_problem(seed=3):
