@@ -505,16 +505,18 @@ def pmc_traffic(kernel: str, shape: str = "u8_gath"):
     files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
     if not files:
         return None, None
-    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    ks = json.load(open(files[-1]))["kernels"]
+    # summary keys carry the template instantiation ("void lk_track_kernel<3>")
+    k = ks.get(kernel) or next((v for n, v in ks.items() if n.split("<")[0].split()[-1] == kernel), None)
     if not k:
         return None, None
     mult, msrc = 2.0, "guide x2 (wide reads)"
     cal = sorted((ROOT / "profiles").glob("*_fetch_calib.json"))
     if cal:
         c = json.load(open(cal[-1]))["kernels"].get(shape)
-        # a calibration outside [1, 8] is a broken measurement (e.g. loads the compiler deleted),
-        # never a counter correction: keep the guide's x2 then
-        if c and c.get("multiplier") and 1.0 <= float(c["multiplier"]) <= 8.0:
+        # a calibration outside [1/4, 8] is a broken measurement (e.g. loads the compiler
+        # deleted), never a counter correction: keep the guide's x2 then
+        if c and c.get("multiplier") and 0.25 <= float(c["multiplier"]) <= 8.0:
             mult, msrc = float(c["multiplier"]), f"{cal[-1].name}:{shape}"
     f, w = k["fetch_size_bytes_per_dispatch"], k["write_size_bytes_per_dispatch"]
     return f * mult + w, {"source": files[-1].name, "fetch_raw": round(f), "write_raw": round(w),
