@@ -1008,6 +1008,39 @@ __device__ __forceinline__ void k5_result(LmState* st, int ok, double d2, double
     st->pending = 1;
 }
 
+// K5's tail (wave 0): dc = x, |dc|^2, g_c.dc, trial poses by SE3 (+) from the prefetched
+// current poses, the state's step fields.  A[0..n) is LDS scratch for dc.
+template <int NF>
+__device__ void k5_finish(const Geometry& G, const Work& Wk, double* A, double x, double gcl_v, int n, int lane,
+                          const double (&p7)[7], int fidx) {
+    LmState* st = Wk.st;
+    const double d2 = wave_sum_det(x * x);
+    const double gd = wave_sum_det(lane < n ? gcl_v * x : 0.0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n) {
+        Wk.dc[lane] = x;
+        A[lane] = x;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    STAMP(4);
+    if (lane < G.n_kf) {  // trial poses from the prefetched current poses
+        double* q = Wk.pose[1 - st->cur] + 7 * lane;
+        if (fidx < 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) q[i] = p7[i];
+        } else {
+            double qv[7];
+            se3_plus(p7, A + 6 * fidx, qv);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) q[i] = qv[i];
+        }
+    }
+    STAMP(5);
+    if (lane == 0) k5_result(st, 1, d2, gd);
+    STAMP(6);
+}
+
 template <int NF>
 __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& Wk, const double* sys, double* A,
                                 int* badw, int* progress, int n, int tid, const double (&p7)[7], int fidx) {
@@ -1044,32 +1077,66 @@ __device__ void camera_solve_w4(const Geometry& G, const Prob& Pr, const Work& W
         yv = lane < j ? upd : yv;
     }
     STAMP(3);
-    const double x = lane < n ? yv : 0.0;
-    const double d2 = wave_sum_det(x * x);
-    const double gd = wave_sum_det(lane < n ? gcl_v * x : 0.0);
-    __builtin_amdgcn_wave_barrier();
-    if (lane < n) {
-        Wk.dc[lane] = x;
-        A[lane] = x;  // A[0..n) holds dc for the pose updates (Lc lies past A[128])
+    k5_finish<NF>(G, Wk, A, lane < n ? yv : 0.0, gcl_v, n, lane, p7, fidx);
+}
+
+// K5 alternative (A/B, RSVIO_K5=gj1): one wave, Gauss-Jordan on [S | b] with lane = row and
+// the full symmetric rows in registers -- no inter-wave hand-off and no back substitution (each
+// pivot also eliminates upward; x_i = b'_i / d_i at the end).  Pivot K: l_i = a_iK / d_K (0 on
+// the pivot row), a_ij -= l_i A[j][K] for j > K (the trailing block is symmetric, so the pivot
+// row's entries are column K's, written to LDS by every lane in one store and read back as
+// broadcasts), b_i -= l_i b_K.  The next pivot's column uses readlanes (no LDS round trip on
+// the 1/d chain); the other columns get the previous pivot's update one step late, from LDS
+// reads issued a step earlier.  (Tolerance parity like the pipelined LDL^T: same pivots, a
+// different elimination order.)
+constexpr int kGjLd = 65;
+
+template <int NP, int K>
+__device__ __forceinline__ void gj1_pivot(double (&a)[NP + 1], double (&uq)[NP], double* U, int lane, bool& bad,
+                                          double inv, double lp) {
+    if constexpr (K >= 1 && K + 1 < NP) a[K + 1] = fma(-lp, uq[K + 1], a[K + 1]);  // pivot K-1, deferred
+    const double aK = a[K];
+    const double l = lane == K ? 0.0 : aK * inv;
+    U[K * kGjLd + lane] = aK;
+    const double ub = rl64(a[NP], K);
+    double inv_next = 1.0;
+    if constexpr (K + 1 < NP) {
+        a[K + 1] = fma(-l, rl64(aK, K + 1), a[K + 1]);
+        const double piv = rl64(a[K + 1], K + 1);
+        bad |= !(piv > 0.0) || !isfinite(piv);
+        inv_next = rcp_f64(piv);
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    STAMP(4);
-    if (lane < G.n_kf) {  // trial poses from the prefetched current poses
-        double* q = Wk.pose[1 - st->cur] + 7 * lane;
-        if (fidx < 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (K >= 1)
 #pragma unroll
-            for (int i = 0; i < 7; ++i) q[i] = p7[i];
-        } else {
-            double qv[7];
-            se3_plus(p7, A + 6 * fidx, qv);
+        for (int j = K + 2; j < NP; ++j) a[j] = fma(-lp, uq[j], a[j]);
+    {
+        const double* uK = U + K * kGjLd;
 #pragma unroll
-            for (int i = 0; i < 7; ++i) q[i] = qv[i];
-        }
+        for (int j = K + 2; j < NP; ++j) uq[j] = uK[j];
     }
-    STAMP(5);
-    if (lane == 0) k5_result(st, 1, d2, gd);
-    STAMP(6);
+    a[NP] = fma(-l, ub, a[NP]);
+    if constexpr (K + 1 < NP) gj1_pivot<NP, K + 1>(a, uq, U, lane, bad, inv_next, l);
+}
+
+// wave 0 of the K5 block; U: NP x kGjLd doubles of LDS.  Returns x_lane (0 past n); bad if a
+// pivot is not > 0.
+template <int NF>
+__device__ double camera_solve_gj1(const double* sys, double* U, int lane, bool& bad) {
+    constexpr int NP = 6 * NF;
+    double a[NP + 1];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        a[j] = lane < NP ? (j <= lane ? *sys_lower<NF>(sys, lane, j) : *sys_lower<NF>(sys, j, lane)) : 0.0;
+    a[NP] = lane < NP ? *sys_lower<NF>(sys, NP, lane) : 0.0;
+    double uq[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) uq[j] = 0.0;
+    const double piv0 = rl64(a[0], 0);
+    bad = !(piv0 > 0.0) || !isfinite(piv0);
+    gj1_pivot<NP, 0>(a, uq, U, lane, bad, rcp_f64(piv0), 0.0);
+    __builtin_amdgcn_wave_barrier();
+    return lane < NP ? a[NP] / U[lane * kGjLd + lane] : 0.0;
 }
 
 template <int NF>
@@ -1082,7 +1149,8 @@ constexpr size_t k5_sys_doubles() { return (size_t)(NF * (NF + 1) / 2) * 36 + 12
 // (+ lambda on the diagonal); sharded: it is the all-reduced sys.  Every write of its results
 // (dc, trial poses, the state's solve_ok/dc2/gcdc/pending) is made by wave 0.
 template <int NF>
-__device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* Ls, int combine) {
+__device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, double* A, double* Ls, int combine,
+                        int variant) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
     __shared__ int badw[4];
     __shared__ int progress;
@@ -1122,16 +1190,29 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
         return;
     }
     STAMP(2);
-    camera_solve_w4<NF>(G, Pr, Wk, sys, A, badw, &progress, n, tid, p7, fidx);
+    if (variant == 0) {
+        camera_solve_w4<NF>(G, Pr, Wk, sys, A, badw, &progress, n, tid, p7, fidx);
+        return;
+    }
+    if (wave != 0) return;
+    const double gcl_v = lane < n ? sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
+    bool bad = false;
+    const double x = camera_solve_gj1<NF>(sys, A + 128, lane, bad);
+    STAMP(7);
+    if (bad) {
+        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
+        return;
+    }
+    k5_finish<NF>(G, Wk, A, x, gcl_v, n, lane, p7, fidx);
 }
 
 template <int NF>
-__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk, int combine) {
+__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk, int combine, int variant) {
     // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
     __shared__ __attribute__((aligned(16))) double A[k5_lds_doubles<NF>()];
     __shared__ double Ls[k5_sys_doubles<NF>()];
     RTSTAMP(4);
-    k5_body<NF>(G, Pr, Wk, A, Ls, combine);
+    k5_body<NF>(G, Pr, Wk, A, Ls, combine, variant);
     RTSTAMP(5);
 }
 
@@ -1693,6 +1774,7 @@ struct BundleAdjuster {
     int g_k = -1;
     rsvio_lm_cfg g_cfg{};
     bool graphs_ok = true;
+    int k5_variant = 0;  // camera solve for n_free <= 10: 0 pipelined 4-wave LDL^T, 1 one-wave Gauss-Jordan
     void drop_graph() {
         if (gexec) (void)hipGraphExecDestroy(gexec);
         gexec = nullptr;
@@ -1771,6 +1853,9 @@ struct BundleAdjuster {
         h_state.alloc(1);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
+        const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
+        if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
+        if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
     }
     ~BundleAdjuster() {
         drop_graph();
@@ -2064,7 +2149,7 @@ struct BundleAdjuster {
         const dim3 g(1), b(256);
         switch (G.n_free <= 10 ? G.n_free : 0) {
 #define RSVIO_CAM(NF) \
-    case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk, combine); break;
+    case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk, combine, k5_variant); break;
             RSVIO_CAM(1) RSVIO_CAM(2) RSVIO_CAM(3) RSVIO_CAM(4) RSVIO_CAM(5)
             RSVIO_CAM(6) RSVIO_CAM(7) RSVIO_CAM(8) RSVIO_CAM(9) RSVIO_CAM(10)
 #undef RSVIO_CAM
