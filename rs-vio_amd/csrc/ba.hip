@@ -75,6 +75,7 @@ constexpr int kPartD = 4;               // trial cost, |dp|^2, g_p.dp, |p|^2 per
 // waves per SIMD then share the FP64 pipe -- although K5's combine moved half the bytes.)
 constexpr int kGrp = 8;
 constexpr int kSchurThreads = 256;      // K4c workgroup: one pair per thread per pass
+constexpr int kK5Threads = 256;         // K5 (n_free <= 10): 4 waves (8 pulling the partials measured no faster)
 
 struct Mat4 {
     double m[16];
@@ -1171,8 +1172,8 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
     }
     STAMP(0);
     const double* sys = Wk.sys;
-    if (combine) {
-        combine_system<256>(G, Pr, Wk, Ls, st->lambda, true);
+    if (combine) {  // all kK5Threads threads pull the partial systems (more loads in flight)
+        combine_system<kK5Threads>(G, Pr, Wk, Ls, st->lambda, true);
         sys = Ls;
     }
     __syncthreads();
@@ -1185,29 +1186,34 @@ __device__ void k5_body(const Geometry& G, const Prob& Pr, const Work& Wk, doubl
     }
     __syncthreads();
     STAMP(1);
+    if (wave >= 4) return;  // the solve is the first 4 waves' (exited waves leave the barriers)
     if (fail) {
         if (tid == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
     STAMP(2);
-    if (variant == 0) {
+    // the one-wave variant is instantiated up to 9 free keyframes (config 3): at 10 its full
+    // rows no longer fit the register file
+    if (NF > 9 || variant == 0) {
         camera_solve_w4<NF>(G, Pr, Wk, sys, A, badw, &progress, n, tid, p7, fidx);
         return;
     }
-    if (wave != 0) return;
-    const double gcl_v = lane < n ? sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
-    bool bad = false;
-    const double x = camera_solve_gj1<NF>(sys, A + 128, lane, bad);
-    STAMP(7);
-    if (bad) {
-        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
-        return;
+    if constexpr (NF <= 9) {
+        if (wave != 0) return;
+        const double gcl_v = lane < n ? sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + lane] : 0.0;  // g_c
+        bool bad = false;
+        const double x = camera_solve_gj1<NF>(sys, A + 128, lane, bad);
+        STAMP(7);
+        if (bad) {
+            if (lane == 0) k5_result(st, 0, 0.0, 0.0);
+            return;
+        }
+        k5_finish<NF>(G, Wk, A, x, gcl_v, n, lane, p7, fidx);
     }
-    k5_finish<NF>(G, Wk, A, x, gcl_v, n, lane, p7, fidx);
 }
 
 template <int NF>
-__global__ __launch_bounds__(256) void ba_camera_solve(Geometry G, Prob Pr, Work Wk, int combine, int variant) {
+__global__ __launch_bounds__(kK5Threads) void ba_camera_solve(Geometry G, Prob Pr, Work Wk, int combine, int variant) {
     // A[0..128): dc for the pose updates; then the L and D L columns of chol_pipe
     __shared__ __attribute__((aligned(16))) double A[k5_lds_doubles<NF>()];
     __shared__ double Ls[k5_sys_doubles<NF>()];
@@ -2146,7 +2152,7 @@ struct BundleAdjuster {
     // register-resident factorisation for n_free <= 10, two rows per lane otherwise; combine:
     // the reduced system is summed from the chunk partials in K5's prologue (single rank)
     void launch_camera_solve(const Prob& pr, const Work& wk, int combine) {
-        const dim3 g(1), b(256);
+        const dim3 g(1), b(kK5Threads);
         switch (G.n_free <= 10 ? G.n_free : 0) {
 #define RSVIO_CAM(NF) \
     case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk, combine, k5_variant); break;
