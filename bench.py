@@ -928,8 +928,10 @@ def main():
                     help="config-4 Estimator row: rendered frames (0: skip)")
     ap.add_argument("--batch-streams", type=int, default=64,
                     help="batched tracker row: independent stereo streams per launch (0: skip)")
-    ap.add_argument("--cu-split", type=float, default=0.5,
-                    help="fraction of CUs given to the tracker stream (0: no CU partition)")
+    ap.add_argument("--cu-split", type=float, default=0.25,
+                    help="fraction of CUs given to the tracker stream (0: no CU partition); 0.25 measured "
+                         "best (round 2 sweep: K4c's 360 two-wave-per-SIMD workgroups fit the BA's 192 CUs "
+                         "in one round)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "p2p"],
                     help="BA exchange for N>1: P2P one-shot all-reduce (auto: if every rank attaches) or RCCL")

@@ -308,11 +308,21 @@ __device__ void make_templates(const uint8_t* pyr, uint32_t w, uint32_t h, float
     if constexpr (L > 4) make_templates_part<L, 4, L - 4>(pyr, w, h, posx, posy, lane, T, ok, sh);
 }
 
-// track_point_at_level (feature_tracker.rs:344-395) with Pattern52::residual (patch.rs:163-232)
+// track_point_at_level (feature_tracker.rs:344-395) with Pattern52::residual (patch.rs:163-232).
+// One iteration is a chain of dependent latencies (gather -> 52-add sum -> residual -> three
+// 52-add increment chains -> exp/update), so it is written without branches until its end:
+// out-of-bound lanes sample a safe pixel and discard it (no exec-masked region around the
+// loads), the residual and increment are formed even when a check has already failed, and the
+// norm, SE(2) exp, product and in-bound test of the trial run side by side.  The checks are then
+// taken in the reference's order -- sum, residual count, finite increment, norm > 1e6 (all
+// "return false"), convergence ("break" before the update), in-bound after it -- so every outcome
+// and every kept value is the one the sequential code produces.
 __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx, float paty, int lane,
                                Aff& A, int max_iter, float thresh, float* sh) {
     const bool act = lane < NP;
     const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
+    const bool tval = T.data >= 0.0f;
+    const float mh0 = -T.h0, mh1 = -T.h1, mh2 = -T.h2;
     for (int it = 0; it < max_iter; ++it) {
 #ifdef RSVIO_STAMPS
         if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] += 1;
@@ -325,16 +335,17 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
         x = x + A.m02;
         y = y + A.m12;
         const bool inb = act && x >= 2.0f && y >= 2.0f && x < wlim && y < hlim;
-        float v = -1.0f;
-        if (inb) {
-            uint32_t ix = (uint32_t)floorf(x), iy = (uint32_t)floorf(y);
-            float dx = x - (float)ix, dy = y - (float)iy;
-            float ddx = 1.0f - dx, ddy = 1.0f - dy;
-            const uint8_t* r0 = im.p + (size_t)iy * im.w + ix;
-            const uint8_t* r1 = r0 + im.w;
-            float p00 = (float)r0[0], p10 = (float)r0[1], p01 = (float)r1[0], p11 = (float)r1[1];
-            v = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
-        }
+        const float sx = inb ? x : 2.0f, sy = inb ? y : 2.0f;
+        const uint32_t ix = (uint32_t)floorf(sx), iy = (uint32_t)floorf(sy);
+        const float dx = sx - (float)ix, dy = sy - (float)iy;
+        const float ddx = 1.0f - dx, ddy = 1.0f - dy;
+        const uint8_t* r0 = im.p + (size_t)iy * im.w + ix;
+        const uint8_t* r1 = r0 + im.w;
+        const float p00 = (float)r0[0], p10 = (float)r0[1], p01 = (float)r1[0], p11 = (float)r1[1];
+        const float v = ddx * ddy * p00 + ddx * dy * p01 + dx * ddy * p10 + dx * dy * p11;
+        const int nv = __popcll(__ballot(inb));
+        const bool use = inb && v >= 0.0f && tval;
+        const int nres = __popcll(__ballot(use));
         LK_CLK(t1);
         LK_ACC(16, t0, t1);
         float sum;
@@ -344,30 +355,29 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
             lane_chains<1, true>(x1, s1, sh, lane);
             sum = s1[0];
         }
-        const int nv = __popcll(__ballot(inb));
-        if (sum < __FLT_EPSILON__) return false;
-        const bool use = inb && v >= 0.0f && T.data >= 0.0f;
         const float r = use ? ((float)nv * v / sum - T.data) : 0.0f;
-        const int nres = __popcll(__ballot(use));
-        if (!(nres > NP / 2)) return false;
         float inc[3];
         LK_CLK(t2);
         LK_ACC(17, t1, t2);
         {
-            const float x3[3] = {(-T.h0) * r, (-T.h1) * r, (-T.h2) * r};
+            const float x3[3] = {mh0 * r, mh1 * r, mh2 * r};
             lane_chains<3, false>(x3, inc, sh, lane);
         }
         LK_CLK(t3);
         LK_ACC(18, t2, t3);
         const float i0 = inc[0], i1 = inc[1], i2 = inc[2];
-        if (!(isfinite(i0) && isfinite(i1) && isfinite(i2))) return false;
+        const bool fin = isfinite(i0) && isfinite(i1) && isfinite(i2);
         const float nrm = sqrtf(i0 * i0 + i1 * i1 + i2 * i2);
-        if (nrm > 1e6f) return false;
-        if (nrm < thresh) break;
-        A = mul3(A, se2_exp(i0, i1, i2));
-        const bool inb2 = inbound(im, A.m02, A.m12, 2);
+#ifdef RSVIO_STAMPS
+        if (lane == 0 && blockIdx.x < 4096 && !(fabsf(i2) < 0.0625f)) g_dbg[blockIdx.x * 32 + 21] += 1;
+#endif
+        const Aff An = mul3(A, se2_exp(i0, i1, i2));
+        const bool inb2 = inbound(im, An.m02, An.m12, 2);
         LK_CLK(t4);
         LK_ACC(19, t3, t4);
+        if (sum < __FLT_EPSILON__ || !(nres > NP / 2) || !fin || nrm > 1e6f) return false;
+        if (nrm < thresh) break;
+        A = An;
         if (!inb2) return false;
     }
     return true;
@@ -471,7 +481,7 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch P) {
     Aff fwd, bwd;
 #ifdef RSVIO_STAMPS
     if (lane == 0 && blockIdx.x < 4096)
-        for (int k = 15; k <= 20; ++k) g_dbg[blockIdx.x * 32 + k] = 0;
+        for (int k = 15; k <= 21; ++k) g_dbg[blockIdx.x * 32 + k] = 0;
 #endif
     STAMP(0);
     bool ok = track_one<L>(pyr0, pyr1, P.w, P.h, T0, lane, patx, paty, P.max_iter, P.thresh, fwd, sh, tsh);

@@ -130,6 +130,77 @@ __global__ void chains(double x0, double* out, long long* cyc) {
     out[lane] = acc;
 }
 
+
+// f32 operations on LK's per-iteration chain (lk_track.hip), compiled with the library's flags
+__global__ void chains32(float x0, const unsigned char* img, float* out, long long* cyc) {
+    const int lane = threadIdx.x;
+    float x = x0 + lane * 1e-3f;
+    long long t0, t1;
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN; ++i) x = x + 1.0001f;
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[0] = t1 - t0;
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN / 4; ++i) x = 3.0f / x;
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[1] = (t1 - t0) * 4;
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN / 4; ++i) x = sqrtf(x + 2.0f);
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[2] = (t1 - t0) * 4;
+    __shared__ float sh[64 * 4];
+    t0 = clock64();
+#pragma unroll 1
+    for (int i = 0; i < kN / 8; ++i) {
+        sh[lane] = x;
+        __builtin_amdgcn_wave_barrier();
+        const float4 q = reinterpret_cast<const float4*>(sh)[(lane + 1) & 15];
+        __builtin_amdgcn_wave_barrier();
+        x = q.x + 1.0f;
+    }
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[3] = (t1 - t0) * 8;
+    // dependent u8 gather chain in a 64 KB image (L2/L1 resident after the first pass)
+    unsigned idx = lane * 977u;
+    for (int i = 0; i < 64; ++i) idx = (idx * 131u + img[idx & 65535u]) & 65535u;
+    t0 = clock64();
+#pragma unroll 1
+    for (int i = 0; i < kN / 8; ++i) idx = (idx * 131u + img[idx & 65535u]) & 65535u;
+    t1 = clock64();
+    cyc[4] = (t1 - t0) * 8;
+    // dependent readlane -> v_add_f32 (SGPR operand)
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN; ++i) x = x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), i & 63));
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[5] = t1 - t0;
+    // dependent f32 add with the other operand from a readlane issued ahead (independent)
+    float yv = x * 0.5f;
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN; ++i) x = x + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), i & 63));
+    __asm__ volatile("" ::"v"(x));
+    t1 = clock64();
+    cyc[6] = t1 - t0;
+    // dependent f64 add
+    double d = x;
+    t0 = clock64();
+#pragma unroll
+    for (int i = 0; i < kN; ++i) d = d + 1.0000001;
+    __asm__ volatile("" ::"v"(d));
+    t1 = clock64();
+    cyc[7] = t1 - t0;
+    out[lane] = x + (float)idx + (float)d;
+}
+
 int main() {
     double* out;
     long long* cyc;
@@ -155,5 +226,18 @@ int main() {
     const char* names[7] = {"fma_f64 dep", "rcp_f64 dep", "readlane2+add_f64 dep", "mul_f64 dep", "fma_f32 dep",
                             "fma_f64 indep (issue)", "ds_write->ds_read dep"};
     for (int i = 0; i < 7; ++i) printf("%-24s %6.1f cycles/op\n", names[i], (double)h[i] / kN);
+    unsigned char* img;
+    hipMalloc(&img, 65536);
+    hipMemset(img, 7, 65536);
+    float* o32;
+    hipMalloc(&o32, 64 * sizeof(float));
+    for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(chains32, dim3(1), dim3(64), 0, 0, 1.5f, img, o32, cyc);
+        hipMemcpy(h, cyc, sizeof h, hipMemcpyDeviceToHost);
+    }
+    const char* n32[8] = {"add_f32 dep", "div_f32 (IEEE) dep", "sqrt_f32 (IEEE) dep", "ds_write->ds_read_b128 dep",
+                          "u8 global gather dep (L1/L2)", "readlane->add_f32 dep", "add_f32 dep, readlane operand",
+                          "add_f64 dep"};
+    for (int i = 0; i < 8; ++i) printf("%-30s %6.1f cycles/op\n", n32[i], (double)h[i] / kN);
     return 0;
 }

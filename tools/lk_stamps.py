@@ -66,3 +66,8 @@ nit = max(it.sum(), 1)
 print("per-iteration phase cycles (mean over all iterations): gather+bilinear %.0f, sum chain + residual %.0f, "
       "increment chains %.0f, exp/update/inbound %.0f" % tuple(ph / nit))
 print("template cycles (mean per template): %.0f" % (st[:, 20].sum() / max(1, (st[:, 20] > 0).sum() * 2 * L)))
+print("slowest feature's per-iteration phase cycles: gather %.0f, sum %.0f, increment %.0f, exp/update %.0f" %
+      tuple(st[k, 16:20] / max(1, it[k])))
+big = (st[:, 21] > 0).sum()
+print("features with an |theta| >= 1/16 increment (OCML sin/cos path): %d; such iterations in total %d; "
+      "slowest feature %d" % (big, st[:, 21].sum(), st[k, 21]))
