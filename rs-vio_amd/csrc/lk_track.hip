@@ -468,6 +468,10 @@ __global__ __launch_bounds__(64) void lk_track_kernel(TrackLaunch P) {
         idx = job - P.start[b];
         if (P.dcount[b] != nullptr && idx >= *P.dcount[b]) return;
         pyr0 = P.pyr0[b]; pyr1 = P.pyr1[b]; ain = P.ain[b]; aout = P.aout[b]; valid = P.valid[b];
+        if (P.mask[b] != nullptr && P.mask[b][idx].w == 0) {  // an empty job (a cell without a corner)
+            if (threadIdx.x == 0) valid[idx] = 0;
+            return;
+        }
     }
     __shared__ __attribute__((aligned(16))) float sh[6 * (L < 4 ? L : 4) * kChainLd];
     __shared__ float tsh[4 * L * 64];

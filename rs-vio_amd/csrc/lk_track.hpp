@@ -21,6 +21,7 @@ struct TrackLaunch {
     float* aout[kMaxTrackBatches];
     uint8_t* valid[kMaxTrackBatches];
     const int* dcount[kMaxTrackBatches];       // optional device-side count (early exit)
+    const int4* mask[kMaxTrackBatches];        // optional: job i runs only when mask[i].w != 0 (else valid = 0)
     // batched serving mode (rsvio_track_points_table_d): when set, batch descriptors and the
     // prefix of their sizes come from device memory and nb may exceed kMaxTrackBatches
     const rsvio_track_batch* table;

@@ -6,12 +6,16 @@
 //
 // Per stereo frame, all on one HIP stream, nothing leaves HBM except the final feature list:
 //   K1 pyramid (both images, all levels, one launch)            pyramid.hip
-//   K2 temporal track cam0 + cam1 (one launch)                   lk_track.hip
-//   Kc compact surviving tracks + bin cam0 tracks into the grid  (1 workgroup)
-//   K3 FAST-9 threshold ladder, one workgroup per empty cell     (integer, exact)
-//   Kg gather new corners in the reference's cell scan order     (1 workgroup)
-//   K2 stereo track of the new corners cam0 -> cam1              lk_track.hip
-//   Ka append survivors with consecutive ids, pack the output    (1 workgroup)
+//   K3 FAST-9 threshold ladder, one workgroup per grid cell, EVERY cell (integer, exact)
+//   K2 ONE launch: temporal track cam0 + cam1, and the stereo track cam0 -> cam1 of every
+//      cell's corner (one job per cell, cells without a corner masked)   lk_track.hip
+//   Ka compact the survivors, bin them, append the corners of the cells holding no surviving
+//      cam0 track in cell scan order with consecutive ids, pack (+ unprojection) (1 workgroup)
+// The reference detects only in the cells its surviving tracks leave empty and then tracks those
+// corners; a cell's corner and its stereo track depend on nothing but the cell and the images,
+// so detecting and tracking every cell up front and dropping the occupied ones afterwards gives
+// the same points and tracks -- and lets the stereo jobs join the temporal launch (one LK
+// latency per frame instead of two).
 // Canonical order: track maps are kept sorted by id; new ids are assigned in detection scan
 // order (the reference's HashMap iteration order is random, feature_tracker.rs:162-170).
 #include <cmath>
@@ -60,73 +64,33 @@ __device__ __forceinline__ uint32_t sat_u32(float v) {
     return (uint32_t)v;
 }
 
-// Block-wide exclusive scan of one int per thread (blockDim.x <= 1024).
+// Block-wide exclusive scan of one int per thread (blockDim.x a multiple of 64, <= 1024): an
+// inclusive scan within each wave (6 shuffle steps, no barrier), the wave totals scanned by
+// wave 0 through LDS -- two barriers instead of two per doubling step.
 __device__ int block_exclusive_scan(int v, int* sh, int* total) {
-    const int tid = threadIdx.x;
-    sh[tid] = v;
-    __syncthreads();
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-        int t = tid >= off ? sh[tid - off] : 0;
-        __syncthreads();
-        sh[tid] += t;
-        __syncthreads();
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
     }
-    int incl = sh[tid];
-    *total = sh[blockDim.x - 1];
+    if (lane == 63) sh[wave] = incl;
     __syncthreads();
-    return incl - v;
-}
-
-// Stable compaction of track map c (keep valid), then bin cam0 positions into grid counters
-// (image_utilities.rs:128-139 with feature_tracker.rs:228-237's rounding).
-__global__ __launch_bounds__(1024) void compact_bin_kernel(
-    int n0, int n1, const float* __restrict__ aff_t0, const float* __restrict__ aff_t1,
-    const uint8_t* __restrict__ v0, const uint8_t* __restrict__ v1, float* __restrict__ map_aff0,
-    float* __restrict__ map_aff1, uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
-    uint64_t* __restrict__ ids_tmp, int* __restrict__ counts, int* __restrict__ bins, GridGeom G,
-    int tracked) {
-    __shared__ int sh[1024];
-    const int tid = threadIdx.x;
-    for (int c = 0; c < 2; ++c) {
-        const int n = c == 0 ? n0 : n1;
-        const float* at = c == 0 ? aff_t0 : aff_t1;
-        const uint8_t* vv = c == 0 ? v0 : v1;
-        float* ma = c == 0 ? map_aff0 : map_aff1;
-        uint64_t* ids = c == 0 ? ids0 : ids1;
-        if (!tracked) {
-            if (tid == 0) counts[c] = n;
-            continue;
+    if (wave == 0) {
+        int w = lane < nw ? sh[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const int t = __shfl_up(w, off, 64);
+            if (lane >= off) w += t;
         }
-        const int per = (n + blockDim.x - 1) / blockDim.x;
-        const int b = tid * per, e = min(n, b + per);
-        int local = 0;
-        for (int i = b; i < e; ++i) local += vv[i] ? 1 : 0;
-        int total;
-        int pos = block_exclusive_scan(local, sh, &total);
-        // ids: copy through a temporary so that in-place compaction is race free
-        for (int i = b; i < e; ++i) ids_tmp[i] = ids[i];
-        __syncthreads();
-        for (int i = b; i < e; ++i) {
-            if (!vv[i]) continue;
-            for (int k = 0; k < 6; ++k) ma[6 * pos + k] = at[6 * i + k];
-            ids[pos] = ids_tmp[i];
-            ++pos;
-        }
-        if (tid == 0) counts[c] = total;
-        __syncthreads();
+        if (lane < nw) sh[16 + lane] = w;  // inclusive prefix of wave totals
     }
     __syncthreads();
-    for (int i = tid; i < G.bin_rows * G.bin_cols; i += blockDim.x) bins[i] = 0;
-    __syncthreads();
-    const int n = counts[0];
-    for (int i = tid; i < n; i += blockDim.x) {
-        uint32_t x = sat_u32(roundf(map_aff0[6 * i + 4]));
-        uint32_t y = sat_u32(roundf(map_aff0[6 * i + 5]));
-        if (x >= (uint32_t)G.xs && y >= (uint32_t)G.ys && x < (uint32_t)(G.xe + G.g) && y < (uint32_t)(G.ye + G.g)) {
-            uint32_t cx = (x - G.xs) / G.g, cy = (y - G.ys) / G.g;
-            atomicAdd(&bins[cy * G.bin_cols + cx], 1);
-        }
-    }
+    *total = sh[16 + nw - 1];
+    const int base = wave > 0 ? sh[16 + wave - 1] : 0;
+    __syncthreads();  // sh is reused by the next scan
+    return base + incl - v;
 }
 
 // FAST-9 score of a candidate (largest t with a contiguous 9-arc all brighter than c + t or all
@@ -157,16 +121,30 @@ __device__ __forceinline__ int fast9_score(const uint8_t* crop, int g, int x, in
 
 // detect_key_points per cell (image_utilities.rs:141-172): skip occupied cells; otherwise
 // thresholds 40, 35, ..., 10 on the cell's grid x grid crop; keep the lowest-score corner
-// (ties: crop scan order) that lies in [19, w-19] x [19, h-19].
+// (ties: crop scan order) that lies in [19, w-19] x [19, h-19].  Occupancy: the cell holds one
+// of the n_pts existing points (pts_valid[i] != 0, or all when null) binned by
+// image_utilities.rs:128-139 with feature_tracker.rs:228-237's rounding -- every workgroup
+// tests the points itself, so no grid-wide binning pass precedes it.  new_aff (optional): the
+// identity Affine2 at the cell's corner (feature_tracker.rs:143-152), indexed by cell.
 __global__ __launch_bounds__(256) void fast_cells_kernel(const uint8_t* __restrict__ img, GridGeom G,
-                                                         const int* __restrict__ bins,
-                                                         int4* __restrict__ cell_pt) {
+                                                         const float* __restrict__ pts_aff,
+                                                         const uint8_t* __restrict__ pts_valid, int n_pts,
+                                                         int4* __restrict__ cell_pt, float* __restrict__ new_aff) {
     extern __shared__ uint8_t crop[];
     __shared__ int s_max, s_key;
     const int s = blockIdx.x;            // scan order: x outer, y inner
     const int cx = s / G.cells_y, cy = s % G.cells_y;
     const int x0 = G.xs + cx * G.g, y0 = G.ys + cy * G.g;
-    if (bins[cy * G.bin_cols + cx] > 0) {
+    int occ = 0;
+    for (int i = threadIdx.x; i < n_pts; i += blockDim.x) {
+        if (pts_valid != nullptr && !pts_valid[i]) continue;
+        const uint32_t x = sat_u32(roundf(pts_aff[6 * i + 4]));
+        const uint32_t y = sat_u32(roundf(pts_aff[6 * i + 5]));
+        if (x >= (uint32_t)G.xs && y >= (uint32_t)G.ys && x < (uint32_t)(G.xe + G.g) && y < (uint32_t)(G.ye + G.g) &&
+            (int)((x - G.xs) / G.g) == cx && (int)((y - G.ys) / G.g) == cy)
+            occ = 1;
+    }
+    if (__syncthreads_or(occ)) {
         if (threadIdx.x == 0) cell_pt[s] = make_int4(0, 0, 0, 0);
         return;
     }
@@ -212,7 +190,14 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(const uint8_t* __restri
     if (threadIdx.x == 0) {
         const int key = s_key;
         const int idx = key & 0xFFFF;
-        cell_pt[s] = make_int4(x0 + idx % g, y0 + idx / g, key >> 16, 1);
+        const int px = x0 + idx % g, py = y0 + idx / g;
+        cell_pt[s] = make_int4(px, py, key >> 16, 1);
+        if (new_aff != nullptr) {
+            float* a = new_aff + 6 * s;
+            a[0] = 1.0f; a[1] = 0.0f; a[2] = 0.0f; a[3] = 1.0f;
+            a[4] = (float)px;
+            a[5] = (float)py;
+        }
     }
 }
 
@@ -245,23 +230,73 @@ struct CamPair {
     int on;
 };
 
-// feature_tracker.rs:162-170 in canonical order, then get_track_points packing.
+// The end of process_frame in one workgroup: (1) the surviving temporal tracks of each camera
+// compacted in order from the tracker's output (at, valid) into the track map (feature_tracker.rs
+// :131-141 -- failed tracks are dropped, the map keeps ascending ids); (2) the corners of the
+// cells holding no cam0 survivor whose stereo track succeeded (cell_pt[i].w && new_valid[i])
+// appended in cell scan order with consecutive ids (feature_tracker.rs:143-170, canonical order); (3) get_track_points packing, with the
+// Frame::add_{left,right}_feature unprojection fused (frame.rs:118-119,131-132).  tracked = 0
+// (first frame): the maps are taken as they are (counts = n0, n1).
 __global__ __launch_bounds__(1024) void append_pack_kernel(
-    const float* __restrict__ new_aff0, const float* __restrict__ new_aff1,
-    const uint8_t* __restrict__ new_valid, const int* __restrict__ new_count, float* __restrict__ map_aff0,
+    GridGeom G, int* __restrict__ bins, int n0, int n1, int tracked, const float* __restrict__ at0, const float* __restrict__ at1,
+    const uint8_t* __restrict__ tv0, const uint8_t* __restrict__ tv1, uint64_t* __restrict__ ids_tmp,
+    const int4* __restrict__ cell_pt, int n_cells, const float* __restrict__ new_aff0,
+    const float* __restrict__ new_aff1, const uint8_t* __restrict__ new_valid, float* __restrict__ map_aff0,
     float* __restrict__ map_aff1, uint64_t* __restrict__ ids0, uint64_t* __restrict__ ids1,
     int* __restrict__ counts, unsigned long long* __restrict__ last_id, int capacity,
     rsvio_feature* __restrict__ out0, rsvio_feature* __restrict__ out1, int* __restrict__ overflow,
     CamPair cams, float2* __restrict__ und0, float2* __restrict__ und1) {
     __shared__ int sh[1024];
-    const int m = *new_count;
-    const int per = (m + blockDim.x - 1) / blockDim.x;
-    const int b = threadIdx.x * per, e = min(m, b + per);
+    const int tid = threadIdx.x;
+    int cnt[2] = {n0, n1};
+    if (tracked) {
+        for (int c = 0; c < 2; ++c) {
+            const int n = c == 0 ? n0 : n1;
+            const float* at = c == 0 ? at0 : at1;
+            const uint8_t* vv = c == 0 ? tv0 : tv1;
+            float* ma = c == 0 ? map_aff0 : map_aff1;
+            uint64_t* ids = c == 0 ? ids0 : ids1;
+            uint64_t* it = ids_tmp + (size_t)c * capacity;
+            const int per = (n + blockDim.x - 1) / blockDim.x;
+            const int b = tid * per, e = min(n, b + per);
+            int local = 0;
+            for (int i = b; i < e; ++i) {
+                local += vv[i] ? 1 : 0;
+                it[i] = ids[i];  // ids are compacted in place: through a copy
+            }
+            int total;
+            int pos = block_exclusive_scan(local, sh, &total);  // its barriers order the copy
+            for (int i = b; i < e; ++i) {
+                if (!vv[i]) continue;
+                for (int k = 0; k < 6; ++k) ma[6 * pos + k] = at[6 * i + k];
+                ids[pos] = it[i];
+                ++pos;
+            }
+            cnt[c] = total;
+        }
+    }
+    // bin the cam0 survivors into the grid counters (image_utilities.rs:128-139 with
+    // feature_tracker.rs:228-237's rounding); a cell with a count keeps no new corner
+    for (int i = tid; i < G.bin_rows * G.bin_cols; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt[0]; i += blockDim.x) {
+        const uint32_t x = sat_u32(roundf(map_aff0[6 * i + 4]));
+        const uint32_t y = sat_u32(roundf(map_aff0[6 * i + 5]));
+        if (x >= (uint32_t)G.xs && y >= (uint32_t)G.ys && x < (uint32_t)(G.xe + G.g) && y < (uint32_t)(G.ye + G.g))
+            atomicAdd(&bins[((y - G.ys) / G.g) * G.bin_cols + (x - G.xs) / G.g], 1);
+    }
+    __syncthreads();
+    auto is_new = [&](int i) {  // cell i (scan order: x outer, y inner) contributes a new point
+        const int cx = i / G.cells_y, cy = i % G.cells_y;
+        return cell_pt[i].w != 0 && new_valid[i] != 0 && bins[cy * G.bin_cols + cx] == 0;
+    };
+    const int per = (n_cells + blockDim.x - 1) / blockDim.x;
+    const int b = tid * per, e = min(n_cells, b + per);
     int local = 0;
-    for (int i = b; i < e; ++i) local += new_valid[i] ? 1 : 0;
+    for (int i = b; i < e; ++i) local += is_new(i) ? 1 : 0;
     int total;
     int pos = block_exclusive_scan(local, sh, &total);
-    const int c0 = counts[0], c1 = counts[1];
+    const int c0 = cnt[0], c1 = cnt[1];
     const unsigned long long base = *last_id;
     // Both cameras append the same new points (feature_tracker.rs:162-170), so admit only as many as
     // the fuller camera has room for: no slot beyond what was written is ever counted, and ids stay
@@ -269,7 +304,7 @@ __global__ __launch_bounds__(1024) void append_pack_kernel(
     // fetch() as RSVIO_ERR_CAPACITY); the flag is rewritten every frame.
     const int admit = min(total, max(0, min(capacity - c0, capacity - c1)));
     for (int i = b; i < e; ++i) {
-        if (!new_valid[i]) continue;
+        if (!is_new(i)) continue;
         if (pos < admit) {
             const int d0 = c0 + pos, d1 = c1 + pos;
             for (int k = 0; k < 6; ++k) {
@@ -282,18 +317,17 @@ __global__ __launch_bounds__(1024) void append_pack_kernel(
         ++pos;
     }
     __syncthreads();
-    const int n0 = c0 + admit, n1 = c1 + admit;
-    if (threadIdx.x == 0) {
-        counts[0] = n0;
-        counts[1] = n1;
+    const int m0 = c0 + admit, m1 = c1 + admit;
+    if (tid == 0) {
+        counts[0] = m0;
+        counts[1] = m1;
         *last_id = base + (unsigned long long)admit;
         *overflow = total > admit ? 1 : 0;
     }
-    // get_track_points packing, both cameras spread over the block; with cameras attached the
-    // Frame::add_{left,right}_feature unprojection (frame.rs:118-119,131-132) is fused here
-    for (int j = threadIdx.x; j < n0 + n1; j += blockDim.x) {
-        const int c = j < n0 ? 0 : 1;
-        const int i = c == 0 ? j : j - n0;
+    // get_track_points packing, both cameras spread over the block
+    for (int j = tid; j < m0 + m1; j += blockDim.x) {
+        const int c = j < m0 ? 0 : 1;
+        const int i = c == 0 ? j : j - m0;
         const float* a = (c == 0 ? map_aff0 : map_aff1) + 6 * i;
         rsvio_feature f;
         f.id = (c == 0 ? ids0 : ids1)[i]; f.x = a[4]; f.y = a[5];
@@ -370,10 +404,10 @@ struct Tracker {
     bool has_prev = false;
     int host_count[2] = {0, 0};
     DevBuf<uint8_t> d_img, d_pyr;   // 2 images; 2 slots x 2 cams pyramids
-    DevBuf<float> map_aff, tmp_aff, new_aff, new_aff1, new_score;
+    DevBuf<float> map_aff, tmp_aff, new_aff, new_aff1;
     DevBuf<uint64_t> ids, ids_tmp, rm_ids;
     DevBuf<uint8_t> valid, new_valid;
-    DevBuf<int> counts, bins, new_count, overflow;
+    DevBuf<int> counts, bins, overflow;
     DevBuf<int4> cell_pt;
     DevBuf<unsigned long long> last_id;
     DevBuf<rsvio_feature> out;
@@ -410,11 +444,9 @@ struct Tracker {
         valid.alloc((size_t)2 * cap);
         new_aff.alloc((size_t)n_cells * 6);
         new_aff1.alloc((size_t)n_cells * 6);
-        new_score.alloc(n_cells);
         new_valid.alloc(n_cells);
         counts.alloc(2);
         bins.alloc((size_t)G.bin_rows * G.bin_cols);
-        new_count.alloc(1);
         overflow.alloc(1);
         cell_pt.alloc(n_cells);
         last_id.alloc(1);
@@ -441,44 +473,36 @@ struct Tracker {
         io.src[0] = d_left; io.dst[0] = pyr(nxt, 0);
         io.src[1] = d_right; io.dst[1] = pyr(nxt, 1);
         plan.enqueue(io, 2, stream);
-        if (has_prev) {
-            TrackLaunch L{};
-            L.w = P.width; L.h = P.height; L.levels = P.levels; L.max_iter = P.max_iterations;
-            L.thresh = P.convergence_threshold;
-            L.nb = 2;
-            L.start[0] = 0; L.start[1] = host_count[0]; L.start[2] = host_count[0] + host_count[1];
-            for (int c = 0; c < 2; ++c) {
-                L.pyr0[c] = pyr(cur, c); L.pyr1[c] = pyr(nxt, c);
-                L.ain[c] = maff(c); L.aout[c] = taff(c); L.valid[c] = valid.p + (size_t)c * cap;
-                L.dcount[c] = nullptr;
-            }
-            enqueue_track(L, stream);
-        }
-        hipLaunchKernelGGL(compact_bin_kernel, dim3(1), dim3(1024), 0, stream, host_count[0], host_count[1],
-                           taff(0), taff(1), valid.p, valid.p + cap, maff(0), maff(1), mid(0), mid(1),
-                           ids_tmp.p, counts.p, bins.p, G, has_prev ? 1 : 0);
-        RSVIO_HIP(hipGetLastError());
+        // FAST-9 in every cell, its corner as a cell-indexed identity affine
         const uint8_t* cur0 = pyr(nxt, 0);  // level 0 == the left image
         hipLaunchKernelGGL(fast_cells_kernel, dim3(n_cells), dim3(256), (size_t)P.grid_size * P.grid_size, stream,
-                           cur0, G, bins.p, cell_pt.p);
+                           cur0, G, nullptr, nullptr, 0, cell_pt.p, new_aff.p);
         RSVIO_HIP(hipGetLastError());
-        hipLaunchKernelGGL(gather_new_kernel, dim3(1), dim3(1024), 0, stream, cell_pt.p, n_cells, new_aff.p,
-                           new_count.p, new_score.p);
-        RSVIO_HIP(hipGetLastError());
-        {
+        {  // one LK launch: [cam0 temporal, cam1 temporal,] stereo of every cell's corner
             TrackLaunch L{};
             L.w = P.width; L.h = P.height; L.levels = P.levels; L.max_iter = P.max_iterations;
             L.thresh = P.convergence_threshold;
-            L.nb = 1;
-            L.start[0] = 0; L.start[1] = n_cells;
-            L.pyr0[0] = pyr(nxt, 0); L.pyr1[0] = pyr(nxt, 1);
-            L.ain[0] = new_aff.p; L.aout[0] = new_aff1.p; L.valid[0] = new_valid.p;
-            L.dcount[0] = new_count.p;
+            int b = 0;
+            L.start[0] = 0;
+            if (has_prev) {
+                for (int c = 0; c < 2; ++c, ++b) {
+                    L.pyr0[b] = pyr(cur, c); L.pyr1[b] = pyr(nxt, c);
+                    L.ain[b] = maff(c); L.aout[b] = taff(c); L.valid[b] = valid.p + (size_t)c * cap;
+                    L.start[b + 1] = L.start[b] + host_count[c];
+                }
+            }
+            L.pyr0[b] = pyr(nxt, 0); L.pyr1[b] = pyr(nxt, 1);
+            L.ain[b] = new_aff.p; L.aout[b] = new_aff1.p; L.valid[b] = new_valid.p;
+            L.mask[b] = cell_pt.p;  // cells without a corner exit at once
+            L.start[b + 1] = L.start[b] + n_cells;
+            L.nb = b + 1;
             enqueue_track(L, stream);
         }
-        hipLaunchKernelGGL(append_pack_kernel, dim3(1), dim3(1024), 0, stream, new_aff.p, new_aff1.p, new_valid.p,
-                           new_count.p, maff(0), maff(1), mid(0), mid(1), counts.p, last_id.p, cap, out.p,
-                           out.p + cap, overflow.p, cams, undist.p, undist.p + (cams.on ? cap : 0));
+        hipLaunchKernelGGL(append_pack_kernel, dim3(1), dim3(1024), 0, stream, G, bins.p, host_count[0],
+                           host_count[1], has_prev ? 1 : 0, taff(0), taff(1), valid.p, valid.p + cap, ids_tmp.p,
+                           cell_pt.p, n_cells, new_aff.p, new_aff1.p, new_valid.p, maff(0), maff(1), mid(0), mid(1),
+                           counts.p, last_id.p, cap, out.p, out.p + cap, overflow.p, cams, undist.p,
+                           undist.p + (cams.on ? cap : 0));
         RSVIO_HIP(hipGetLastError());
         cur = nxt;
         has_prev = true;
@@ -842,10 +866,9 @@ int rsvio_detect_keypoints(const uint8_t* img, int32_t w, int32_t h, int32_t gri
         rsvio::GridGeom G = rsvio::make_grid(w, h, grid);
         const int n_cells = G.cells_x * G.cells_y;
         const int ne = std::max(n_existing, 1);
-        rsvio::DevBuf<uint8_t> di((size_t)w * h), dv(ne);
+        rsvio::DevBuf<uint8_t> di((size_t)w * h);
         rsvio::DevBuf<float> ea((size_t)ne * 6), na((size_t)n_cells * 6), ns(n_cells);
-        rsvio::DevBuf<uint64_t> ids(ne), idt(ne);
-        rsvio::DevBuf<int> counts(2), bins((size_t)G.bin_rows * G.bin_cols), nc(1);
+        rsvio::DevBuf<int> nc(1);
         rsvio::DevBuf<int4> cp(n_cells);
         RSVIO_HIP(hipMemcpy(di.p, img, (size_t)w * h, hipMemcpyHostToDevice));
         std::vector<float> aff((size_t)ne * 6, 0.0f);
@@ -854,12 +877,8 @@ int rsvio_detect_keypoints(const uint8_t* img, int32_t w, int32_t h, int32_t gri
             aff[6 * i + 5] = existing_xy[2 * i + 1];
         }
         RSVIO_HIP(hipMemcpy(ea.p, aff.data(), sizeof(float) * aff.size(), hipMemcpyHostToDevice));
-        // counts[0] = n_existing, map already "compacted": run the kernel in not-tracked mode
-        hipLaunchKernelGGL(rsvio::compact_bin_kernel, dim3(1), dim3(1024), 0, nullptr, n_existing, 0, ea.p, ea.p,
-                           dv.p, dv.p, ea.p, ea.p, ids.p, ids.p, idt.p, counts.p, bins.p, G, 0);
-        RSVIO_HIP(hipGetLastError());
         hipLaunchKernelGGL(rsvio::fast_cells_kernel, dim3(n_cells), dim3(256), (size_t)grid * grid, nullptr, di.p, G,
-                           bins.p, cp.p);
+                           ea.p, nullptr, n_existing, cp.p, nullptr);
         RSVIO_HIP(hipGetLastError());
         hipLaunchKernelGGL(rsvio::gather_new_kernel, dim3(1), dim3(1024), 0, nullptr, cp.p, n_cells, na.p, nc.p, ns.p);
         RSVIO_HIP(hipGetLastError());

@@ -1,0 +1,16 @@
+"""GPU box: only bench.py's config-4 Estimator row (no CPU leg), printed as JSON.
+usage: python tools/pipeline_row.py [frames] [repeats]"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "rs-vio_amd")]
+
+import bench  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 500
+for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 1):
+    r = bench.measure_pipeline_row(0, cpu=False, n_frames=n)
+    print(json.dumps({k: r[k] for k in ("value", "ms_per_frame", "stage_ms_per_frame", "host_ms_per_frame",
+                                         "keyframes", "ba_solves", "max_position_error_m")}), flush=True)
