@@ -59,6 +59,17 @@ __global__ void make_taps_kernel(TapTable tab, int n_entries) {
 __global__ __launch_bounds__(256) void pyramid_kernel(PyrLaunch L, PyrIO io) {
     extern __shared__ uint32_t smem[];
     const int img = blockIdx.y;
+    {  // the FAST workgroups after the pyramid's (image 0 only)
+        const int fb = (int)blockIdx.x - (L.copy_blocks + L.tile_start[L.levels]);
+        if (fb >= 0) {
+            if (img == 0 && fb < io.fast_cells) {
+                const uint8_t* s0 = io.psrc ? io.psrc : io.src[0];
+                fast_cell(s0, io.fg, fb, nullptr, nullptr, 0, io.fast_pt, io.fast_aff,
+                          reinterpret_cast<uint8_t*>(smem));
+            }
+            return;
+        }
+    }
     const uint8_t* __restrict__ src = io.psrc ? io.psrc + (size_t)img * L.w * L.h : io.src[img];
     uint8_t* __restrict__ dst_base = io.psrc ? io.pdst + (size_t)img * L.pyr_bytes : io.dst[img];
     int b = blockIdx.x;
@@ -250,7 +261,9 @@ void PyramidPlan::init(int w_, int h_, int levels_) {
 void PyramidPlan::enqueue(const PyrIO& io, int n_img, hipStream_t s) const {
     if (n_img <= 0) return;
     if (n_img > (io.psrc ? 65535 : kMaxPyrIO)) throw std::invalid_argument("too many images per pyramid launch");
-    hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks, n_img), dim3(256), lds_bytes, s, launch, io);
+    const size_t lds = io.fast_cells > 0 ? std::max(lds_bytes, (size_t)io.fg.g * io.fg.g) : lds_bytes;
+    hipLaunchKernelGGL(pyramid_kernel, dim3(total_blocks + std::max(io.fast_cells, 0), n_img), dim3(256), lds, s,
+                       launch, io);
     RSVIO_HIP(hipGetLastError());
 }
 

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "fast.hpp"
 
 namespace rsvio {
 
@@ -44,6 +45,12 @@ struct PyrIO {
     // packed mode (any number of images): image i at psrc + i * w * h, pyramid i at pdst + i * pyr_bytes
     const uint8_t* psrc;
     uint8_t* pdst;
+    // optional: FAST-9 on every grid cell of image 0 (the tracker frame's detection, fast.hpp) as
+    // fast_cells extra workgroups of the same launch -- it reads only the source image
+    int fast_cells;
+    GridGeom fg;
+    int4* fast_pt;
+    float* fast_aff;
 };
 
 struct PyramidPlan {

@@ -6,7 +6,8 @@
 //
 // Per stereo frame, all on one HIP stream, nothing leaves HBM except the final feature list:
 //   K1 pyramid (both images, all levels, one launch)            pyramid.hip
-//   K3 FAST-9 threshold ladder, one workgroup per grid cell, EVERY cell (integer, exact)
+//   K3 FAST-9 threshold ladder, one workgroup per grid cell, EVERY cell (integer, exact), as
+//      extra workgroups of the K1 launch (it reads the left image itself)
 //   K2 ONE launch: temporal track cam0 + cam1, and the stereo track cam0 -> cam1 of every
 //      cell's corner (one job per cell, cells without a corner masked)   lk_track.hip
 //   Ka compact the survivors, bin them, append the corners of the cells holding no surviving
@@ -28,41 +29,13 @@
 #include "lk_track.hpp"
 #include "pyramid.hpp"
 #include "camera.hpp"
+#include "fast.hpp"
 
 namespace rsvio {
 
 namespace {
 
 thread_local std::string g_last_error;
-
-constexpr int kEdge = 19;  // EDGE_THRESHOLD, image_utilities.rs:114
-
-struct GridGeom {
-    int w, h, g;
-    int xs, ys, xe, ye;   // x_start, y_start, x_stop, y_stop (image_utilities.rs:121-125)
-    int bin_rows, bin_cols;  // (h / g + 1) x (w / g + 1) counters
-    int cells_x, cells_y;    // cells actually scanned
-};
-
-GridGeom make_grid(int w, int h, int g) {
-    GridGeom G;
-    G.w = w; G.h = h; G.g = g;
-    G.xs = (w % g) / 2;
-    G.xe = G.xs + g * (w / g - 1) + 1;
-    G.ys = (h % g) / 2;
-    G.ye = G.ys + g * (h / g - 1) + 1;
-    G.bin_rows = h / g + 1;
-    G.bin_cols = w / g + 1;
-    G.cells_x = (G.xe - G.xs + g - 1) / g;
-    G.cells_y = (G.ye - G.ys + g - 1) / g;
-    return G;
-}
-
-__device__ __forceinline__ uint32_t sat_u32(float v) {
-    if (!(v > 0.0f)) return 0u;
-    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)v;
-}
 
 // Block-wide exclusive scan of one int per thread (blockDim.x a multiple of 64, <= 1024): an
 // inclusive scan within each wave (6 shuffle steps, no barrier), the wave totals scanned by
@@ -93,112 +66,13 @@ __device__ int block_exclusive_scan(int v, int* sh, int* total) {
     return base + incl - v;
 }
 
-// FAST-9 score of a candidate (largest t with a contiguous 9-arc all brighter than c + t or all
-// darker than c - t); equals imageproc's binary-searched fast_corner_score whenever the pixel is
-// a corner at the starting threshold.
-__device__ __forceinline__ int fast9_score(const uint8_t* crop, int g, int x, int y) {
-    const int8_t ox[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int8_t oy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
-    const int c = crop[y * g + x];
-    int d[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) d[i] = (int)crop[(y + oy[i]) * g + x + ox[i]] - c;
-    int sb = -1000, sd = -1000;
-#pragma unroll
-    for (int a = 0; a < 16; ++a) {
-        int mb = 1000, md = 1000;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            int v = d[(a + k) & 15];
-            mb = min(mb, v);
-            md = min(md, -v);
-        }
-        sb = max(sb, mb);
-        sd = max(sd, md);
-    }
-    return max(sb, sd) - 1;
-}
-
-// detect_key_points per cell (image_utilities.rs:141-172): skip occupied cells; otherwise
-// thresholds 40, 35, ..., 10 on the cell's grid x grid crop; keep the lowest-score corner
-// (ties: crop scan order) that lies in [19, w-19] x [19, h-19].  Occupancy: the cell holds one
-// of the n_pts existing points (pts_valid[i] != 0, or all when null) binned by
-// image_utilities.rs:128-139 with feature_tracker.rs:228-237's rounding -- every workgroup
-// tests the points itself, so no grid-wide binning pass precedes it.  new_aff (optional): the
-// identity Affine2 at the cell's corner (feature_tracker.rs:143-152), indexed by cell.
+// detect_key_points per cell (fast.hpp): one 256-thread workgroup per cell, crop in dynamic LDS
 __global__ __launch_bounds__(256) void fast_cells_kernel(const uint8_t* __restrict__ img, GridGeom G,
                                                          const float* __restrict__ pts_aff,
                                                          const uint8_t* __restrict__ pts_valid, int n_pts,
                                                          int4* __restrict__ cell_pt, float* __restrict__ new_aff) {
     extern __shared__ uint8_t crop[];
-    __shared__ int s_max, s_key;
-    const int s = blockIdx.x;            // scan order: x outer, y inner
-    const int cx = s / G.cells_y, cy = s % G.cells_y;
-    const int x0 = G.xs + cx * G.g, y0 = G.ys + cy * G.g;
-    int occ = 0;
-    for (int i = threadIdx.x; i < n_pts; i += blockDim.x) {
-        if (pts_valid != nullptr && !pts_valid[i]) continue;
-        const uint32_t x = sat_u32(roundf(pts_aff[6 * i + 4]));
-        const uint32_t y = sat_u32(roundf(pts_aff[6 * i + 5]));
-        if (x >= (uint32_t)G.xs && y >= (uint32_t)G.ys && x < (uint32_t)(G.xe + G.g) && y < (uint32_t)(G.ye + G.g) &&
-            (int)((x - G.xs) / G.g) == cx && (int)((y - G.ys) / G.g) == cy)
-            occ = 1;
-    }
-    if (__syncthreads_or(occ)) {
-        if (threadIdx.x == 0) cell_pt[s] = make_int4(0, 0, 0, 0);
-        return;
-    }
-    const int g = G.g;
-    for (int i = threadIdx.x; i < g * g; i += blockDim.x) crop[i] = img[(size_t)(y0 + i / g) * G.w + x0 + i % g];
-    if (threadIdx.x == 0) {
-        s_max = -1;
-        s_key = 0x7FFFFFFF;
-    }
-    __syncthreads();
-    const int span = g - 6;  // crop-local candidates [3, g - 3)
-    int my_best = -1;
-    for (int i = threadIdx.x; i < span * span; i += blockDim.x) {
-        const int x = 3 + i % span, y = 3 + i / span;
-        const int X = x0 + x, Y = y0 + y;
-        if (X < kEdge || X > G.w - kEdge || Y < kEdge || Y > G.h - kEdge) continue;
-        int sc = fast9_score(crop, g, x, y);
-        if (sc >= 10) my_best = max(my_best, sc);
-    }
-    if (my_best >= 0) atomicMax(&s_max, my_best);
-    __syncthreads();
-    const int smax = s_max;
-    int tstar = -1;
-    for (int t = 40; t >= 10; t -= 5)
-        if (smax >= t) {
-            tstar = t;
-            break;
-        }
-    if (tstar < 0) {
-        if (threadIdx.x == 0) cell_pt[s] = make_int4(0, 0, 0, 0);
-        return;
-    }
-    int my_key = 0x7FFFFFFF;
-    for (int i = threadIdx.x; i < span * span; i += blockDim.x) {
-        const int x = 3 + i % span, y = 3 + i / span;
-        const int X = x0 + x, Y = y0 + y;
-        if (X < kEdge || X > G.w - kEdge || Y < kEdge || Y > G.h - kEdge) continue;
-        int sc = fast9_score(crop, g, x, y);
-        if (sc >= tstar) my_key = min(my_key, (sc << 16) | (y * g + x));
-    }
-    atomicMin(&s_key, my_key);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int key = s_key;
-        const int idx = key & 0xFFFF;
-        const int px = x0 + idx % g, py = y0 + idx / g;
-        cell_pt[s] = make_int4(px, py, key >> 16, 1);
-        if (new_aff != nullptr) {
-            float* a = new_aff + 6 * s;
-            a[0] = 1.0f; a[1] = 0.0f; a[2] = 0.0f; a[3] = 1.0f;
-            a[4] = (float)px;
-            a[5] = (float)py;
-        }
-    }
+    fast_cell(img, G, (int)blockIdx.x, pts_aff, pts_valid, n_pts, cell_pt, new_aff, crop);
 }
 
 // New corners in scan order -> identity Affine2 at the corner (feature_tracker.rs:143-152)
@@ -469,15 +343,13 @@ struct Tracker {
     // Enqueue one frame; images already in device memory.
     void enqueue_frame(const uint8_t* d_left, const uint8_t* d_right) {
         const int nxt = has_prev ? 1 - cur : cur;
+        // K1 + K3: both pyramids and FAST-9 in every cell of the left image (its corner as a
+        // cell-indexed identity affine) in one launch
         PyrIO io{};
         io.src[0] = d_left; io.dst[0] = pyr(nxt, 0);
         io.src[1] = d_right; io.dst[1] = pyr(nxt, 1);
+        io.fast_cells = n_cells; io.fg = G; io.fast_pt = cell_pt.p; io.fast_aff = new_aff.p;
         plan.enqueue(io, 2, stream);
-        // FAST-9 in every cell, its corner as a cell-indexed identity affine
-        const uint8_t* cur0 = pyr(nxt, 0);  // level 0 == the left image
-        hipLaunchKernelGGL(fast_cells_kernel, dim3(n_cells), dim3(256), (size_t)P.grid_size * P.grid_size, stream,
-                           cur0, G, nullptr, nullptr, 0, cell_pt.p, new_aff.p);
-        RSVIO_HIP(hipGetLastError());
         {  // one LK launch: [cam0 temporal, cam1 temporal,] stereo of every cell's corner
             TrackLaunch L{};
             L.w = P.width; L.h = P.height; L.levels = P.levels; L.max_iter = P.max_iterations;
