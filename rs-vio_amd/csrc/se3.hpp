@@ -44,20 +44,49 @@ __device__ __forceinline__ void huber(double s, double d, double* rho, double* w
     }
 }
 
-// T (+) delta = T * Exp([rho; theta]) (same formula as oracle orc_se3_plus)
+// Coefficient k of the even power series in u = theta^2 used by se3_plus: (-1)^k / (4^k (2k)!)
+// for cos(theta/2), (-1)^k / (2 4^k (2k+1)!) for sin(theta/2)/theta, (-1)^k / (2k+2)! for
+// (1 - cos theta)/theta^2 and (-1)^k / (2k+3)! for (theta - sin theta)/theta^3.
+constexpr double se3_series_coef(int which, int k) {
+    double f = 1.0;  // the factorial
+    const int n = which == 0 ? 2 * k : which == 1 ? 2 * k + 1 : which == 2 ? 2 * k + 2 : 2 * k + 3;
+    for (int i = 2; i <= n; ++i) f *= (double)i;
+    double q = 1.0;
+    if (which <= 1)
+        for (int i = 0; i < k; ++i) q *= 4.0;
+    const double v = 1.0 / (f * q * (which == 1 ? 2.0 : 1.0));
+    return (k & 1) ? -v : v;
+}
+
+template <int W>
+__device__ __forceinline__ double se3_series(double u) {
+    constexpr int kTerms = 8;  // u <= 1/16: the first omitted term is < 1e-24 of the sum
+    double p = se3_series_coef(W, kTerms - 1);
+#pragma unroll
+    for (int k = kTerms - 2; k >= 0; --k) p = fma(p, u, se3_series_coef(W, k));
+    return p;
+}
+
+// T (+) delta = T * Exp([rho; theta]) (same formula as oracle orc_se3_plus).  An LM step's
+// rotation is small: for |theta| < 1/4 the four functions of theta it needs are even power
+// series in theta^2 (no square root, sin/cos or division on the chain; within an ulp or two of
+// the closed forms -- tolerance parity), and the product quaternion is normalised by a
+// reciprocal square root refined by two Newton steps.
 __device__ inline void se3_plus(const double* p7, const double* d, double* out) {
     const double* rho = d;
     const double* om = d + 3;
     double th2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
-    double th = sqrt(th2);
     double qd[4], A, Bc;
-    if (th < 1e-8) {
-        qd[0] = 1.0; qd[1] = 0.5 * om[0]; qd[2] = 0.5 * om[1]; qd[3] = 0.5 * om[2];
-        A = 0.5 - th2 / 24.0;
-        Bc = 1.0 / 6.0 - th2 / 120.0;
+    if (th2 < 0.0625) {
+        const double s = se3_series<1>(th2);  // sin(theta/2) / theta
+        qd[0] = se3_series<0>(th2);           // cos(theta/2)
+        qd[1] = s * om[0]; qd[2] = s * om[1]; qd[3] = s * om[2];
+        A = se3_series<2>(th2);
+        Bc = se3_series<3>(th2);
     } else {
         // one sincos of theta/2: sin(th) = 2 s c, 1 - cos(th) = 2 s^2 (same values as the
         // oracle's libm calls to within an ulp; tolerance parity)
+        const double th = sqrt(th2);
         double sh, ch;
         sincos(0.5 * th, &sh, &ch);
         const double ith = 1.0 / th;
@@ -80,7 +109,11 @@ __device__ inline void se3_plus(const double* p7, const double* d, double* out) 
     double w0 = p7[3], x0 = p7[4], y0 = p7[5], z0 = p7[6];
     double qn[4] = {w0 * qd[0] - x0 * qd[1] - y0 * qd[2] - z0 * qd[3], w0 * qd[1] + x0 * qd[0] + y0 * qd[3] - z0 * qd[2],
                     w0 * qd[2] - x0 * qd[3] + y0 * qd[0] + z0 * qd[1], w0 * qd[3] + x0 * qd[2] - y0 * qd[1] + z0 * qd[0]};
-    const double inn = 1.0 / sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    const double n2 = qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3];
+    const double h = 0.5 * n2;
+    double inn = __builtin_amdgcn_rsq(n2);
+    inn = inn * fma(-h * inn, inn, 1.5);
+    inn = inn * fma(-h * inn, inn, 1.5);
     for (int i = 0; i < 4; ++i) out[3 + i] = qn[i] * inn;
 }
 
