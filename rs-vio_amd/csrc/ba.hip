@@ -1649,10 +1649,17 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 // K7: the pending decision at the end of a chunk of iterations (one wave, in place: the state
 // the host reads back, and the next chunk's K4c finds nothing pending).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la) {
+// host: the pinned host copy of the state the host reads at the end of a chunk -- written here
+// directly (system-scope release), so no copy follows the solve on the stream
+__global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
+                                                   LmState* host) {
     STAMP(8);
     const LmState s = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
-    if (threadIdx.x == 0) *Wk.st = s;
+    if (threadIdx.x == 0) {
+        *Wk.st = s;
+        *host = s;
+        __threadfence_system();
+    }
     STAMP(10);
 }
 
@@ -2197,7 +2204,7 @@ struct BundleAdjuster {
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
         hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, prob(), work_at(it & 1), sharded() ? 1 : 0,
-                           lm_args(cfg));
+                           lm_args(cfg), h_state.p);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -2216,10 +2223,8 @@ struct BundleAdjuster {
     void enqueue_chunk(int k) {
         for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg, pend.enq + i);
         pend.enq += k;
-        enqueue_decide(pend.cfg, pend.enq);
+        enqueue_decide(pend.cfg, pend.enq);  // K7 also writes the state into h_state
         RSVIO_HIP(hipEventRecord(ev1, stream));
-        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p + (pend.enq & 1), sizeof(LmState), hipMemcpyDeviceToHost,
-                                 stream));
     }
 
     void start(const rsvio_lm_cfg& cfg) {
@@ -2244,8 +2249,6 @@ struct BundleAdjuster {
         if (start_graph(cfg, k)) {
             pend.enq += k;
             RSVIO_HIP(hipEventRecord(ev1, stream));
-            RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p + (pend.enq & 1), sizeof(LmState), hipMemcpyDeviceToHost,
-                                     stream));
         } else {
             enqueue_start(cfg.lambda_init);
             enqueue_chunk(k);
