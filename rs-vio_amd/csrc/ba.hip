@@ -31,6 +31,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -214,6 +215,7 @@ struct Work {
     double* trial4;          // 4 (sharded: reduced trial scalars)
     const LmState* st_prev;  // K4c: the state left by the previous iteration (read only)
     LmState* st;             // this iteration's state (K4c's owner block writes it; K5, K6 use it)
+    unsigned long long* tick;  // [0] decisions published to the host, [1] solve start (wall clock)
 };
 
 __device__ __forceinline__ size_t sys_len(const Geometry& G) { return (size_t)G.n_pb * 36 + 12 * G.n_free + 2; }
@@ -230,6 +232,7 @@ __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
         Wk.pw[1][i] = Wk.pw_init[i];
     }
     if (i == 0) {
+        Wk.tick[1] = wall_clock64();
         *Wk.singular = 0;
         LmState s{};
         s.lambda = lambda0;
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk,
             Wk.pw[1][i] = Wk.pw_init[i];
         }
         if (s == 0) {
+            Wk.tick[1] = wall_clock64();
             *Wk.singular = 0;
             LmState st{};
             st.lambda = lambda0;
@@ -1651,14 +1655,22 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 // ---------------------------------------------------------------------------------------
 // host: the pinned host copy of the state the host reads at the end of a chunk -- written here
 // directly (system-scope release), so no copy follows the solve on the stream
+// host: the pinned LmState copy; htick (pinned, fine-grained): [1] solve start, [2] this
+// decision's wall clock, then [0] = the decision's ticket, a system-scope release the host polls
+// (rsvio_ba_wait returns on it, before the kernel's end-of-kernel signal).
 __global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
-                                                   LmState* host) {
+                                                   LmState* host, unsigned long long* htick) {
     STAMP(8);
     const LmState s = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
     if (threadIdx.x == 0) {
         *Wk.st = s;
         *host = s;
+        const unsigned long long t = Wk.tick[0] + 1;
+        Wk.tick[0] = t;
+        htick[1] = Wk.tick[1];
+        htick[2] = wall_clock64();
         __threadfence_system();
+        __hip_atomic_store(htick, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     STAMP(10);
 }
@@ -1844,6 +1856,13 @@ struct BundleAdjuster {
     size_t n_pad = 0;
     DevBuf<LmState> d_state;  // two copies, alternating by iteration (LmState)
     HostBuf<LmState> h_state;
+    // decision tickets (ba_lm_decide): device counter + start stamp, pinned fine-grained host
+    // copy; n_tick = decisions enqueued (graph launches included); settled = stream known idle
+    DevBuf<unsigned long long> d_tick;
+    unsigned long long* h_tick = nullptr;
+    unsigned long long n_tick = 0;
+    bool settled = true, tick_wait = true;
+    double wclk_khz = 1.0e5;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     // collective of the sharded path: 0 none (single rank), 1 RCCL, 2 peer-to-peer one-shot
@@ -1863,7 +1882,19 @@ struct BundleAdjuster {
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
-        h_state.alloc(1);
+        h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
+        d_tick.alloc(2);
+        RSVIO_HIP(hipMemset(d_tick.p, 0, 2 * sizeof(unsigned long long)));
+        RSVIO_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_tick), 4 * sizeof(unsigned long long),
+                                hipHostMallocCoherent));
+        std::memset(h_tick, 0, 4 * sizeof(unsigned long long));
+        {
+            int khz = 0;
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, P.device) == hipSuccess && khz > 0)
+                wclk_khz = khz;
+        }
+        const char* wv = std::getenv("RSVIO_BA_WAIT");  // "sync": hipStreamSynchronize (A/B switch)
+        tick_wait = !(wv && std::strcmp(wv, "sync") == 0);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
@@ -1871,6 +1902,8 @@ struct BundleAdjuster {
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
     }
     ~BundleAdjuster() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (h_tick) (void)hipHostFree(h_tick);
         drop_graph();
         if (comm) ncclCommDestroy(comm);
         for (int r = 0; r < kP2PMax; ++r)
@@ -1936,6 +1969,7 @@ struct BundleAdjuster {
         w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p;
         w.st = d_state.p + si;
         w.st_prev = w.st;
+        w.tick = d_tick.p;
         return w;
     }
 
@@ -2204,7 +2238,7 @@ struct BundleAdjuster {
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
         hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, prob(), work_at(it & 1), sharded() ? 1 : 0,
-                           lm_args(cfg), h_state.p);
+                           lm_args(cfg), h_state.p, h_tick);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -2224,6 +2258,7 @@ struct BundleAdjuster {
         for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg, pend.enq + i);
         pend.enq += k;
         enqueue_decide(pend.cfg, pend.enq);  // K7 also writes the state into h_state
+        ++n_tick;
         RSVIO_HIP(hipEventRecord(ev1, stream));
     }
 
@@ -2241,12 +2276,14 @@ struct BundleAdjuster {
             return;
         }
         pend.max_it = std::max(cfg.max_iterations, 1);
+        settled = false;
         RSVIO_HIP(hipEventRecord(ev0, stream));
         const int k = std::min(std::max(last_iterations, 1), pend.max_it);
         // a new problem (every keyframe in the Estimator) is re-captured: capture + instantiate +
         // one launch measured cheaper in host time than its ~25 direct launches (config-4 BA stage
         // 0.100 vs 0.115 ms per frame, round 2), so graphs stay on for fresh problems too
         if (start_graph(cfg, k)) {
+            ++n_tick;
             pend.enq += k;
             RSVIO_HIP(hipEventRecord(ev1, stream));
         } else {
@@ -2265,15 +2302,27 @@ struct BundleAdjuster {
             res->solve_ms = 0.0;
             return;
         }
+        // single rank: return as soon as the last decision's ticket lands in pinned host memory
+        // (its state was written before it); the stream settles before anything else touches
+        // the handle's buffers (require_idle).  Sharded, or RSVIO_BA_WAIT=sync: stream sync.
+        const bool by_tick = tick_wait && coll == 0;
         while (true) {
-            RSVIO_HIP(hipStreamSynchronize(stream));
+            if (by_tick)
+                wait_tick();
+            else
+                RSVIO_HIP(hipStreamSynchronize(stream));
             if (h_state.p->done || pend.enq >= pend.max_it) break;
             enqueue_chunk(std::min(iter_chunk, pend.max_it - pend.enq));
         }
         last_iterations = h_state.p->iter;
         if (coll == 2) p2p_check();
         float ms = 0.0f;
-        RSVIO_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+        if (by_tick) {
+            ms = (float)((double)(h_tick[2] - h_tick[1]) / wclk_khz);
+        } else {
+            settled = true;
+            RSVIO_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+        }
         const LmState& s = *h_state.p;
         res->status = s.status;
         res->iterations = s.iter;
@@ -2306,6 +2355,7 @@ struct BundleAdjuster {
     // open the peers' exchange buffers and self-test one all-reduce; on any failure the
     // handle keeps its previous collective
     void p2p_attach(int nr, int rk, const hipIpcMemHandle_t* hs) {
+        settle();
         if (nr < 1 || nr > kP2PMax || rk < 0 || rk >= nr) throw std::invalid_argument("P2P: bad rank layout");
         if (!xbuf) throw std::logic_error("P2P: export the buffer first");
         P2P P{};
@@ -2366,8 +2416,35 @@ struct BundleAdjuster {
 
     // entry points that read or replace what an in-flight solve uses (rsvio_ba_run_async before
     // rsvio_ba_wait) are refused, as set_stream is
-    void require_idle(const char* what) const {
+    void require_idle(const char* what) {
         if (pend.active) throw std::logic_error(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
+        settle();
+    }
+
+    // the stream's tail after a ticket (the decision kernel's exit, its cache write-back) is
+    // drained before host-side copies touch the buffers
+    void settle() {
+        if (!settled) {
+            RSVIO_HIP(hipStreamSynchronize(stream));
+            settled = true;
+        }
+    }
+
+    // spin on the ticket of the last enqueued decision; a bounded spin (1 s) falls back to a
+    // stream sync, which reports a device error if there was one
+    void wait_tick() {
+        const unsigned long long want = n_tick;
+        auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 1;; ++it) {
+            if (__atomic_load_n(h_tick, __ATOMIC_ACQUIRE) >= want) return;
+            if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+                RSVIO_HIP(hipStreamSynchronize(stream));
+                settled = true;
+                if (__atomic_load_n(h_tick, __ATOMIC_ACQUIRE) >= want) return;
+                throw std::runtime_error("BA: the decision ticket never arrived");
+            }
+            __builtin_ia32_pause();
+        }
     }
 
     void get_state(double* pose7, double* pW) {
@@ -2560,6 +2637,7 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
         ncclUniqueId id;  // a 1-rank communicator is legal: it runs the sharded code path on one GPU
         __builtin_memcpy(&id, unique_id, sizeof(id));
         RSVIO_HIP(hipSetDevice(B.P.device));
+        B.settle();
         if (ncclCommInitRank(&B.comm, nranks, id, rank) != ncclSuccess) {
             rsvio::set_last_error("ncclCommInitRank failed");
             return (int)RSVIO_ERR_RCCL;

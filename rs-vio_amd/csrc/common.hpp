@@ -136,9 +136,9 @@ template <class T>
 struct HostBuf {
     T* p = nullptr;
     size_t n = 0;
-    void alloc(size_t count) {
+    void alloc(size_t count, unsigned flags = hipHostMallocDefault) {
         release();
-        if (count) RSVIO_HIP(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+        if (count) RSVIO_HIP(hipHostMalloc(&p, count * sizeof(T), flags));
         n = count;
     }
     void release() {
