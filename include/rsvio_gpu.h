@@ -307,7 +307,11 @@ int rsvio_ba_set_problem(rsvio_ba* ba, int32_t n_kf, const double* pose7, const 
 int rsvio_ba_run(rsvio_ba* ba, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
 /* rsvio_ba_run split in two so the host can overlap other work (e.g. the next frame's
  * tracking) with the solve: _run_async enqueues the first chunk of LM iterations and returns;
- * _wait completes the solve and fills res.  One solve in flight per handle. */
+ * _wait completes the solve and fills res.  One solve in flight per handle.  Single rank, _wait
+ * returns when the final LM state has landed in host memory (a ticket the last decision kernel
+ * publishes); the stream may still be draining that kernel's exit, and the handle synchronises
+ * it before any later call copies to or from its buffers.  res->solve_ms: device wall clock
+ * from the solve's first kernel to its last decision. */
 int rsvio_ba_run_async(rsvio_ba* ba, const rsvio_lm_cfg* cfg);
 /* Enqueue the handle's work on a caller-owned stream (NULL: back to the handle's own stream). */
 int rsvio_ba_set_stream(rsvio_ba* ba, void* stream);
