@@ -2259,7 +2259,7 @@ struct BundleAdjuster {
         pend.enq += k;
         enqueue_decide(pend.cfg, pend.enq);  // K7 also writes the state into h_state
         ++n_tick;
-        RSVIO_HIP(hipEventRecord(ev1, stream));
+        if (!by_tick()) RSVIO_HIP(hipEventRecord(ev1, stream));
     }
 
     void start(const rsvio_lm_cfg& cfg) {
@@ -2277,7 +2277,7 @@ struct BundleAdjuster {
         }
         pend.max_it = std::max(cfg.max_iterations, 1);
         settled = false;
-        RSVIO_HIP(hipEventRecord(ev0, stream));
+        if (!by_tick()) RSVIO_HIP(hipEventRecord(ev0, stream));  // the ticket carries device stamps
         const int k = std::min(std::max(last_iterations, 1), pend.max_it);
         // a new problem (every keyframe in the Estimator) is re-captured: capture + instantiate +
         // one launch measured cheaper in host time than its ~25 direct launches (config-4 BA stage
@@ -2285,7 +2285,7 @@ struct BundleAdjuster {
         if (start_graph(cfg, k)) {
             ++n_tick;
             pend.enq += k;
-            RSVIO_HIP(hipEventRecord(ev1, stream));
+            if (!by_tick()) RSVIO_HIP(hipEventRecord(ev1, stream));
         } else {
             enqueue_start(cfg.lambda_init);
             enqueue_chunk(k);
@@ -2305,7 +2305,7 @@ struct BundleAdjuster {
         // single rank: return as soon as the last decision's ticket lands in pinned host memory
         // (its state was written before it); the stream settles before anything else touches
         // the handle's buffers (require_idle).  Sharded, or RSVIO_BA_WAIT=sync: stream sync.
-        const bool by_tick = tick_wait && coll == 0;
+        const bool by_tick = this->by_tick();
         while (true) {
             if (by_tick)
                 wait_tick();
@@ -2416,6 +2416,9 @@ struct BundleAdjuster {
 
     // entry points that read or replace what an in-flight solve uses (rsvio_ba_run_async before
     // rsvio_ba_wait) are refused, as set_stream is
+    // single rank waits on the decision ticket (RSVIO_BA_WAIT=sync: on the stream + events)
+    bool by_tick() const { return tick_wait && coll == 0; }
+
     void require_idle(const char* what) {
         if (pend.active) throw std::logic_error(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
         settle();

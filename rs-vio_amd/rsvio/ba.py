@@ -32,6 +32,9 @@ def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, hub
     return _lib.LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init, linear_solver)
 
 
+_DEFAULT_CFG = lm_cfg()
+
+
 def fallback_cfg(cfg=None):
     """The SparseCholesky configuration the reference retries with (sliding_window.rs:333-341)."""
     c = cfg or lm_cfg()
@@ -115,7 +118,7 @@ class BundleAdjuster:
 
     def run_async(self, cfg=None) -> None:
         """Enqueue the solve and return (rsvio_ba_run_async); wait() completes it."""
-        self._cfg = cfg or lm_cfg()  # kept alive until wait()
+        self._cfg = cfg or _DEFAULT_CFG  # kept alive until wait() (the C side only reads it)
         check(_lib.load().rsvio_ba_run_async(self._h, C.byref(self._cfg)))
 
     def wait(self) -> _lib.BaResult:
