@@ -233,6 +233,28 @@ def test_async_solve_equals_run(gpu, cfg3):
     a.close()
 
 
+def test_ticket_wait_equals_stream_sync(gpu, cfg3, monkeypatch):
+    """rsvio_ba_wait on the decision ticket (default) returns the same solve as the stream-sync
+    wait (RSVIO_BA_WAIT=sync, read at handle creation), back-to-back solves included, and the
+    state read right after the ticket (get_state settles the stream) is bit-identical."""
+    monkeypatch.setenv("RSVIO_BA_WAIT", "sync")
+    s = _adjuster(gpu, cfg3)
+    monkeypatch.delenv("RSVIO_BA_WAIT")
+    t = _adjuster(gpu, cfg3)
+    for _ in range(3):
+        s.run_async()
+        t.run_async()
+        rs, rt = s.wait(), t.wait()
+        assert (rs.status, rs.iterations, rs.initial_cost, rs.final_cost) == \
+            (rt.status, rt.iterations, rt.initial_cost, rt.final_cost)
+        assert rt.status > 0 and 0.0 < rt.solve_ms < 100.0
+        ps, ws = s.state()
+        pt, wt = t.state()
+        assert np.array_equal(ps, pt) and np.array_equal(ws, wt)
+    s.close()
+    t.close()
+
+
 def test_async_wrong_call_order_refused(gpu, cfg3):
     """Between rsvio_ba_run_async and rsvio_ba_wait, every entry point that reads or replaces
     what the solve uses is refused with RSVIO_ERR_INVALID_ARG (the in-flight solve is intact)."""
