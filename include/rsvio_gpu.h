@@ -205,6 +205,20 @@ int rsvio_ft_add_points(const float* fine, int32_t w, int32_t h, const float* tr
                         float threshold, int32_t min_dist, float detection_blur, uint32_t* out_xy, int32_t cap,
                         int32_t* n_out);
 
+/* ============ T11: the trackers' f32 sin/cos (glibc sinf/cosf restated, trig.hpp) ============ */
+
+/* Rust's f32::sin/cos as se2_exp_matrix reaches them through nalgebra's Rotation2::new
+ * (src/feature_tracker/image_utilities.rs:84,93-94) and the crate's exp_se2
+ * (feature_tracker/src/feature_tracker/feature_tracking.rs:199-203): glibc sinf/cosf on x86-64
+ * Linux.  Parity entry points for the device restatement the LK kernels use:
+ * rsvio_sincosf evaluates it on n host values; rsvio_sincosf_digest evaluates it on the f32 bit
+ * patterns [first, first + count) and returns one 64-bit digest per 2^chunk_log2 inputs (the sum
+ * mod 2^64 of splitmix64(((sin bits << 32) | cos bits) + u * 0x9E3779B97F4A7C15) over inputs u,
+ * NaNs as 0x7fc00000), so all 2^32 inputs can be compared with the host's libm.  first must be
+ * chunk-aligned, first + count <= 2^32, 16 <= chunk_log2 <= 32. */
+int rsvio_sincosf(const float* x, size_t n, float* sin_out, float* cos_out);
+int rsvio_sincosf_digest(uint64_t first, uint64_t count, uint32_t chunk_log2, uint64_t* digests_out);
+
 /* ================= T12: camera unprojection (Frame::add_*_feature) ================= */
 
 /* Camera models of src/datasets/mod.rs:93-163 (camera-intrinsic-model 0.7.2):

@@ -20,8 +20,6 @@
 #include <limits>
 #include <vector>
 
-int orc_trig_mode_internal();  // tracker_oracle.cpp
-
 namespace {
 
 constexpr int NP = 52;
@@ -36,14 +34,10 @@ const float PAT[NP][2] = {
     {-3, -3}, {-1, -3}, {1, -3},  {3, -3},  {5, -3},  {7, -3},  {-5, -5}, {-3, -5}, {-1, -5},
     {1, -5},  {3, -5},  {5, -5},  {-3, -7}, {-1, -7}, {1, -7},  {3, -7}};
 
+// Rust f32::sin / f32::cos (feature_tracking.rs:199-203) -> glibc sinf / cosf on x86-64 Linux.
 inline void sin_cos(float th, float* s, float* c) {
-    if (orc_trig_mode_internal() == 1) {
-        *s = (float)std::sin((double)th);
-        *c = (float)std::cos((double)th);
-    } else {
-        *s = sinf(th);
-        *c = cosf(th);
-    }
+    *s = sinf(th);
+    *c = cosf(th);
 }
 
 // Rust `f32 as u32` saturates (NaN and negatives -> 0).

@@ -67,7 +67,7 @@ _SIG = {
                                    C.c_double, C.c_double, C.POINTER(OrcMotionResult)]),
     "orc_unproject": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
     "orc_project": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
-    "orc_set_trig_mode": (None, [C.c_int]),
+    "orc_libm_sincosf_digest": (None, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, P]),
     "orc_se2_exp": (None, [P, P]),
     "orc_pyramid_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
     "orc_pyramid_bytes": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
@@ -123,8 +123,12 @@ def _p(a):
     return a.ctypes.data
 
 
-def set_trig_mode(mode: int):
-    load().orc_set_trig_mode(mode)
+def libm_sincosf_digest(first: int, count: int, chunk_log2: int, nthreads: int = 8):
+    """libm sinf/cosf digests per 2^chunk_log2 inputs (rsvio_sincosf_digest's definition)."""
+    n = (count + (1 << chunk_log2) - 1) >> chunk_log2
+    out = np.zeros(n, np.uint64)
+    load().orc_libm_sincosf_digest(first, count, chunk_log2, nthreads, out.ctypes.data)
+    return out
 
 
 def se2_exp(twist):

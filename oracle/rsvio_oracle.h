@@ -34,9 +34,11 @@ extern "C" {
 
 /* ---------------- tracker (src/feature_tracker/) ---------------- */
 
-/* 0 = glibc sinf/cosf (what Rust f32::sin_cos calls on linux-gnu; default),
- * 1 = (float)sin((double)x) -- the correctly-rounded form the GPU kernel uses. */
-void orc_set_trig_mode(int mode);
+/* The trackers' trig is glibc sinf/cosf (what Rust f32::sin/cos call on linux-gnu).  Per-chunk
+ * digests of libm over f32 bit patterns, as rsvio_sincosf_digest defines them (the checker of
+ * the device restatement). */
+void orc_libm_sincosf_digest(uint64_t first, uint64_t count, uint32_t chunk_log2, int nthreads,
+                             uint64_t* digests);
 
 /* se2_exp_matrix (image_utilities.rs:82-106), twist [vx, vy, theta] -> row-major 3x3 */
 void orc_se2_exp(const float* twist, float* out9);

@@ -14,16 +14,11 @@
 
 namespace {
 
-int g_trig_mode = 0;
-
+// Rust f32::sin / f32::cos (reached through nalgebra Rotation2::new, image_utilities.rs:84) call
+// glibc sinf / cosf on x86-64 Linux: the oracle calls the same libm.
 inline void sin_cos_f32(float th, float* s, float* c) {
-    if (g_trig_mode == 1) {
-        *s = (float)std::sin((double)th);
-        *c = (float)std::cos((double)th);
-    } else {
-        *s = sinf(th);
-        *c = cosf(th);
-    }
+    *s = sinf(th);
+    *c = cosf(th);
 }
 
 // Rust `f32 as u32` saturates (NaN -> 0, negative -> 0).
@@ -549,10 +544,41 @@ std::vector<Corner> detect_key_points(const Img& im, uint32_t grid,
 // =====================================================================================
 extern "C" {
 
-void orc_set_trig_mode(int mode) { g_trig_mode = mode; }
+// Per-chunk digests of libm's sinf/cosf over f32 bit patterns [first, first + count), the
+// definition rsvio_sincosf_digest (include/rsvio_gpu.h) states, over nthreads threads.
+void orc_libm_sincosf_digest(uint64_t first, uint64_t count, uint32_t chunk_log2, int nthreads,
+                             uint64_t* digests) {
+    const uint64_t n_chunks = (count + (1ull << chunk_log2) - 1) >> chunk_log2;
+    for (uint64_t k = 0; k < n_chunks; ++k) digests[k] = 0;
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t)
+        pool.emplace_back([=] {
+            for (uint64_t k = (uint64_t)t; k < n_chunks; k += (uint64_t)nthreads) {
+                const uint64_t a = k << chunk_log2;
+                const uint64_t b = std::min(count, (k + 1) << chunk_log2);
+                uint64_t acc = 0;
+                for (uint64_t off = a; off < b; ++off) {
+                    const uint32_t u = (uint32_t)(first + off);
+                    float y;
+                    std::memcpy(&y, &u, 4);
+                    const float sv = sinf(y), cv = cosf(y);
+                    uint32_t sb, cb;
+                    std::memcpy(&sb, &sv, 4);
+                    std::memcpy(&cb, &cv, 4);
+                    if (sv != sv) sb = 0x7fc00000u;
+                    if (cv != cv) cb = 0x7fc00000u;
+                    uint64_t z = (((uint64_t)sb << 32) | cb) + (uint64_t)u * 0x9E3779B97F4A7C15ull;
+                    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                    acc += z ^ (z >> 31);
+                }
+                digests[k] = acc;
+            }
+        });
+    for (auto& th : pool) th.join();
+}
 }  // extern "C"
-
-int orc_trig_mode_internal() { return g_trig_mode; }
 
 extern "C" {
 

@@ -3,7 +3,7 @@
 // Replaces build_image_pyramid (feature_tracker/src/image_operations.rs:47-78), track_points /
 // track_point / track_point_at_level / exp_se2 (feature_tracking.rs:16-219) and Patch52
 // (patch.rs:57-255).  Bit-exact with oracle/ft_oracle.cpp: same f32 operations in the same
-// order (-ffp-contract=off, correctly rounded divide/sqrt), sin/cos rounded from f64 (trig.hpp).
+// order (-ffp-contract=off, correctly rounded divide/sqrt), sin/cos = glibc sinf/cosf restated (trig.hpp).
 //
 // Pyramid: one launch per level (each level is resized from the previous one); a workgroup owns
 // a 64 x 8 output tile, the vertical pass over the tile's source-column span is staged in LDS
@@ -282,7 +282,7 @@ __device__ __forceinline__ void iso_apply(const Iso& a, float x, float y, float&
 // feature_tracking.rs:195-219, twist [theta, vx, vy]
 __device__ __forceinline__ Iso exp_se2(float theta, float v0, float v1) {
     float s, c;
-    sincos_f64_rounded(theta, &s, &c);
+    libm_trig::sincosf(theta, &s, &c);
     float diag, cross;
     if (fabsf(theta) > 1e-4f) {
         diag = s / theta;

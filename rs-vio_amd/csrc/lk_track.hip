@@ -135,10 +135,10 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
     return C;
 }
 
-// image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos from trig.hpp
+// image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos = glibc sinf/cosf (trig.hpp)
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
     float s, c;
-    sincos_f64_rounded(theta, &s, &c);
+    libm_trig::sincosf(theta, &s, &c);
     float sin_by, omc_by;
     if (fabsf(theta) < __FLT_EPSILON__) {
         float th2 = theta * theta;

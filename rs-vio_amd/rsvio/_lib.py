@@ -101,6 +101,8 @@ SIG = {
                                                      C.c_size_t, C.POINTER(C.c_size_t)]),
     "rsvio_tracker_remove_ids": (C.c_int, [P, P, C.c_size_t]),
     "rsvio_tracker_stream": (P, [P]),
+    "rsvio_sincosf": (C.c_int, [P, C.c_size_t, P, P]),
+    "rsvio_sincosf_digest": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, P]),
     "rsvio_unproject": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P]),
     "rsvio_unproject_d": (C.c_int, [C.POINTER(Camera), P, C.c_size_t, P, P, P]),
     "rsvio_tracker_set_cameras": (C.c_int, [P, C.POINTER(Camera), C.POINTER(Camera)]),

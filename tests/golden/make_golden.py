@@ -41,28 +41,21 @@ def tracker_golden():
     pyr_r0 = O.build_pyramid(right[0], L)
     pyr_noise6 = O.build_pyramid(noise_img, 5)
     aff = S.track_features(left[0], 24, seed=3, spacing=12.0)
-    O.set_trig_mode(0)
     t_aff, t_valid = O.track_points(pyr_l0, pyr_l1, w, h, L, aff)
     s_aff, s_valid = O.track_points(pyr_l0, pyr_r0, w, h, L, aff)
-    O.set_trig_mode(1)
-    t_aff_cr, t_valid_cr = O.track_points(pyr_l0, pyr_l1, w, h, L, aff)
-    O.set_trig_mode(0)
     det_xy, det_score = O.detect_key_points(left[0], 30, None)
     det2_xy, det2_score = O.detect_key_points(left[0], 30, det_xy[: len(det_xy) // 2].astype(np.float32))
     # full StereoPatchTracker over 4 frames (grid 30, L=3)
-    O.set_trig_mode(1)
     tr = O.StereoTracker(w, h, L, 30, 20, 0.01)
     pipe = []
     for k in range(4):
         fl, fr = tr.process_frame(left[k], right[k])
         pipe.append((fl, fr))
-    O.set_trig_mode(0)
     pipe_l = np.array([(k, f[0], f[1], f[2]) for k, (fl, _) in enumerate(pipe) for f in fl], np.float64)
     pipe_r = np.array([(k, f[0], f[1], f[2]) for k, (_, fr) in enumerate(pipe) for f in fr], np.float64)
     np.savez_compressed(OUT / "tracker_small.npz", w=w, h=h, levels=L, left=left, right=right,
                         noise_img=noise_img, pyr_l0=pyr_l0, pyr_l1=pyr_l1, pyr_r0=pyr_r0, pyr_noise5=pyr_noise6,
-                        aff=aff, t_aff=t_aff, t_valid=t_valid, s_aff=s_aff, s_valid=s_valid, t_aff_cr=t_aff_cr,
-                        t_valid_cr=t_valid_cr, det_xy=det_xy, det_score=det_score, det2_xy=det2_xy,
+                        aff=aff, t_aff=t_aff, t_valid=t_valid, s_aff=s_aff, s_valid=s_valid, det_xy=det_xy, det_score=det_score, det2_xy=det2_xy,
                         det2_score=det2_score, pipe_l=pipe_l, pipe_r=pipe_r)
 
 
@@ -89,11 +82,10 @@ def sha(a):
 
 
 def ft_golden():
-    """feature_tracker/ crate variant: 160 x 120 mosaic frames, 3 levels (trig mode 1 = the GPU's
-    f64-rounded sin/cos).  Large float outputs are pinned by SHA-256 of their bytes."""
+    """feature_tracker/ crate variant: 160 x 120 mosaic frames, 3 levels (glibc sinf/cosf, as the
+    reference's f32::sin/cos).  Large float outputs are pinned by SHA-256 of their bytes."""
     w, h, L = 160, 120, 3
     frames = ft_frames(4, w, h)
-    O.set_trig_mode(1)
     pyr0 = O.ft_build_pyramid(frames[0], L)
     pyr1 = O.ft_build_pyramid(frames[1], L)
     pyr0_noblur = O.ft_build_pyramid(frames[0], L, blur=False)
@@ -110,7 +102,6 @@ def ft_golden():
     for k in range(len(frames)):
         ids, fxy = ft.process_frame(frames[k])
         pipe += [(k, int(i), float(p[0]), float(p[1])) for i, p in zip(ids, fxy)]
-    O.set_trig_mode(0)
     np.savez_compressed(OUT / "ft_small.npz", w=w, h=h, levels=L, frames=frames, sha_pyr0=sha(pyr0),
                         sha_pyr1=sha(pyr1), sha_pyr0_noblur=sha(pyr0_noblur), sha_score0=sha(score0), new0=new0,
                         trk_xy=trk_xy, new0_tr=new0_tr, xy=xy, iso_ssd=iso_ssd, v_ssd=v_ssd, iso_lssd=iso_lssd,

@@ -2,8 +2,8 @@
 with fused unprojection, PnP + keyframe rule, BA -- against the same host logic over the oracle
 backend (oracle/estimator.py), frame by frame on the rendered stream.
 
-Parity: features (ids, f32 undistorted coordinates) bit-exact every frame (trig mode 1, the
-oracle's device-matched sin/cos); keyframe flags equal; PnP and BA outcomes equal in class
+Parity: features (ids, f32 undistorted coordinates) bit-exact every frame (both sides use glibc
+sinf/cosf semantics, as the reference's f32::sin/cos); keyframe flags equal; PnP and BA outcomes equal in class
 (ran / success / failure); poses within 1e-6 m / rad -- BA and PnP agree to 1e-7 per solve
 (test_ba_gpu, test_motion_gpu) and map points are narrowed to f32 between solves, so
 differences may carry over frames.  The termination REASON of a converged LM (cost tolerance 1
@@ -41,37 +41,33 @@ def _compare_with_oracle(oracle, s, win):
     from rsvio.estimator import DeviceBackend, Estimator
     h, w = s.frames[0][0].shape
     cams = [Camera.opencv5(*p) for p in s.intrinsics]
-    oracle.set_trig_mode(1)
-    try:
-        dev = _Spy(DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0))
-        orc = _Spy(OracleBackend(oracle, w, h, cams))
-        ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev)
-        eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=orc)
-        n_kf = flips = 0
-        for k, (l, r) in enumerate(s.frames):
-            rd = ed.process_frame(l, r)
-            ro = eo.process_frame(l, r)
-            for (ids_d, uv_d), (ids_o, uv_o) in zip(dev.feats, orc.feats):
-                assert np.array_equal(ids_d, ids_o), f"frame {k}"
-                assert np.array_equal(np.asarray(uv_d, np.float32).view(np.uint32),
-                                      np.asarray(uv_o, np.float32).view(np.uint32)), f"frame {k}"
-            assert rd.is_keyframe == ro.is_keyframe, f"frame {k}"
-            for a, b in ((rd.pnp_status, ro.pnp_status), (rd.ba_status, ro.ba_status)):
-                assert (a is None) == (b is None) and (a is None or (a > 0) == (b > 0)), f"frame {k}: {a} vs {b}"
-            flips += (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)
-            assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
-            n_kf += rd.is_keyframe
-        assert flips <= max(1, len(s.frames) // 20), flips
-        for Td, To in zip(ed.trajectory(), eo.trajectory()):
-            assert np.abs(Td - To).max() <= POSE_TOL
-        assert win < n_kf < len(s.frames)
-        md, mo = ed.window.map_points, eo.window.map_points
-        assert sorted(md) == sorted(mo)
-        assert max(np.abs(md[i].astype(np.float64) - mo[i]).max() for i in md) <= 1e-5
-        dev.be.close()
-        return n_kf, ed.window.fallbacks + eo.window.fallbacks
-    finally:
-        oracle.set_trig_mode(0)
+    dev = _Spy(DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0))
+    orc = _Spy(OracleBackend(oracle, w, h, cams))
+    ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev)
+    eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=orc)
+    n_kf = flips = 0
+    for k, (l, r) in enumerate(s.frames):
+        rd = ed.process_frame(l, r)
+        ro = eo.process_frame(l, r)
+        for (ids_d, uv_d), (ids_o, uv_o) in zip(dev.feats, orc.feats):
+            assert np.array_equal(ids_d, ids_o), f"frame {k}"
+            assert np.array_equal(np.asarray(uv_d, np.float32).view(np.uint32),
+                                  np.asarray(uv_o, np.float32).view(np.uint32)), f"frame {k}"
+        assert rd.is_keyframe == ro.is_keyframe, f"frame {k}"
+        for a, b in ((rd.pnp_status, ro.pnp_status), (rd.ba_status, ro.ba_status)):
+            assert (a is None) == (b is None) and (a is None or (a > 0) == (b > 0)), f"frame {k}: {a} vs {b}"
+        flips += (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)
+        assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
+        n_kf += rd.is_keyframe
+    assert flips <= max(1, len(s.frames) // 20), flips
+    for Td, To in zip(ed.trajectory(), eo.trajectory()):
+        assert np.abs(Td - To).max() <= POSE_TOL
+    assert win < n_kf < len(s.frames)
+    md, mo = ed.window.map_points, eo.window.map_points
+    assert sorted(md) == sorted(mo)
+    assert max(np.abs(md[i].astype(np.float64) - mo[i]).max() for i in md) <= 1e-5
+    dev.be.close()
+    return n_kf, ed.window.fallbacks + eo.window.fallbacks
 
 
 def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):

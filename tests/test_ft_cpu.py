@@ -148,28 +148,24 @@ def test_track_points_recovers_translation(oracle):
 def test_golden_vectors(oracle):
     g = np.load(GOLD / "ft_small.npz", allow_pickle=False)
     w, h, L = int(g["w"]), int(g["h"]), int(g["levels"])
-    oracle.set_trig_mode(1)
-    try:
-        frames = g["frames"]
-        pyr0 = oracle.ft_build_pyramid(frames[0], L)
-        pyr1 = oracle.ft_build_pyramid(frames[1], L)
-        assert sha(pyr0) == str(g["sha_pyr0"]) and sha(pyr1) == str(g["sha_pyr1"])
-        assert sha(oracle.ft_build_pyramid(frames[0], L, blur=False)) == str(g["sha_pyr0_noblur"])
-        fine0 = pyr0[:w * h].reshape(h, w)
-        assert sha(oracle.ft_shi_tomasi_score(fine0)) == str(g["sha_score0"])
-        assert np.array_equal(oracle.ft_add_points(fine0), g["new0"])
-        assert np.array_equal(oracle.ft_add_points(fine0, g["trk_xy"]), g["new0_tr"])
-        for cost, key in ((0, "ssd"), (1, "lssd")):
-            iso, ok = oracle.ft_track_points(pyr0, pyr1, w, h, g["xy"], nlevels=L, cost=cost)
-            assert np.array_equal(ok, g["v_" + key]) and np.array_equal(iso, g["iso_" + key])
-        ft = oracle.FeatureTracker(w, h, oracle.ft_config(nlevels=L))
-        rows = []
-        for k in range(len(frames)):
-            ids, xy = ft.process_frame(frames[k])
-            rows += [(k, int(i), float(p[0]), float(p[1])) for i, p in zip(ids, xy)]
-        assert np.array_equal(np.array(rows, np.float64), g["pipe"])
-    finally:
-        oracle.set_trig_mode(0)
+    frames = g["frames"]
+    pyr0 = oracle.ft_build_pyramid(frames[0], L)
+    pyr1 = oracle.ft_build_pyramid(frames[1], L)
+    assert sha(pyr0) == str(g["sha_pyr0"]) and sha(pyr1) == str(g["sha_pyr1"])
+    assert sha(oracle.ft_build_pyramid(frames[0], L, blur=False)) == str(g["sha_pyr0_noblur"])
+    fine0 = pyr0[:w * h].reshape(h, w)
+    assert sha(oracle.ft_shi_tomasi_score(fine0)) == str(g["sha_score0"])
+    assert np.array_equal(oracle.ft_add_points(fine0), g["new0"])
+    assert np.array_equal(oracle.ft_add_points(fine0, g["trk_xy"]), g["new0_tr"])
+    for cost, key in ((0, "ssd"), (1, "lssd")):
+        iso, ok = oracle.ft_track_points(pyr0, pyr1, w, h, g["xy"], nlevels=L, cost=cost)
+        assert np.array_equal(ok, g["v_" + key]) and np.array_equal(iso, g["iso_" + key])
+    ft = oracle.FeatureTracker(w, h, oracle.ft_config(nlevels=L))
+    rows = []
+    for k in range(len(frames)):
+        ids, xy = ft.process_frame(frames[k])
+        rows += [(k, int(i), float(p[0]), float(p[1])) for i, p in zip(ids, xy)]
+    assert np.array_equal(np.array(rows, np.float64), g["pipe"])
 
 
 def test_feature_tracker_bookkeeping(oracle):

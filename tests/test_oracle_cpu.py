@@ -82,7 +82,6 @@ def test_golden_tracker_reproduced(oracle):
     w, h, L = int(g["w"]), int(g["h"]), int(g["levels"])
     assert np.array_equal(oracle.build_pyramid(g["left"][0], L), g["pyr_l0"])
     assert np.array_equal(oracle.build_pyramid(g["noise_img"], 5), g["pyr_noise5"])
-    oracle.set_trig_mode(0)
     a, v = oracle.track_points(g["pyr_l0"], g["pyr_l1"], w, h, L, g["aff"])
     assert np.array_equal(v, g["t_valid"].astype(bool)) and np.array_equal(a, g["t_aff"])
     xy, sc = oracle.detect_key_points(g["left"][0], 30, None)
