@@ -545,7 +545,7 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
     Problem pr = make_problem(n_kf, kf_fixed, n_lm, n_obs, obs_lm, obs_kf, obs_cam, obs_uv, TCB2, cfg->huber_delta);
     res->iterations = 0;
     // sliding_window.rs:303-319 guards
-    int num_vars = pr.n_free + n_lm;
+    int num_vars = n_kf + n_lm;  // every keyframe variable, KF_0 included (:217-226, :304)
     if (n_obs < 6 || n_obs < num_vars) {
         res->status = LM_SKIPPED;
         res->initial_cost = res->final_cost = 0.0;

@@ -1800,8 +1800,13 @@ struct BundleAdjuster {
     rsvio_lm_cfg g_cfg{};
     bool graphs_ok = true;
     int k5_variant = 0;  // camera solve for n_free <= 10: 0 pipelined 4-wave LDL^T, 1 one-wave Gauss-Jordan
+    // an exec whose launch may still run is never destroyed: the stream settles first (a ticket
+    // wait returns before the last decision kernel has exited)
     void drop_graph() {
-        if (gexec) (void)hipGraphExecDestroy(gexec);
+        if (gexec) {
+            settle();
+            (void)hipGraphExecDestroy(gexec);
+        }
         gexec = nullptr;
         g_k = -1;
     }
@@ -1848,9 +1853,22 @@ struct BundleAdjuster {
         return true;
     }
     int last_iterations = 3;  // first chunk = previous solve's iteration count
-    DevBuf<double> d_pose2, d_pose_init, d_pw2, d_pw_init, d_slot_uv;
-    DevBuf<int> d_slot_hdr;
-    DevBuf<int> d_free, d_pairs, d_pb_fa, d_pb_fb;
+    DevBuf<double> d_pose2, d_pw2;
+    // The static problem (initial state, keyframe map, slot headers + observations, Schur pair
+    // lists, camera-block table) lives in one device arena, filled in one pinned staging image
+    // and uploaded by ONE asynchronous copy (ev_up marks its completion before the staging
+    // image is refilled).  Offsets in bytes, 256-B aligned.
+    DevBuf<uint8_t> d_arena;
+    HostBuf<uint8_t> h_arena;
+    hipEvent_t ev_up = nullptr;
+    bool up_pending = false;
+    struct ArenaLayout {
+        size_t pose_init, pw_init, free_idx, hdr, uv, pairs, pb_fa, pb_fb, total;
+    } lay{};
+    bool state_fresh = false;  // set_problem without a run since: get_state resets the buffers first
+    // host scratch of set_problem, kept across problems (no per-problem allocations)
+    std::vector<int> hs_free, hs_cnt, hs_order, hs_slot_kf, hs_slot_lm, hs_slot_obs, hs_lm_slot, hs_wave_slot,
+        hs_pslot, hs_lm_group, hs_pb_of, hs_pair_cnt, hs_pb_fa, hs_pb_fb;
     DevBuf<double> d_raws, d_rawl, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
     DevBuf<int> d_singular;
     size_t n_pad = 0;
@@ -1882,6 +1900,7 @@ struct BundleAdjuster {
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
+        RSVIO_HIP(hipEventCreateWithFlags(&ev_up, hipEventDisableTiming));
         h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
         d_tick.alloc(2);
         RSVIO_HIP(hipMemset(d_tick.p, 0, 2 * sizeof(unsigned long long)));
@@ -1903,6 +1922,7 @@ struct BundleAdjuster {
     }
     ~BundleAdjuster() {
         if (stream) (void)hipStreamSynchronize(stream);
+        settled = true;
         if (h_tick) (void)hipHostFree(h_tick);
         drop_graph();
         if (comm) ncclCommDestroy(comm);
@@ -1911,6 +1931,7 @@ struct BundleAdjuster {
         if (xbuf) (void)hipFree(xbuf);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        if (ev_up) (void)hipEventDestroy(ev_up);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -1918,35 +1939,14 @@ struct BundleAdjuster {
     static void grow(DevBuf<T>& b, size_t n) {
         if (b.n < n) b.alloc(std::max<size_t>(n, 1));
     }
-    // set_problem's uploads go through one pinned staging buffer (sized per problem), so each is a
-    // real asynchronous DMA instead of a pageable copy the host waits for
-    HostBuf<uint8_t> h_stage;
-    size_t stage_off = 0;
-    static size_t stage_bytes(size_t bytes) { return (bytes + 255) & ~(size_t)255; }
-    template <class T>
-    void up(DevBuf<T>& b, const T* src, size_t n) {
-        grow(b, n);
-        if (!n) return;
-        const size_t bytes = n * sizeof(T);
-        if (stage_off + bytes <= h_stage.n) {
-            uint8_t* dst = h_stage.p + stage_off;
-            std::memcpy(dst, static_cast<const void*>(src), bytes);
-            stage_off += stage_bytes(bytes);
-            RSVIO_HIP(hipMemcpyAsync(b.p, dst, bytes, hipMemcpyHostToDevice, stream));
-        } else {
-            RSVIO_HIP(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream));
-        }
-    }
-    template <class T>
-    void up(DevBuf<T>& b, const std::vector<T>& v) { up(b, v.data(), v.size()); }
-
     Prob prob() const {
         Prob p;
-        p.free_idx = d_free.p;
-        p.slot_hdr = reinterpret_cast<const int4*>(d_slot_hdr.p);
-        p.slot_uv = reinterpret_cast<const double2*>(d_slot_uv.p);
-        p.pairs = reinterpret_cast<const int4*>(d_pairs.p);
-        p.pb_fa = d_pb_fa.p; p.pb_fb = d_pb_fb.p;
+        p.free_idx = reinterpret_cast<const int*>(d_arena.p + lay.free_idx);
+        p.slot_hdr = reinterpret_cast<const int4*>(d_arena.p + lay.hdr);
+        p.slot_uv = reinterpret_cast<const double2*>(d_arena.p + lay.uv);
+        p.pairs = reinterpret_cast<const int4*>(d_arena.p + lay.pairs);
+        p.pb_fa = reinterpret_cast<const int*>(d_arena.p + lay.pb_fa);
+        p.pb_fb = reinterpret_cast<const int*>(d_arena.p + lay.pb_fb);
         return p;
     }
     // the kernels of LM iteration `it` read state copy it & 1 and work on copy (it + 1) & 1
@@ -1960,7 +1960,8 @@ struct BundleAdjuster {
         Work w;
         w.pose[0] = d_pose2.p; w.pose[1] = d_pose2.p + 7 * (size_t)G.n_kf;
         w.pw[0] = d_pw2.p; w.pw[1] = d_pw2.p + 3 * (size_t)std::max(G.n_lm, 1);
-        w.pose_init = d_pose_init.p; w.pw_init = d_pw_init.p;
+        w.pose_init = reinterpret_cast<const double*>(d_arena.p + lay.pose_init);
+        w.pw_init = reinterpret_cast<const double*>(d_arena.p + lay.pw_init);
         w.raws[0] = d_raws.p; w.raws[1] = d_raws.p + (size_t)kRawF * std::max<size_t>(n_pad, 1);
         w.rawl[0] = d_rawl.p; w.rawl[1] = d_rawl.p + (size_t)kLmF * std::max(G.n_lm, 1);
         w.singular = d_singular.p;
@@ -1973,6 +1974,11 @@ struct BundleAdjuster {
         return w;
     }
 
+    // sliding_window.rs:159-299 problem assembly, restated for the device layout (see Prob).  The
+    // host work is linear in the observations (counting sort by landmark, then each landmark's few
+    // (keyframe, camera) entries by insertion), written straight into the pinned staging image;
+    // no kernel and no stream synchronisation: the initial state is set by the solve's first
+    // kernel (K4 with K0 folded in).
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
@@ -1981,31 +1987,51 @@ struct BundleAdjuster {
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
             throw std::invalid_argument("problem exceeds the handle's capacities");
-        std::vector<int> free_idx(n_kf, -1);
+        auto& free_idx = hs_free;
+        free_idx.assign(n_kf, -1);
         int n_free = 0;
         for (int k = 0; k < n_kf; ++k)
             if (!kf_fixed[k]) free_idx[k] = n_free++;
         if (n_free > kMaxFree) throw std::invalid_argument("too many free keyframes");
         if (n_free < 1) throw std::invalid_argument("no free keyframe");
-        for (int i = 0; i < n_obs; ++i)
+        // observations sorted by (landmark, keyframe, camera), stable: counting sort by landmark,
+        // then insertion sort of each landmark's entries
+        auto& cnt = hs_cnt;
+        cnt.assign((size_t)n_lm + 1, 0);
+        for (int i = 0; i < n_obs; ++i) {
             if (obs_lm[i] < 0 || obs_lm[i] >= n_lm || obs_kf[i] < 0 || obs_kf[i] >= n_kf || obs_cam[i] > 1)
                 throw std::invalid_argument("observation index out of range");
-        // observations sorted by (landmark, keyframe, camera)
-        std::vector<int> order(n_obs);
-        std::iota(order.begin(), order.end(), 0);
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-            if (obs_lm[a] != obs_lm[b]) return obs_lm[a] < obs_lm[b];
-            if (obs_kf[a] != obs_kf[b]) return obs_kf[a] < obs_kf[b];
-            return obs_cam[a] < obs_cam[b];
-        });
-        std::vector<double> uv(2 * (size_t)n_obs);
-        std::vector<uint8_t> cam(n_obs);
-        std::vector<int> slot_kf, slot_lm, slot_obs, lm_slot(n_lm + 1, 0);
+            cnt[obs_lm[i] + 1] += 1;
+        }
+        for (int l = 0; l < n_lm; ++l) cnt[l + 1] += cnt[l];
+        auto& order = hs_order;
+        order.resize(n_obs);
+        {
+            auto& cur = hs_lm_slot;  // scratch cursor
+            cur.assign(cnt.begin(), cnt.end() - 1);
+            for (int i = 0; i < n_obs; ++i) order[cur[obs_lm[i]]++] = i;
+        }
+        for (int l = 0; l < n_lm; ++l) {
+            const int a0 = cnt[l], a1 = cnt[l + 1];
+            for (int q = a0 + 1; q < a1; ++q) {
+                const int o = order[q];
+                const int key = 2 * obs_kf[o] + obs_cam[o];
+                int r = q;
+                while (r > a0 && 2 * obs_kf[order[r - 1]] + obs_cam[order[r - 1]] > key) {
+                    order[r] = order[r - 1];
+                    --r;
+                }
+                order[r] = o;
+            }
+        }
+        // slots: (landmark, keyframe) runs of 1-2 observations
+        auto &slot_kf = hs_slot_kf, &slot_lm = hs_slot_lm, &slot_obs = hs_slot_obs, &lm_slot = hs_lm_slot;
+        slot_kf.clear();
+        slot_lm.clear();
+        slot_obs.clear();
+        lm_slot.assign((size_t)n_lm + 1, 0);
         for (int q = 0; q < n_obs; ++q) {
             const int o = order[q];
-            uv[2 * q] = obs_uv[2 * o];
-            uv[2 * q + 1] = obs_uv[2 * o + 1];
-            cam[q] = obs_cam[o];
             if (q == 0 || obs_lm[o] != obs_lm[order[q - 1]] || obs_kf[o] != obs_kf[order[q - 1]]) {
                 slot_kf.push_back(obs_kf[o]);
                 slot_lm.push_back(obs_lm[o]);
@@ -2016,48 +2042,24 @@ struct BundleAdjuster {
         const int n_slot = (int)slot_kf.size();
         slot_obs.push_back(n_obs);
         for (int l = 0; l < n_lm; ++l) lm_slot[l + 1] += lm_slot[l];
-        std::vector<int> slot_first(n_slot), slot_nk(n_slot), wave_slot{0};
+        // waves: whole landmarks, <= 64 slots each (greedy)
+        auto& wave_slot = hs_wave_slot;
+        wave_slot.assign(1, 0);
         for (int l = 0; l < n_lm; ++l) {
             const int nk = lm_slot[l + 1] - lm_slot[l];
             if (nk > 64) throw std::invalid_argument("a landmark is observed by more than 64 keyframes");
-            for (int s = lm_slot[l]; s < lm_slot[l + 1]; ++s) {
-                slot_first[s] = lm_slot[l];
-                slot_nk[s] = nk;
-            }
-            // greedy: whole landmarks per wave, <= 64 slots
             if (nk && lm_slot[l + 1] - wave_slot.back() > 64) wave_slot.push_back(lm_slot[l]);
         }
         if (n_slot > wave_slot.back()) wave_slot.push_back(n_slot);
         const int n_wave = (int)wave_slot.size() - 1;
-        // padded slot layout (64 per wave) with inline headers and observations (Prob::slot_hdr)
-        std::vector<int> pslot(n_slot);
-        n_pad = (size_t)64 * n_wave;
-        std::vector<int> hdr(8 * n_pad, 0);
-        std::vector<double> huv(4 * n_pad, 0.0);
-        for (int w = 0; w < n_wave; ++w)
-            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
-                const int ps = 64 * w + (sl - wave_slot[w]);
-                pslot[sl] = ps;
-                const int no = slot_obs[sl + 1] - slot_obs[sl];
-                if (no > 2)
-                    throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
-                int* h = hdr.data() + 8 * (size_t)ps;
-                h[0] = slot_kf[sl];
-                h[1] = slot_lm[sl];
-                h[2] = slot_first[sl] - wave_slot[w];
-                h[3] = slot_nk[sl];
-                h[4] = free_idx[slot_kf[sl]];
-                h[5] = no;
-                for (int q = 0; q < no; ++q) {
-                    const int o = slot_obs[sl] + q;
-                    h[6] |= cam[o] << q;
-                    huv[4 * (size_t)ps + 2 * q] = uv[2 * o];
-                    huv[4 * (size_t)ps + 2 * q + 1] = uv[2 * o + 1];
-                }
-            }
-        for (size_t ps = 0; ps < n_pad; ++ps) hdr[8 * ps + 4] = hdr[8 * ps + 5] ? hdr[8 * ps + 4] : -1;
+        for (int sl = 0; sl < n_slot; ++sl)
+            if (slot_obs[sl + 1] - slot_obs[sl] > 2)
+                throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
         // camera blocks (fa <= fb)
-        std::vector<int> pb_fa, pb_fb, pb_of((size_t)n_free * n_free, -1);
+        auto &pb_fa = hs_pb_fa, &pb_fb = hs_pb_fb, &pb_of = hs_pb_of;
+        pb_fa.clear();
+        pb_fb.clear();
+        pb_of.assign((size_t)n_free * n_free, -1);
         for (int a = 0; a < n_free; ++a)
             for (int b = a; b < n_free; ++b) {
                 pb_of[a * n_free + b] = (int)pb_fa.size();
@@ -2067,67 +2069,116 @@ struct BundleAdjuster {
         const int n_pb = (int)pb_fa.size();
         // XCD groups: wave w (K4 / K6 workgroup w, whole landmarks) is dispatched to XCD w % 8, so
         // the landmarks of group x are those of the waves w % 8 == x; their Schur chunks run on
-        // XCD x too (chunk c on XCD c % 8) and re-read the slot records K6 wrote there
-        std::vector<int> lm_group(n_lm, 0);
+        // XCD x too (chunk c on XCD c % 8) and re-read what K6 wrote there
+        auto& lm_group = hs_lm_group;
+        lm_group.assign(std::max(n_lm, 1), 0);
+        auto& pslot = hs_pslot;
+        pslot.resize(n_slot);
         for (int w = 0; w < n_wave; ++w)
-            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) lm_group[slot_lm[sl]] = w % kGrp;
-        // slot pairs of each (group, camera block), ascending landmark
-        std::vector<std::vector<std::pair<int, int>>> pairs((size_t)kGrp * std::max(n_pb, 1));
+            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
+                lm_group[slot_lm[sl]] = w % kGrp;
+                pslot[sl] = 64 * w + (sl - wave_slot[w]);
+            }
+        // slot pairs per chunk 8 pb + x: counted first (the stride), filled in landmark order below
+        const int n_chunk = kGrp * n_pb;
+        auto& pcnt = hs_pair_cnt;
+        pcnt.assign((size_t)n_chunk, 0);
         for (int l = 0; l < n_lm; ++l)
             for (int sa = lm_slot[l]; sa < lm_slot[l + 1]; ++sa) {
                 const int fa = free_idx[slot_kf[sa]];
                 if (fa < 0) continue;
                 for (int sb = sa; sb < lm_slot[l + 1]; ++sb) {
                     const int fb = free_idx[slot_kf[sb]];
-                    if (fb < 0) continue;
-                    pairs[(size_t)lm_group[l] * n_pb + pb_of[fa * n_free + fb]].push_back({sa, sb});
+                    if (fb >= 0) pcnt[kGrp * pb_of[fa * n_free + fb] + lm_group[l]] += 1;
                 }
             }
-        // chunk 8 pb + x: the pairs of block pb in group x, padded to a common stride
-        const int n_chunk = kGrp * n_pb;
-        size_t stride = 1;
-        for (const auto& pv : pairs) stride = std::max(stride, pv.size());
-        std::vector<int> pq(4 * (size_t)n_chunk * stride, 0);
-        for (size_t i = 0; i < pq.size(); i += 4) pq[i] = -1;
-        for (int b = 0; b < n_pb; ++b)
-            for (int x = 0; x < kGrp; ++x) {
-                const auto& pv = pairs[(size_t)x * n_pb + b];
-                int* d = pq.data() + 4 * ((size_t)(kGrp * b + x) * stride);
-                for (size_t q = 0; q < pv.size(); ++q) {
-                    d[4 * q] = pslot[pv[q].first];
-                    d[4 * q + 1] = pslot[pv[q].second];
-                    d[4 * q + 2] = slot_lm[pv[q].first];
-                }
-            }
-        {
-            // every DMA of the previous set_problem finished (it ends with a stream sync) and no
-            // kernel reads the stage, so it can be refilled (or regrown) now
-            size_t need = stage_bytes(sizeof(double) * 7 * (size_t)n_kf) + stage_bytes(sizeof(double) * 3 * (size_t)n_lm);
-            for (size_t b : {free_idx.size(), hdr.size(), pq.size(), pb_fa.size(), pb_fb.size()})
-                need += stage_bytes(sizeof(int) * b);
-            need += stage_bytes(sizeof(double) * huv.size());
-            if (h_stage.n < need) h_stage.alloc(need + need / 2);
-            stage_off = 0;
+        int stride = 1;
+        for (int c : pcnt) stride = std::max(stride, c);
+        n_pad = (size_t)64 * n_wave;
+        // arena layout
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        ArenaLayout L{};
+        size_t off = 0;
+        L.pose_init = off; off += al(sizeof(double) * 7 * (size_t)n_kf);
+        L.pw_init = off;   off += al(sizeof(double) * 3 * (size_t)std::max(n_lm, 1));
+        L.free_idx = off;  off += al(sizeof(int) * (size_t)n_kf);
+        L.hdr = off;       off += al(sizeof(int4) * 2 * std::max<size_t>(n_pad, 1));
+        L.uv = off;        off += al(sizeof(double2) * 2 * std::max<size_t>(n_pad, 1));
+        L.pairs = off;     off += al(sizeof(int4) * (size_t)n_chunk * stride);
+        L.pb_fa = off;     off += al(sizeof(int) * (size_t)n_pb);
+        L.pb_fb = off;     off += al(sizeof(int) * (size_t)n_pb);
+        L.total = off;
+        if (up_pending) {  // the previous upload still reads the staging image
+            RSVIO_HIP(hipEventSynchronize(ev_up));
+            up_pending = false;
         }
+        if (h_arena.n < L.total) h_arena.alloc(L.total + L.total / 4);
+        if (d_arena.n < L.total) d_arena.alloc(L.total + L.total / 4);
+        lay = L;
+        uint8_t* hb = h_arena.p;
+        std::memcpy(hb + L.pose_init, pose7, sizeof(double) * 7 * (size_t)n_kf);
+        if (n_lm) std::memcpy(hb + L.pw_init, pW, sizeof(double) * 3 * (size_t)n_lm);
+        std::memcpy(hb + L.free_idx, free_idx.data(), sizeof(int) * (size_t)n_kf);
+        // padded slot layout (64 per wave): two int4 headers + 2 double2 observations per slot
+        int* hdr = reinterpret_cast<int*>(hb + L.hdr);
+        double* huv = reinterpret_cast<double*>(hb + L.uv);
+        std::memset(hdr, 0, sizeof(int4) * 2 * n_pad);
+        std::memset(huv, 0, sizeof(double2) * 2 * n_pad);
+        for (size_t ps = 0; ps < n_pad; ++ps) hdr[8 * ps + 4] = -1;
+        for (int w = 0; w < n_wave; ++w)
+            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
+                const size_t ps = (size_t)pslot[sl];
+                const int l = slot_lm[sl];
+                int* h = hdr + 8 * ps;
+                const int no = slot_obs[sl + 1] - slot_obs[sl];
+                h[0] = slot_kf[sl];
+                h[1] = l;
+                h[2] = lm_slot[l] - wave_slot[w];
+                h[3] = lm_slot[l + 1] - lm_slot[l];
+                h[4] = no ? free_idx[slot_kf[sl]] : -1;
+                h[5] = no;
+                for (int q = 0; q < no; ++q) {
+                    const int o = order[slot_obs[sl] + q];
+                    h[6] |= obs_cam[o] << q;
+                    huv[4 * ps + 2 * q] = obs_uv[2 * (size_t)o];
+                    huv[4 * ps + 2 * q + 1] = obs_uv[2 * (size_t)o + 1];
+                }
+            }
+        {  // pairs: {slot a, slot b, landmark, 0} at a fixed stride per chunk, padding a = -1
+            int4* pq = reinterpret_cast<int4*>(hb + L.pairs);
+            for (size_t i = 0; i < (size_t)n_chunk * stride; ++i) pq[i] = make_int4(-1, 0, 0, 0);
+            std::fill(pcnt.begin(), pcnt.end(), 0);  // reused as fill cursors
+            for (int l = 0; l < n_lm; ++l)
+                for (int sa = lm_slot[l]; sa < lm_slot[l + 1]; ++sa) {
+                    const int fa = free_idx[slot_kf[sa]];
+                    if (fa < 0) continue;
+                    for (int sb = sa; sb < lm_slot[l + 1]; ++sb) {
+                        const int fb = free_idx[slot_kf[sb]];
+                        if (fb < 0) continue;
+                        const int c = kGrp * pb_of[fa * n_free + fb] + lm_group[l];
+                        pq[(size_t)c * stride + pcnt[c]++] = make_int4(pslot[sa], pslot[sb], l, 0);
+                    }
+                }
+        }
+        std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
+        std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.total, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipEventRecord(ev_up, stream));
+        up_pending = true;
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
-        G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = (int)stride;
+        G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
-        up(d_pose_init, pose7, 7 * (size_t)n_kf);
-        up(d_pw_init, pW, 3 * (size_t)n_lm);
         grow(d_pose2, 14 * (size_t)n_kf);
         grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
-        up(d_free, free_idx);
-        up(d_slot_hdr, hdr);
-        up(d_slot_uv, huv);
-        up(d_pairs, pq);
-        {  // partial systems: slots nobody writes (a block without pairs in a group) stay zero
+        {  // partial systems: every entry of every slot is written by K4c each iteration; zeroed
+           // once when (re)allocated
             const size_t nc = (size_t)kGrp * ((size_t)36 * n_pb + 12 * n_free + 2);
-            grow(d_cpart, nc);
-            RSVIO_HIP(hipMemsetAsync(d_cpart.p, 0, sizeof(double) * nc, stream));
+            if (d_cpart.n < nc) {
+                grow(d_cpart, nc);
+                RSVIO_HIP(hipMemsetAsync(d_cpart.p, 0, sizeof(double) * d_cpart.n, stream));
+            }
         }
-        up(d_pb_fa, pb_fa);
-        up(d_pb_fb, pb_fb);
         grow(d_raws, (size_t)2 * kRawF * std::max<size_t>(n_pad, 1));
         grow(d_rawl, (size_t)2 * kLmF * std::max(n_lm, 1));
         grow(d_singular, 1);
@@ -2137,9 +2188,8 @@ struct BundleAdjuster {
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
         grow(d_state, 2);
-        enqueue_reset(1e-4);  // state buffers hold the initial values until the first run
-        RSVIO_HIP(hipMemcpyAsync(h_state.p, d_state.p, sizeof(LmState), hipMemcpyDeviceToHost, stream));
-        RSVIO_HIP(hipStreamSynchronize(stream));
+        *h_state.p = LmState{};  // cur = 0: buffer 0 holds the initial state once it is set
+        state_fresh = true;
         has_problem = true;
     }
 
@@ -2250,6 +2300,7 @@ struct BundleAdjuster {
     // convergence.
     struct Pending {
         bool active = false, skipped = false;
+        bool by_tick = false;  // the wait mode fixed at start(): finish() never switches it mid-solve
         rsvio_lm_cfg cfg{};
         int enq = 0, max_it = 0;
     } pend;
@@ -2259,25 +2310,48 @@ struct BundleAdjuster {
         pend.enq += k;
         enqueue_decide(pend.cfg, pend.enq);  // K7 also writes the state into h_state
         ++n_tick;
-        if (!by_tick()) RSVIO_HIP(hipEventRecord(ev1, stream));
+        if (!pend.by_tick) RSVIO_HIP(hipEventRecord(ev1, stream));
+    }
+
+    // After a failed enqueue or a lost ticket the host's ticket count may be off by the decisions
+    // that did (not) reach the queue: settle the stream and take the device's count.
+    void resync_ticks() noexcept {
+        (void)hipStreamSynchronize(stream);
+        (void)hipGetLastError();
+        settled = true;
+        unsigned long long t = 0;
+        if (hipMemcpy(&t, d_tick.p, sizeof t, hipMemcpyDeviceToHost) == hipSuccess) n_tick = t;
+        pend.active = false;
     }
 
     void start(const rsvio_lm_cfg& cfg) {
+        // refusals first: they leave an in-flight solve untouched
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
-        if (pend.active) throw std::logic_error("a solve is already in flight (call finish first)");
+        if (pend.active) throw CallOrderError("a solve is already in flight (call finish first)");
+        try {
+            start_impl(cfg);
+        } catch (...) {
+            resync_ticks();
+            throw;
+        }
+    }
+
+    void start_impl(const rsvio_lm_cfg& cfg) {
         G.huber_delta = cfg.huber_delta;
         G.chol = cfg.linear_solver == RSVIO_SOLVER_CHOLESKY ? 1 : 0;
         pend = Pending{};
         pend.active = true;
         pend.cfg = cfg;
+        pend.by_tick = by_tick();
         // sliding_window.rs:303-319: too few residuals / underconstrained -> skipped (Ok(false))
-        if (!sharded() && (G.n_obs < 6 || G.n_obs < G.n_free + G.n_lm)) {
+        if (!sharded() && (G.n_obs < 6 || G.n_obs < G.n_kf + G.n_lm)) {
             pend.skipped = true;
             return;
         }
         pend.max_it = std::max(cfg.max_iterations, 1);
         settled = false;
-        if (!by_tick()) RSVIO_HIP(hipEventRecord(ev0, stream));  // the ticket carries device stamps
+        state_fresh = false;  // K4 (K0 folded in) sets both state buffers
+        if (!pend.by_tick) RSVIO_HIP(hipEventRecord(ev0, stream));  // the ticket carries device stamps
         const int k = std::min(std::max(last_iterations, 1), pend.max_it);
         // a new problem (every keyframe in the Estimator) is re-captured: capture + instantiate +
         // one launch measured cheaper in host time than its ~25 direct launches (config-4 BA stage
@@ -2285,7 +2359,7 @@ struct BundleAdjuster {
         if (start_graph(cfg, k)) {
             ++n_tick;
             pend.enq += k;
-            if (!by_tick()) RSVIO_HIP(hipEventRecord(ev1, stream));
+            if (!pend.by_tick) RSVIO_HIP(hipEventRecord(ev1, stream));
         } else {
             enqueue_start(cfg.lambda_init);
             enqueue_chunk(k);
@@ -2293,7 +2367,16 @@ struct BundleAdjuster {
     }
 
     void finish(rsvio_ba_result* res) {
-        if (!pend.active) throw std::logic_error("no solve in flight");
+        if (!pend.active) throw CallOrderError("no solve in flight");
+        try {
+            finish_impl(res);
+        } catch (...) {
+            resync_ticks();
+            throw;
+        }
+    }
+
+    void finish_impl(rsvio_ba_result* res) {
         pend.active = false;
         res->iterations = 0;
         if (pend.skipped) {
@@ -2305,7 +2388,7 @@ struct BundleAdjuster {
         // single rank: return as soon as the last decision's ticket lands in pinned host memory
         // (its state was written before it); the stream settles before anything else touches
         // the handle's buffers (require_idle).  Sharded, or RSVIO_BA_WAIT=sync: stream sync.
-        const bool by_tick = this->by_tick();
+        const bool by_tick = pend.by_tick;
         while (true) {
             if (by_tick)
                 wait_tick();
@@ -2355,9 +2438,9 @@ struct BundleAdjuster {
     // open the peers' exchange buffers and self-test one all-reduce; on any failure the
     // handle keeps its previous collective
     void p2p_attach(int nr, int rk, const hipIpcMemHandle_t* hs) {
-        settle();
+        require_idle("rsvio_ba_attach_p2p");
         if (nr < 1 || nr > kP2PMax || rk < 0 || rk >= nr) throw std::invalid_argument("P2P: bad rank layout");
-        if (!xbuf) throw std::logic_error("P2P: export the buffer first");
+        if (!xbuf) throw CallOrderError("P2P: export the buffer first");
         P2P P{};
         P.nranks = nr;
         P.rank = rk;
@@ -2391,13 +2474,14 @@ struct BundleAdjuster {
     }
 
     void p2p_detach() {
+        require_idle("rsvio_ba_detach_p2p");
         if (coll == 2) coll = comm ? 1 : 0;
         drop_graph();
     }
 
     // run on a caller-owned stream (e.g. one restricted to a CU subset); nullptr = own stream
     void set_stream(hipStream_t s) {
-        if (pend.active) throw std::logic_error("a solve is in flight");
+        if (pend.active) throw CallOrderError("a solve is in flight");
         RSVIO_HIP(hipStreamSynchronize(stream));
         if (s) {
             if (own_stream) RSVIO_HIP(hipStreamDestroy(stream));
@@ -2420,7 +2504,7 @@ struct BundleAdjuster {
     bool by_tick() const { return tick_wait && coll == 0; }
 
     void require_idle(const char* what) {
-        if (pend.active) throw std::logic_error(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
+        if (pend.active) throw CallOrderError(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
         settle();
     }
 
@@ -2452,6 +2536,10 @@ struct BundleAdjuster {
 
     void get_state(double* pose7, double* pW) {
         require_idle("get_state");
+        if (state_fresh) {  // no solve since set_problem: the initial state into both buffers
+            enqueue_reset(1e-4);
+            state_fresh = false;
+        }
         const int cur = h_state.p->cur;
         const Work wk = work_at(0);
         RSVIO_HIP(hipMemcpyAsync(pose7, wk.pose[cur], sizeof(double) * 7 * G.n_kf, hipMemcpyDeviceToHost, stream));
@@ -2640,7 +2728,7 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
         ncclUniqueId id;  // a 1-rank communicator is legal: it runs the sharded code path on one GPU
         __builtin_memcpy(&id, unique_id, sizeof(id));
         RSVIO_HIP(hipSetDevice(B.P.device));
-        B.settle();
+        B.require_idle("rsvio_ba_attach_comm");
         if (ncclCommInitRank(&B.comm, nranks, id, rank) != ncclSuccess) {
             rsvio::set_last_error("ncclCommInitRank failed");
             return (int)RSVIO_ERR_RCCL;
@@ -2670,6 +2758,8 @@ int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_
         for (int r = 0; r < nranks; ++r) __builtin_memcpy(&hs[r], handles + (size_t)r * sizeof(hipIpcMemHandle_t), sizeof(hipIpcMemHandle_t));
         try {
             ba->b.p2p_attach(nranks, rank, hs.data());
+        } catch (const rsvio::CallOrderError&) {
+            throw;  // refused while a solve is in flight: a caller error, not a P2P failure
         } catch (const std::exception& e) {
             rsvio::set_last_error(std::string("P2P attach failed: ") + e.what());
             return (int)RSVIO_ERR_RCCL;
@@ -2680,8 +2770,10 @@ int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_
 
 int rsvio_ba_detach_p2p(rsvio_ba* ba) {
     if (!ba) return RSVIO_ERR_INVALID_ARG;
-    ba->b.p2p_detach();
-    return RSVIO_OK;
+    return guarded([&] {
+        ba->b.p2p_detach();
+        return (int)RSVIO_OK;
+    });
 }
 
 }  // extern "C"

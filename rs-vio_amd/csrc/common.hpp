@@ -26,6 +26,13 @@ struct HipError {
                                             std::to_string(__LINE__)};                     \
     } while (0)
 
+// A caller error: a bad argument or an entry point called in the wrong order (e.g. while a solve
+// is in flight).  std::invalid_argument and this map to RSVIO_ERR_INVALID_ARG; other
+// std::logic_errors (length_error, out_of_range from the STL) are internal failures.
+struct CallOrderError : std::invalid_argument {
+    using std::invalid_argument::invalid_argument;
+};
+
 // Run a C-ABI body, translating exceptions into status codes (never unwinds across the ABI).
 template <class F>
 int guarded(F&& f) {
@@ -37,7 +44,7 @@ int guarded(F&& f) {
     } catch (const std::bad_alloc&) {
         set_last_error("host allocation failed");
         return RSVIO_ERR_NOMEM;
-    } catch (const std::logic_error& e) {  // bad arguments or call order (std::invalid_argument too)
+    } catch (const std::invalid_argument& e) {  // bad arguments or call order (CallOrderError)
         set_last_error(e.what());
         return RSVIO_ERR_INVALID_ARG;
     } catch (const std::exception& e) {

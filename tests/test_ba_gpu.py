@@ -255,6 +255,50 @@ def test_ticket_wait_equals_stream_sync(gpu, cfg3, monkeypatch):
     t.close()
 
 
+def test_recapture_after_ticket_wait(gpu, cfg3):
+    """A ticket wait returns before the last decision kernel has exited; the next solve with a
+    different LM configuration re-captures the graph (the old exec is destroyed only after the
+    stream settles).  Each solve equals the same solve on a fresh handle, bit for bit."""
+    from rsvio.ba import fallback_cfg, lm_cfg
+    cfgs = [lm_cfg(), lm_cfg(max_iterations=7), fallback_cfg(), lm_cfg(lambda_init=1e-3), lm_cfg()]
+    a = _adjuster(gpu, cfg3)
+    for c in cfgs:
+        a.run_async(c)
+        ra = a.wait()
+        pa, wa = a.state()
+        f = _adjuster(gpu, cfg3)
+        rf = f.run(c)
+        pf, wf = f.state()
+        f.close()
+        assert (ra.status, ra.iterations, ra.final_cost) == (rf.status, rf.iterations, rf.final_cost)
+        assert np.array_equal(pa, pf) and np.array_equal(wa, wf)
+    # back to back: the async solve's ticket, then a synchronous run with another config at once
+    a.run_async(lm_cfg())
+    a.wait()
+    r = a.run(lm_cfg(max_iterations=3))
+    assert r.iterations <= 3
+    a.close()
+
+
+def test_skip_guard_counts_every_keyframe(gpu, oracle):
+    """sliding_window.rs:304,315: num_variables counts every keyframe variable, the fixed KF_0
+    included, so n_obs == n_free + n_lm is underconstrained (skipped) and n_obs == n_kf + n_lm
+    is not -- on the device and in the oracle."""
+    import dataclasses
+
+    from rsvio import synthetic as S
+    prob = S.ba_problem(n_kf=3, n_lm=8, kf_per_lm=3, seed=9, init_seed=10)
+    for n_obs, skipped in ((prob.n_kf - 1 + prob.n_lm, True), (prob.n_kf + prob.n_lm, False)):
+        cut = dataclasses.replace(prob, obs_lm=prob.obs_lm[:n_obs], obs_kf=prob.obs_kf[:n_obs],
+                                  obs_cam=prob.obs_cam[:n_obs], obs_uv=prob.obs_uv[:n_obs])
+        assert len(cut.obs_lm) == n_obs and int(cut.kf_fixed.sum()) == 1
+        ba = _adjuster(gpu, cut)
+        r = ba.run()
+        _, _, ro = oracle.ba_solve(cut)
+        assert (r.status == -2) == skipped and (ro.status == -2) == skipped, (n_obs, r.status, ro.status)
+        ba.close()
+
+
 def test_async_wrong_call_order_refused(gpu, cfg3):
     """Between rsvio_ba_run_async and rsvio_ba_wait, every entry point that reads or replaces
     what the solve uses is refused with RSVIO_ERR_INVALID_ARG (the in-flight solve is intact)."""
@@ -262,7 +306,9 @@ def test_async_wrong_call_order_refused(gpu, cfg3):
     ra = a.run()
     pa, wa = a.state()
     a.run_async()
-    for call in (lambda: a.state(), lambda: a.set_problem_from(cfg3), lambda: a.run_async()):
+    for call in (lambda: a.state(), lambda: a.set_problem_from(cfg3), lambda: a.run_async(),
+                 lambda: a.detach_p2p(), lambda: a.attach_comm(1, 0, a.rccl_unique_id()),
+                 lambda: a.attach_p2p(1, 0, [bytes(64)])):
         with pytest.raises(gpu.RsvioError) as e:
             call()
         assert e.value.code == -1
