@@ -276,17 +276,29 @@ def measure_config5_row(device: int, cpu: bool, reps: int = 10):
                         "frac": round(tf / FP64_PEAK_TFLOPS, 6), "flop_per_iter": flops,
                         "note": "latency-bound LM chain (3 kernels per iteration, serial 114x114 solve)"}}
     if cpu:
-        from oracle import oracle as O
+        legs = [cpu_ba_leg(prob, host_cores(), 3.0, "config-5"), cpu_ba_leg(prob, 1, 2.0, "config-5")]
+        row["cpu_baseline"] = dict(legs[0], single_thread=legs[1])
+    return row
+
+
+def cpu_ba_leg(prob, threads: int, budget_s: float, name: str) -> dict:
+    """The oracle's BA solve on the host: `threads` = 1 is the sequential reference order, more
+    is the threaded Schur variant (landmark ranges in parallel, BASELINE.md's nproc leg)."""
+    from oracle import oracle as O
+    O.set_ba_threads(threads)
+    try:
         t0 = time.perf_counter()
         k = 0
-        while time.perf_counter() - t0 < 2.0 or k < 2:
+        while time.perf_counter() - t0 < budget_s or k < 2:
             _, _, rr = O.ba_solve(prob)
             k += 1
         cms = 1e3 * (time.perf_counter() - t0) / k
-        row["cpu_baseline"] = {"value": round(cms / max(rr.iterations, 1), 3), "unit": "ms/iter", "cores": 1,
-                               "kind": "port", "ms_per_solve": round(cms, 2), "lm_iterations": rr.iterations,
-                               "sample": f"{k} config-5 solves, oracle/ba_oracle.cpp, 1 thread"}
-    return row
+    finally:
+        O.set_ba_threads(1)
+    return {"value": round(cms / max(rr.iterations, 1), 3), "unit": "ms/iter", "cores": threads, "kind": "port",
+            "ms_per_solve": round(cms, 2), "lm_iterations": rr.iterations,
+            "sample": f"{k} {name} solves, oracle/ba_oracle.cpp, " +
+                      ("1 thread" if threads == 1 else f"{threads} threads (threaded Schur: landmark ranges)")}
 
 
 class _StageTimer:
@@ -399,27 +411,52 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         from oracle import oracle as O
         from oracle.estimator import OracleBackend
         host = [(l.cpu().numpy(), r.cpu().numpy()) for l, r in s.frames]
-        ob = _StageTimer(OracleBackend(O, W, H, cams))
-        est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=ob)
-        t0 = time.perf_counter()
-        k = 0
-        oerr = 0.0
-        # the whole stream when it fits the budget: the oracle's drift on the same frames is the
-        # correctness anchor of max_position_error_m (the reference's quirks -- identity poses
-        # until the window fills, depth-2.0 initialisation, f32 map -- drift alike)
-        while k < len(host) and (time.perf_counter() - t0 < cpu_seconds or k < 30):
-            ro = est.process_frame(*host[k])
-            oerr = max(oerr, float(np.linalg.norm(ro.T_W_B[:3, 3] - s.T_W_B[k][:3, 3])))
-            k += 1
-        cel = time.perf_counter() - t0
+
+        def oracle_leg(threads, budget_s, compare):
+            """The same Estimator host logic over the oracle backend: `threads` = 1 sequential,
+            more = the tracker's levels / features and the Schur BA threaded (rayon analogue)."""
+            ob = _StageTimer(OracleBackend(O, W, H, cams, threads=threads))
+            O.set_ba_threads(threads)
+            est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=ob)
+            t0 = time.perf_counter()
+            k, oerr, first, maxd = 0, 0.0, None, 0.0
+            try:
+                # the whole stream when it fits the budget: frame-by-frame parity of the device run
+                # (keyframe flags, PnP / BA status, pose) and the oracle's drift on the same frames
+                while k < len(host) and (time.perf_counter() - t0 < budget_s or k < 30):
+                    ro = est.process_frame(*host[k])
+                    oerr = max(oerr, float(np.linalg.norm(ro.T_W_B[:3, 3] - s.T_W_B[k][:3, 3])))
+                    if compare:
+                        rd = out[k]
+                        d = float(np.abs(rd.T_W_B - ro.T_W_B).max())
+                        maxd = max(maxd, d)
+                        if first is None and (rd.is_keyframe != ro.is_keyframe or d > 1e-6 or
+                                              (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)):
+                            first = k
+                    k += 1
+            finally:
+                O.set_ba_threads(1)
+            cel = time.perf_counter() - t0
+            return k, cel, oerr, first, maxd, ob
+
+        k, cel, oerr, first, maxd, ob = oracle_leg(1, cpu_seconds, True)
         gerr_k = max(float(np.linalg.norm(r.T_W_B[:3, 3] - T[:3, 3])) for r, T in zip(out[:k], s.T_W_B[:k]))
         row["oracle_max_position_error_m"] = round(oerr, 5)
         row["oracle_frames"] = k
         row["gpu_max_position_error_m_same_frames"] = round(gerr_k, 5)
-        row["cpu_baseline"] = {"value": round(k / cel, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"the first {k} frames of the same stream through the same Estimator "
-                                         "host logic over the oracle (oracle/estimator.py), 1 thread",
-                               "stage_ms_per_frame": {kk: round(1e3 * v / k, 3) for kk, v in ob.t.items()}}
+        row["first_divergent_frame"] = first
+        row["max_pose_diff_vs_oracle"] = maxd
+        single = {"value": round(k / cel, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                  "sample": f"the first {k} frames of the same stream through the same Estimator "
+                            "host logic over the oracle (oracle/estimator.py), 1 thread",
+                  "stage_ms_per_frame": {kk: round(1e3 * v / k, 3) for kk, v in ob.t.items()}}
+        nt = host_cores()
+        k2, cel2, _, _, _, ob2 = oracle_leg(nt, min(cpu_seconds / 2, 20.0), False)
+        row["cpu_baseline"] = {"value": round(k2 / cel2, 3), "unit": "frames/s", "cores": nt, "kind": "port",
+                               "sample": f"the first {k2} frames through the oracle backend with {nt} threads "
+                                         "(tracker levels / features and the Schur BA threaded)",
+                               "stage_ms_per_frame": {kk: round(1e3 * v / k2, 3) for kk, v in ob2.t.items()},
+                               "single_thread": single}
     return row
 
 
@@ -900,7 +937,7 @@ def cpu_baseline(frames_budget_s: float, threads: int = 1):
     """The oracle (C++ restatement of the reference) on the host: same tracker frame + BA solve.
     threads > 1 mirrors the reference's rayon parallelism: per-level pyramids
     (feature_tracker.rs:213) and per-feature track_points (:260) over `threads` threads; the BA
-    solve stays single-threaded like apex's per-block loop."""
+    solve runs the threaded Schur variant (landmark ranges in parallel) on the all-cores leg."""
     from oracle import oracle as O
     from rsvio import synthetic as S
     frames = list(S.stereo_sequence(2, W, H))
@@ -919,7 +956,11 @@ def cpu_baseline(frames_budget_s: float, threads: int = 1):
         O.track_points(pyr_prev[1], pc[1], W, H, LEVELS, aff1, MAX_IT, THRESH, threads)
         O.track_points(pc[0], pc[1], W, H, LEVELS, affn, MAX_IT, THRESH, threads)
         t1 = time.perf_counter()
-        _, _, r = O.ba_solve(prob)
+        O.set_ba_threads(threads)   # the threaded Schur variant on the all-cores leg
+        try:
+            _, _, r = O.ba_solve(prob)
+        finally:
+            O.set_ba_threads(1)
         t2 = time.perf_counter()
         t_track += t1 - t0
         t_ba += t2 - t1
@@ -929,7 +970,7 @@ def cpu_baseline(frames_budget_s: float, threads: int = 1):
             "sample": f"{n} frames of config 2 (2 pyramids + 3x300 track_points) each followed by one config-3 "
                       f"BA solve ({r.iterations} LM iterations), oracle/ C++ restatement, "
                       + ("1 thread" if threads == 1 else
-                         f"{threads} threads (pyramid levels and features in parallel, BA 1 thread)"),
+                         f"{threads} threads (pyramid levels and features in parallel, threaded Schur BA)"),
             "tracker_ms_per_frame": round(1e3 * t_track / n, 3), "ba_ms_per_solve": round(1e3 * t_ba / n, 3),
             "ba_ms_per_iter": round(1e3 * t_ba / n / max(r.iterations, 1), 3)}
 

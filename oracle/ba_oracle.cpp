@@ -17,6 +17,7 @@
 #include <limits>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -186,7 +187,43 @@ struct System {
     bool ok;
 };
 
+// Threads of the BA restatement (orc_set_ba_threads; 1 = the sequential reference order).  With
+// T > 1 the landmarks are split into T contiguous ranges whose sums (S, b, g_c, U, cost, the
+// step norms) are combined in range order -- the "threaded Schur variant" CPU leg of BASELINE.md;
+// deterministic for a given T, tolerance-equal to T = 1.
+int g_ba_threads = 1;
+
+template <class F>
+void for_ranges(int n, int T, F&& f) {  // f(range index, begin, end) over T contiguous ranges
+    if (T <= 1 || n < 2 * T) {
+        f(0, 0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) pool.emplace_back([&, t] { f(t, (int)((long long)n * t / T), (int)((long long)n * (t + 1) / T)); });
+    for (auto& th : pool) th.join();
+}
+
 double eval_cost(const Problem& pr, const std::vector<Pose>& poses, const double* pW) {
+    if (g_ba_threads > 1) {
+        std::vector<double> part(g_ba_threads, 0.0);
+        for_ranges(pr.n_lm, g_ba_threads, [&](int t, int l0, int l1) {
+            double c = 0.0;
+            for (int l = l0; l < l1; ++l)
+                for (int q = pr.lm_ptr[l]; q < pr.lm_ptr[l + 1]; ++q) {
+                    int o = pr.order[q];
+                    double r[2], J[2][9];
+                    linearize(pW + 3 * l, poses[pr.obs_kf[o]], pr.TCB2 + 16 * pr.obs_cam[o], pr.obs_uv + 2 * o, r, J);
+                    double s = r[0] * r[0] + r[1] * r[1], rho, w;
+                    huber(s, pr.delta, &rho, &w);
+                    c += 0.5 * rho;
+                }
+            part[t] = c;
+        });
+        double cost = 0.0;
+        for (double c : part) cost += c;
+        return cost;
+    }
     double cost = 0.0;
     for (int l = 0; l < pr.n_lm; ++l) {
         for (int q = pr.lm_ptr[l]; q < pr.lm_ptr[l + 1]; ++q) {
@@ -201,20 +238,13 @@ double eval_cost(const Problem& pr, const std::vector<Pose>& poses, const double
     return cost;
 }
 
-System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW, double lambda) {
-    System sy;
-    int n = 6 * pr.n_free;
-    sy.n = n;
-    sy.S.assign((size_t)n * n, 0.0);
-    sy.b.assign(n, 0.0);
-    sy.gc.assign(n, 0.0);
-    sy.lms.resize(pr.n_lm);
-    sy.cost = 0.0;
-    sy.ok = true;
-    std::vector<double> U((size_t)pr.n_free * 36, 0.0);
-    for (int l = 0; l < pr.n_lm; ++l) {
+// landmarks [l0, l1) into sy's S, b, g_c, cost and U (the per-landmark blocks into lms)
+void build_range(const Problem& pr, const std::vector<Pose>& poses, const double* pW, double lambda, int l0, int l1,
+                 System& sy, std::vector<double>& U, std::vector<LmBlock>& lms) {
+    const int n = sy.n;
+    for (int l = l0; l < l1; ++l) {
         double V[3][3] = {{0}}, gp[3] = {0, 0, 0};
-        LmBlock& B = sy.lms[l];
+        LmBlock& B = lms[l];
         B.W.clear();
         for (int q = pr.lm_ptr[l]; q < pr.lm_ptr[l + 1]; ++q) {
             int o = pr.order[q];
@@ -253,7 +283,7 @@ System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW
         }
         for (int a = 0; a < 3; ++a) B.gp[a] = gp[a];
         // Y_k = W_k Vi ; S_kk' -= Y_k W_k'^T ; b_k += Y_k gp
-        std::vector<std::array<double, 18>> Y(B.W.size());
+        std::array<double, 18> Y[64];  // <= 64 keyframes per landmark (the device's limit too)
         for (size_t i = 0; i < B.W.size(); ++i)
             for (int a = 0; a < 6; ++a)
                 for (int c = 0; c < 3; ++c) {
@@ -273,6 +303,46 @@ System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW
             }
             for (int a = 0; a < 6; ++a)
                 sy.b[6 * ki + a] += (Y[i][a * 3 + 0] * gp[0] + Y[i][a * 3 + 1] * gp[1]) + Y[i][a * 3 + 2] * gp[2];
+        }
+    }
+}
+
+System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW, double lambda) {
+    System sy;
+    int n = 6 * pr.n_free;
+    sy.n = n;
+    sy.S.assign((size_t)n * n, 0.0);
+    sy.b.assign(n, 0.0);
+    sy.gc.assign(n, 0.0);
+    sy.lms.resize(pr.n_lm);
+    sy.cost = 0.0;
+    sy.ok = true;
+    std::vector<double> U((size_t)pr.n_free * 36, 0.0);
+    const int T = g_ba_threads;
+    if (T <= 1 || pr.n_lm < 2 * T) {
+        build_range(pr, poses, pW, lambda, 0, pr.n_lm, sy, U, sy.lms);
+    } else {
+        std::vector<System> part(T);
+        std::vector<std::vector<double>> Up(T);
+        for (int t = 0; t < T; ++t) {
+            part[t].n = n;
+            part[t].S.assign((size_t)n * n, 0.0);
+            part[t].b.assign(n, 0.0);
+            part[t].gc.assign(n, 0.0);
+            part[t].cost = 0.0;
+            part[t].ok = true;
+            Up[t].assign((size_t)pr.n_free * 36, 0.0);
+        }
+        for_ranges(pr.n_lm, T, [&](int t, int l0, int l1) { build_range(pr, poses, pW, lambda, l0, l1, part[t], Up[t], sy.lms); });
+        for (int t = 0; t < T; ++t) {  // range order
+            for (size_t i = 0; i < sy.S.size(); ++i) sy.S[i] += part[t].S[i];
+            for (int i = 0; i < n; ++i) {
+                sy.b[i] += part[t].b[i];
+                sy.gc[i] += part[t].gc[i];
+            }
+            for (size_t i = 0; i < U.size(); ++i) U[i] += Up[t][i];
+            sy.cost += part[t].cost;
+            sy.ok = sy.ok && part[t].ok;
         }
     }
     for (int f = 0; f < pr.n_free; ++f)
@@ -539,6 +609,8 @@ int orc_ba_build_system(int n_kf, const double* pose7, const uint8_t* kf_fixed, 
     return sy.ok ? 0 : -1;
 }
 
+void orc_set_ba_threads(int threads) { g_ba_threads = threads < 1 ? 1 : threads; }
+
 int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, double* p_W, int n_obs,
                  const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam,
                  const double* obs_uv, const double* TCB2, const orc_lm_cfg* cfg, orc_ba_result* res) {
@@ -602,22 +674,41 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
             dx2 += dc[f] * dc[f];
             gdx += sy.gc[f] * dc[f];
         }
-        for (int l = 0; l < n_lm; ++l) {
-            const LmBlock& B = sy.lms[l];
-            double rhs[3] = {-B.gp[0], -B.gp[1], -B.gp[2]};
-            for (const auto& wk : B.W) {
-                const double* d6 = &dc[6 * wk.first];
-                for (int c = 0; c < 3; ++c) {
-                    double s = 0.0;
-                    for (int a = 0; a < 6; ++a) s += wk.second[a * 3 + c] * d6[a];
-                    rhs[c] -= s;
+        {
+            const int T = std::max(g_ba_threads, 1);
+            std::vector<double> pdx(T, 0.0), pgd(T, 0.0);
+            for_ranges(n_lm, T, [&](int t, int l0, int l1) {
+                double d2 = 0.0, gd = 0.0;
+                for (int l = l0; l < l1; ++l) {
+                    const LmBlock& B = sy.lms[l];
+                    double rhs[3] = {-B.gp[0], -B.gp[1], -B.gp[2]};
+                    for (const auto& wk : B.W) {
+                        const double* d6 = &dc[6 * wk.first];
+                        for (int c = 0; c < 3; ++c) {
+                            double s = 0.0;
+                            for (int a = 0; a < 6; ++a) s += wk.second[a * 3 + c] * d6[a];
+                            rhs[c] -= s;
+                        }
+                    }
+                    for (int c = 0; c < 3; ++c) {
+                        dp[3 * l + c] = (B.Vi[c][0] * rhs[0] + B.Vi[c][1] * rhs[1]) + B.Vi[c][2] * rhs[2];
+                        if (T == 1) {  // the sequential reference order
+                            dx2 += dp[3 * l + c] * dp[3 * l + c];
+                            gdx += B.gp[c] * dp[3 * l + c];
+                        } else {
+                            d2 += dp[3 * l + c] * dp[3 * l + c];
+                            gd += B.gp[c] * dp[3 * l + c];
+                        }
+                    }
                 }
-            }
-            for (int c = 0; c < 3; ++c) {
-                dp[3 * l + c] = (B.Vi[c][0] * rhs[0] + B.Vi[c][1] * rhs[1]) + B.Vi[c][2] * rhs[2];
-                dx2 += dp[3 * l + c] * dp[3 * l + c];
-                gdx += B.gp[c] * dp[3 * l + c];
-            }
+                pdx[t] = d2;
+                pgd[t] = gd;
+            });
+            if (T > 1)
+                for (int t = 0; t < T; ++t) {
+                    dx2 += pdx[t];
+                    gdx += pgd[t];
+                }
         }
         }
         for (int k = 0; k < n_kf; ++k)

@@ -35,9 +35,12 @@ class OracleSolver:
 
 class OracleBackend:
     def __init__(self, oracle, width, height, cameras, levels=6, grid_size=50, max_iterations=20, thresh=0.01,
-                 translation_threshold=0.05, rotation_threshold=0.05):
+                 translation_threshold=0.05, rotation_threshold=0.05, threads=1):
+        """threads > 1: the all-cores CPU leg -- the tracker's pyramid levels and features in
+        parallel (rayon's par_iter) and the threaded Schur BA (oracle.set_ba_threads, a process-wide
+        setting the caller restores)."""
         self.o = oracle
-        self.tracker = oracle.StereoTracker(width, height, levels, grid_size, max_iterations, thresh)
+        self.tracker = oracle.StereoTracker(width, height, levels, grid_size, max_iterations, thresh, threads=threads)
         self.cams = [oracle.camera(c.model, c.params, CONVENTIONS[c.convention], c.max_iterations) for c in cameras]
         self.thr = (translation_threshold, rotation_threshold)
         self.solver = OracleSolver(oracle)

@@ -67,6 +67,7 @@ _SIG = {
                                    C.c_double, C.c_double, C.POINTER(OrcMotionResult)]),
     "orc_unproject": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
     "orc_project": (C.c_int, [C.POINTER(OrcCamera), P, C.c_size_t, P, P]),
+    "orc_set_ba_threads": (None, [C.c_int]),
     "orc_libm_sincosf_digest": (None, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, P]),
     "orc_se2_exp": (None, [P, P]),
     "orc_pyramid_offset": (C.c_size_t, [C.c_int, C.c_int, C.c_int]),
@@ -81,6 +82,7 @@ _SIG = {
     "orc_detect_keypoints": (C.c_int, [P, C.c_int, C.c_int, C.c_int, P, C.c_int, P, P, C.c_int]),
     "orc_tracker_create": (P, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float]),
     "orc_tracker_destroy": (None, [P]),
+    "orc_tracker_set_threads": (None, [P, C.c_int]),
     "orc_tracker_process_frame": (C.c_int, [P, P, P, P, C.c_int, C.POINTER(C.c_int), P, C.c_int,
                                             C.POINTER(C.c_int)]),
     "orc_tracker_remove_ids": (None, [P, P, C.c_int]),
@@ -200,8 +202,10 @@ def detect_key_points(img, grid, existing_xy=None, cap=4096):
 
 
 class StereoTracker:
-    def __init__(self, w, h, levels=6, grid=50, max_iter=20, thresh=0.01, cap=4096):
+    def __init__(self, w, h, levels=6, grid=50, max_iter=20, thresh=0.01, cap=4096, threads=1):
         self.h = load().orc_tracker_create(w, h, levels, grid, max_iter, C.c_float(thresh))
+        if threads > 1:  # the all-cores CPU leg: pyramid levels and features in parallel (rayon)
+            load().orc_tracker_set_threads(self.h, threads)
         self.cap = cap
         self.ol = (OrcFeature * cap)()
         self.orr = (OrcFeature * cap)()
@@ -274,6 +278,11 @@ def lm_cfg(max_iterations=20, cost_tolerance=1e-6, parameter_tolerance=1e-9, hub
            linear_solver=0):
     """linear_solver 0: SparseSchurComplement; 1: the SparseCholesky fallback (dense full system here)."""
     return LmCfg(max_iterations, cost_tolerance, parameter_tolerance, huber_delta, lambda_init, linear_solver)
+
+
+def set_ba_threads(threads: int):
+    """Threads of the BA restatement (1: the sequential reference order)."""
+    load().orc_set_ba_threads(int(threads))
 
 
 def ba_solve(prob, cfg=None):

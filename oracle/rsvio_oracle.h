@@ -90,6 +90,7 @@ typedef struct {
 } orc_feature;
 orc_tracker* orc_tracker_create(int w, int h, int levels, int grid, int max_iter, float thresh);
 void orc_tracker_destroy(orc_tracker* t);
+void orc_tracker_set_threads(orc_tracker* t, int threads);  /* all-cores CPU leg; 1 = sequential */
 /* returns 0; fills up to cap features per camera, counts in n_l/n_r */
 int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t* right,
                               orc_feature* out_l, int cap_l, int* n_l,
@@ -200,6 +201,9 @@ int orc_ba_build_system(int n_kf, const double* pose7, const uint8_t* kf_fixed,
                         double huber_delta, double lambda, double* S, double* b, double* cost);
 
 /* Full LM solve (build's restatement of apex-solver LM with Schur elimination). */
+/* threads of the BA restatement (1 = sequential reference order; T > 1: T contiguous landmark
+ * ranges summed in range order -- the threaded-Schur CPU baseline leg) */
+void orc_set_ba_threads(int threads);
 int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed,
                  int n_lm, double* p_W,
                  int n_obs, const int32_t* obs_lm, const int32_t* obs_kf,

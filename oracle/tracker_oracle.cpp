@@ -752,6 +752,7 @@ struct orc_tracker {
     std::vector<orc_feature> map0, map1;
     std::vector<uint8_t> prev0, prev1;
     bool has_prev = false;
+    int threads = 1;  // rayon analogue: pyramid levels and features in parallel (all-cores CPU leg)
 };
 
 orc_tracker* orc_tracker_create(int w, int h, int levels, int grid, int max_iter, float thresh) {
@@ -761,6 +762,7 @@ orc_tracker* orc_tracker_create(int w, int h, int levels, int grid, int max_iter
     return t;
 }
 void orc_tracker_destroy(orc_tracker* t) { delete t; }
+void orc_tracker_set_threads(orc_tracker* t, int threads) { t->threads = threads < 1 ? 1 : threads; }
 
 static void track_map(const orc_tracker* t, const uint8_t* pa, const uint8_t* pb,
                       std::vector<orc_feature>& m) {
@@ -769,7 +771,7 @@ static void track_map(const orc_tracker* t, const uint8_t* pa, const uint8_t* pb
     std::vector<uint8_t> v(n);
     for (int i = 0; i < n; ++i) memcpy(&ain[6 * i], m[i].aff, 24);
     orc_track_points(pa, pb, t->w, t->h, t->levels, ain.data(), n, t->max_iter, t->thresh,
-                     aout.data(), v.data(), 1);
+                     aout.data(), v.data(), t->threads);
     std::vector<orc_feature> out;
     for (int i = 0; i < n; ++i)
         if (v[i]) {
@@ -787,8 +789,8 @@ int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t
                               int cap_r, int* n_r) {
     size_t pb = orc_pyramid_bytes(t->w, t->h, t->levels);
     std::vector<uint8_t> cur0(pb), cur1(pb);
-    orc_build_pyramid(left, t->w, t->h, t->levels, cur0.data());
-    orc_build_pyramid(right, t->w, t->h, t->levels, cur1.data());
+    orc_build_pyramid_mt(left, t->w, t->h, t->levels, cur0.data(), t->threads);
+    orc_build_pyramid_mt(right, t->w, t->h, t->levels, cur1.data(), t->threads);
     if (t->has_prev) {
         track_map(t, t->prev0.data(), cur0.data(), t->map0);
         track_map(t, t->prev1.data(), cur1.data(), t->map1);
@@ -814,7 +816,7 @@ int orc_tracker_process_frame(orc_tracker* t, const uint8_t* left, const uint8_t
         a[5] = (float)pts[i].y;
     }
     orc_track_points(cur0.data(), cur1.data(), t->w, t->h, t->levels, a0.data(), m, t->max_iter,
-                     t->thresh, a1.data(), v.data(), 1);
+                     t->thresh, a1.data(), v.data(), t->threads);
     // feature_tracker.rs:162-170, canonical order = ascending detection index
     for (int i = 0; i < m; ++i) {
         if (!v[i]) continue;

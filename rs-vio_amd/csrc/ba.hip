@@ -1227,6 +1227,273 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve(Geometry G, Prob P
 }
 
 // ---------------------------------------------------------------------------------------
+// K5 on the matrix cores (n <= 60; RSVIO_K5=mfma): blocked right-looking
+// LDL^T of the camera system with 16-column panels.  The system (padded to NPP = 16 ceil(n/16)
+// with identity rows / columns, which couple to nothing) sits column-major in LDS.  Per panel:
+//   * wave 0 (lane = row) factors the panel's columns in registers -- per pivot K the 1/d_K
+//     chain (v_rcp_f64 + the folded Newton step), l = u / d_K, the in-panel updates from
+//     readlanes of the unscaled column, and b_i -= l_iK b_K (so b ends as L^-1 b) -- and writes
+//     L into the panel's columns of M, U = D L into Up;
+//   * every wave then updates its share of the trailing lower tiles (I, J > panel) with
+//     v_mfma_f64_16x16x4_f64: C_IJ += (-U_I) L_J^T over the panel's 16 columns (4 MFMAs per
+//     tile, accumulator in registers, C loaded from / stored to M).
+// The serial chain is the pivots inside the panels; the O(n^3) trailing work runs on the matrix
+// cores, off wave 0's chain.  z = D^-1 L^-1 b, then L^T x = z by wave 0 (readlanes, as pipe4).
+// Tolerance parity like pipe4 (same pivots; the trailing sums reassociated by the MFMA).
+// ---------------------------------------------------------------------------------------
+typedef double mf_dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kMfLd = 65;  // f64 leading dimension of M and Up (odd: column reads spread banks)
+
+template <int NF>
+struct MfDims {
+    static constexpr int NP = 6 * NF;
+    static constexpr int NT = (NP + 15) / 16;
+    static constexpr int NPP = 16 * NT;
+};
+
+// pivot J of panel PK (width PW) by wave 0: inv = 1 / d_K ready.  Column J+1 (the next pivot's)
+// and column J+2 are updated from readlanes of the unscaled column u; columns >= J+3 from LDS
+// broadcasts of u issued this step and consumed one step later (uq, with the pivot's l as lp), so
+// neither the readlane issue cost nor the LDS latency sits on the 1/d chain.
+template <int PK, int J, int PW>
+__device__ __forceinline__ void mf_pivot(double (&a)[16], double (&uq)[16], double lp, double& b, double& myinv,
+                                         double inv, double* M, double* Up, int lane, bool& bad) {
+    constexpr int K = 16 * PK + J;
+    const double u = a[J];
+    const double l = u * inv;
+    double inv_next = 1.0;
+    if constexpr (J + 1 < PW) {  // the next pivot first: its 1/d chain overlaps the rest
+        a[J + 1] = fma(-l, rl64(u, K + 1), a[J + 1]);
+        const double piv = rl64(a[J + 1], K + 1);
+        bad |= !(piv > 0.0) || !isfinite(piv);
+        inv_next = rcp_f64(piv);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the previous pivot's deferred updates (columns >= J+2), then this pivot's column J+2
+    if constexpr (J > 0)
+#pragma unroll
+        for (int jj = J + 2; jj < PW; ++jj) a[jj] = fma(-lp, uq[jj], a[jj]);
+    if constexpr (J + 2 < PW) a[J + 2] = fma(-l, rl64(u, K + 2), a[J + 2]);
+    M[K * kMfLd + lane] = l;   // column K of L (rows > K; the upper part is never read)
+    Up[J * kMfLd + lane] = u;  // column J of the panel's U = D L
+#pragma unroll
+    for (int jj = J + 3; jj < PW; ++jj) uq[jj] = Up[J * kMfLd + 16 * PK + jj];  // broadcasts
+    const double bK = rl64(b, K);
+    myinv = lane == K ? inv : myinv;
+    b = lane > K ? fma(-l, bK, b) : b;
+    if constexpr (J + 1 < PW) mf_pivot<PK, J + 1, PW>(a, uq, l, b, myinv, inv_next, M, Up, lane, bad);
+}
+
+template <int NF, int PK>
+__device__ __forceinline__ void mf_panel(double* M, double* Up, int tid, double& b, double& myinv, bool& bad) {
+    constexpr int NP = MfDims<NF>::NP, NT = MfDims<NF>::NT;
+    constexpr int PW = (NP - 16 * PK) < 16 ? (NP - 16 * PK) : 16;
+    const int lane = tid & 63, wave = tid >> 6;
+    if (wave == 0) {
+        double a[16], uq[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            a[jj] = jj < PW ? M[(16 * PK + jj) * kMfLd + lane] : 0.0;
+            uq[jj] = 0.0;
+        }
+        const double piv = rl64(a[0], 16 * PK);
+        bad |= !(piv > 0.0) || !isfinite(piv);
+        mf_pivot<PK, 0, PW>(a, uq, 0.0, b, myinv, rcp_f64(piv), M, Up, lane, bad);
+    }
+    // diagnostic stamps (stamps build): panel PK factored (9, 15, 30 / 7 for the last)
+    if constexpr (PK == 0) STAMP(9); else if constexpr (PK == 1) STAMP(15); else if constexpr (PK == 2) STAMP(30);
+    if constexpr (PK + 1 == NT) STAMP(7);
+    if constexpr (PK + 1 < NT) {
+        __syncthreads();
+        // trailing lower tiles (I, J), PK < J <= I < NT; wave 0 (the panel's) takes the fewest
+        constexpr int R = NT - 1 - PK;  // tile rows / columns left
+        constexpr int NTILE = R * (R + 1) / 2;
+        const int i16 = lane & 15, k4 = lane >> 4;
+        for (int t = 3 - wave; t < NTILE; t += 4) {
+            int J = 0, rem = t;
+            while (rem >= R - J) {
+                rem -= R - J;
+                ++J;
+            }
+            const int TJ = PK + 1 + J, TI = TJ + rem;
+            double av[4], bv[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int kk = 4 * m + k4;
+                av[m] = -Up[kk * kMfLd + 16 * TI + i16];
+                bv[m] = M[(16 * PK + kk) * kMfLd + 16 * TJ + i16];
+            }
+            mf_dbl4 c0, c1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c0[r] = M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r];
+            // two independent accumulation chains (columns 0-7 and 8-15 of the panel)
+            c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], c1, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], c1, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r] = c0[r] + c1[r];
+        }
+        __syncthreads();
+        if constexpr (PK == 0) STAMP(13); else if constexpr (PK == 1) STAMP(19); else if constexpr (PK == 2) STAMP(31);
+        mf_panel<NF, PK + 1>(M, Up, tid, b, myinv, bad);
+    }
+}
+
+// The reduced system straight into the dense column-major lower triangle M (single rank):
+// combine_system's sums (8 partial systems in slot order, + lambda on the diagonal after the sum)
+// scattered to M[col][row], row >= col; b and g_c into bsh / gsh; M's other entries zero, the
+// padding diagonal one (written while the partial systems' loads are in flight).
+template <int NF>
+__device__ void combine_dense(const Geometry& G, const Work& Wk, double* M, double* bsh, double* gsh, double lambda,
+                              int* fail) {
+    constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
+    constexpr int NPB = NF * (NF + 1) / 2;
+    constexpr int SB0 = NPB * 36, SG0 = SB0 + 6 * NF, NE = SG0 + 6 * NF;
+    constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
+    const size_t L = sys_len(G);
+    const int tid = threadIdx.x;
+    double pa[16];
+    int sing = 0;
+    if (tid < 64) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pa[k] = tid + 64 * k < G.n_wave ? Wk.partA[(tid + 64 * k) * kPartA] : 0.0;
+        sing = *Wk.singular;
+    }
+    double v[kE][kGrp];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+#pragma unroll
+        for (int x = 0; x < kGrp; ++x) v[i][x] = e < NE ? Wk.cpart[(size_t)x * L + e] : 0.0;
+    }
+    for (int e = tid; e < NPP * kMfLd; e += T) {
+        const int c = e / kMfLd, r = e - c * kMfLd;
+        M[e] = (r == c && r >= NP) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= NE) break;
+        double a = v[i][0];
+#pragma unroll
+        for (int x = 1; x < kGrp; ++x) a += v[i][x];
+        if (e < SB0) {
+            const int pb = e / 36, k = e - 36 * pb, ra = k / 6, ca = k - 6 * ra;
+            int fa = 0, rem = pb;
+            while (rem >= NF - fa) {
+                rem -= NF - fa;
+                ++fa;
+            }
+            const int fb = fa + rem;
+            if (fa == fb) {
+                if (ra == ca) a += lambda;
+                if (ra >= ca) M[(6 * fa + ca) * kMfLd + 6 * fa + ra] = a;
+            } else {
+                M[(6 * fa + ra) * kMfLd + 6 * fb + ca] = a;
+            }
+        } else if (e < SG0) {
+            bsh[e - SB0] = a;
+        } else {
+            gsh[e - SG0] = a;
+        }
+    }
+    if (tid < 64) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+        c = wave_sum_det(c);
+        if (tid == 0) {
+            Wk.sys[G.n_pb * 36 + 12 * G.n_free] = c;  // the decision of iteration 0 reads the initial cost here
+            *fail = sing;
+        }
+    }
+}
+
+template <int NF>
+__global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, Prob Pr, Work Wk, int combine) {
+    static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
+    constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
+    __shared__ __attribute__((aligned(16))) double M[NPP * kMfLd];
+    __shared__ __attribute__((aligned(16))) double Up[16 * kMfLd];
+    __shared__ double bsh[NP], gsh[NP];
+    __shared__ int fail;
+    RTSTAMP(4);
+    LmState* st = Wk.st;
+    if (st->done) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nF = G.n_free, n = 6 * nF;
+    const int SC0 = G.n_pb * 36 + 12 * nF;
+    const int cur = st->cur;
+    double p7[7] = {0, 0, 0, 1, 0, 0, 0};
+    int fidx = -1;
+    if (wave == 0 && lane < G.n_kf) {
+        fidx = Pr.free_idx[lane];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
+    }
+    STAMP(0);
+    if (combine) {
+        combine_dense<NF>(G, Wk, M, bsh, gsh, st->lambda, &fail);
+    } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys
+        const double* sys = Wk.sys;
+        for (int e = tid; e < NPP * kMfLd; e += kK5Threads) {
+            const int c = e / kMfLd, r = e - c * kMfLd;
+            double v = 0.0;
+            if (r < NP && c < NP) {
+                if (r >= c) v = *sys_lower<NF>(sys, r, c);
+            } else if (r == c) {
+                v = 1.0;
+            }
+            M[e] = v;
+        }
+        if (tid < NP) {
+            bsh[tid] = *sys_lower<NF>(sys, NP, tid);
+            gsh[tid] = sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + tid];
+        }
+        if (tid == 0) fail = sys[SC0 + 1] != 0.0;
+    }
+    __syncthreads();
+    STAMP(1);
+    if (tid == 0) {
+        fail |= *Wk.singular;
+        *Wk.singular = 0;
+    }
+    const double gcl_v = (wave == 0 && lane < n) ? gsh[lane] : 0.0;
+    double b = (wave == 0 && lane < NP) ? bsh[lane] : 0.0;
+    __syncthreads();
+    STAMP(2);
+    if (fail) {
+        if (tid == 0) k5_result(st, 0, 0.0, 0.0);
+        return;
+    }
+    double myinv = 0.0;
+    bool bad = false;
+    mf_panel<NF, 0>(M, Up, tid, b, myinv, bad);
+    if (wave != 0) return;
+    if (bad) {
+        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
+        return;
+    }
+    // z = D^-1 L^-1 b; L^T x = z (unit diagonal): lane j, L[i][j] = M[j][i] column-major, zero
+    // for i <= j so the update needs no select
+    double yv = lane < NP ? b * myinv : 0.0;
+    double lt[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const double m = M[(lane < NP ? lane : 0) * kMfLd + j];
+        lt[j] = lane < j ? m : 0.0;
+    }
+#pragma unroll
+    for (int j = NP - 1; j >= 0; --j) yv = fma(-lt[j], rl64(yv, j), yv);
+    STAMP(3);
+    k5_finish<NF>(G, Wk, Up, lane < n ? yv : 0.0, gcl_v, n, lane, p7, fidx);
+    RTSTAMP(5);
+}
+
+// ---------------------------------------------------------------------------------------
 // K5 for 11..20 free keyframes (61 <= n <= 120): the pipelined register LDL^T with two rows per
 // lane (rows lane and lane + 64) over 8 waves.  The system is padded to NP = 6 NF (NF in
 // {13, 16, 20}) with identity rows / columns after the real ones and b as row NP: a padded
@@ -1799,7 +2066,8 @@ struct BundleAdjuster {
     int g_k = -1;
     rsvio_lm_cfg g_cfg{};
     bool graphs_ok = true;
-    int k5_variant = 0;  // camera solve for n_free <= 10: 0 pipelined 4-wave LDL^T, 1 one-wave Gauss-Jordan
+    int k5_variant = 0;  // camera solve for n_free <= 10: 0 pipelined 4-wave LDL^T, 1 one-wave Gauss-Jordan,
+                         // 2 blocked LDL^T with MFMA trailing updates
     // an exec whose launch may still run is never destroyed: the stream settles first (a ticket
     // wait returns before the last decision kernel has exited)
     void drop_graph() {
@@ -1865,6 +2133,7 @@ struct BundleAdjuster {
     struct ArenaLayout {
         size_t pose_init, pw_init, free_idx, hdr, uv, pairs, pb_fa, pb_fb, total;
     } lay{};
+    bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
     bool state_fresh = false;  // set_problem without a run since: get_state resets the buffers first
     // host scratch of set_problem, kept across problems (no per-problem allocations)
     std::vector<int> hs_free, hs_cnt, hs_order, hs_slot_kf, hs_slot_lm, hs_slot_obs, hs_lm_slot, hs_wave_slot,
@@ -1916,9 +2185,11 @@ struct BundleAdjuster {
         tick_wait = !(wv && std::strcmp(wv, "sync") == 0);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
+        prof_env = std::getenv("RSVIO_BA_PROFILE") != nullptr;
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
+        if (kv && std::strcmp(kv, "mfma") == 0) k5_variant = 2;
     }
     ~BundleAdjuster() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -1982,7 +2253,19 @@ struct BundleAdjuster {
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
+        const bool prof = prof_env;
+        auto tp0 = std::chrono::steady_clock::now();
+        double tms[12];
+        int ntm = 0;
+        auto mark = [&] {
+            if (!prof) return;
+            const auto t = std::chrono::steady_clock::now();
+            tms[ntm++] = std::chrono::duration<double, std::micro>(t - tp0).count();
+            tp0 = t;
+        };
         require_idle("set_problem");
+        mark();
+        mark();
         drop_graph();  // kernel arguments (sizes, buffers) change with the problem
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
@@ -2024,6 +2307,7 @@ struct BundleAdjuster {
                 order[r] = o;
             }
         }
+        mark();
         // slots: (landmark, keyframe) runs of 1-2 observations
         auto &slot_kf = hs_slot_kf, &slot_lm = hs_slot_lm, &slot_obs = hs_slot_obs, &lm_slot = hs_lm_slot;
         slot_kf.clear();
@@ -2055,6 +2339,7 @@ struct BundleAdjuster {
         for (int sl = 0; sl < n_slot; ++sl)
             if (slot_obs[sl + 1] - slot_obs[sl] > 2)
                 throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
+        mark();
         // camera blocks (fa <= fb)
         auto &pb_fa = hs_pb_fa, &pb_fb = hs_pb_fb, &pb_of = hs_pb_of;
         pb_fa.clear();
@@ -2095,6 +2380,7 @@ struct BundleAdjuster {
         int stride = 1;
         for (int c : pcnt) stride = std::max(stride, c);
         n_pad = (size_t)64 * n_wave;
+        mark();
         // arena layout
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         ArenaLayout L{};
@@ -2115,6 +2401,7 @@ struct BundleAdjuster {
         if (h_arena.n < L.total) h_arena.alloc(L.total + L.total / 4);
         if (d_arena.n < L.total) d_arena.alloc(L.total + L.total / 4);
         lay = L;
+        mark();
         uint8_t* hb = h_arena.p;
         std::memcpy(hb + L.pose_init, pose7, sizeof(double) * 7 * (size_t)n_kf);
         if (n_lm) std::memcpy(hb + L.pw_init, pW, sizeof(double) * 3 * (size_t)n_lm);
@@ -2144,6 +2431,7 @@ struct BundleAdjuster {
                     huv[4 * ps + 2 * q + 1] = obs_uv[2 * (size_t)o + 1];
                 }
             }
+        mark();
         {  // pairs: {slot a, slot b, landmark, 0} at a fixed stride per chunk, padding a = -1
             int4* pq = reinterpret_cast<int4*>(hb + L.pairs);
             for (size_t i = 0; i < (size_t)n_chunk * stride; ++i) pq[i] = make_int4(-1, 0, 0, 0);
@@ -2162,9 +2450,11 @@ struct BundleAdjuster {
         }
         std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
+        mark();
         RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.total, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
+        mark();
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
@@ -2188,9 +2478,15 @@ struct BundleAdjuster {
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
         grow(d_state, 2);
+        mark();
         *h_state.p = LmState{};  // cur = 0: buffer 0 holds the initial state once it is set
         state_fresh = true;
         has_problem = true;
+        mark();
+        if (prof)
+            fprintf(stderr, "[rsvio] set_problem us: idle %.1f - %.1f drop+sort %.1f slots+waves %.1f pairs-count %.1f "
+                    "layout+wait+alloc %.1f hdr %.1f pairs %.1f upload %.1f grow %.1f tail %.1f (bytes %zu)\n",
+                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], tms[6], tms[7], tms[8], tms[9], tms[10], L.total);
     }
 
     void allreduce(double* buf, size_t n) {
@@ -2244,6 +2540,18 @@ struct BundleAdjuster {
     // the reduced system is summed from the chunk partials in K5's prologue (single rank)
     void launch_camera_solve(const Prob& pr, const Work& wk, int combine) {
         const dim3 g(1), b(kK5Threads);
+        if (k5_variant == 2 && G.n_free <= 10) {
+            switch (G.n_free) {
+#define RSVIO_CAMM(NF) \
+    case NF: hipLaunchKernelGGL(ba_camera_solve_mfma<NF>, g, b, 0, stream, G, pr, wk, combine); break;
+                RSVIO_CAMM(1) RSVIO_CAMM(2) RSVIO_CAMM(3) RSVIO_CAMM(4) RSVIO_CAMM(5)
+                RSVIO_CAMM(6) RSVIO_CAMM(7) RSVIO_CAMM(8) RSVIO_CAMM(9) RSVIO_CAMM(10)
+#undef RSVIO_CAMM
+                default: break;
+            }
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
         switch (G.n_free <= 10 ? G.n_free : 0) {
 #define RSVIO_CAM(NF) \
     case NF: hipLaunchKernelGGL(ba_camera_solve<NF>, g, b, 0, stream, G, pr, wk, combine, k5_variant); break;

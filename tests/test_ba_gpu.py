@@ -199,6 +199,47 @@ def test_window_sizes_match_oracle(gpu, oracle, n_kf):
     ba.close()
 
 
+@pytest.mark.parametrize("variant", ["mfma", "gj1"])
+@pytest.mark.parametrize("n_kf", [2, 3, 4, 5, 7, 8, 10, 11])
+def test_camera_solve_variants_match_oracle(gpu, oracle, monkeypatch, variant, n_kf):
+    """The K5 A/B variants (RSVIO_K5, read at handle creation) for 1..10 free keyframes: the
+    blocked LDL^T with MFMA trailing updates and the one-wave Gauss-Jordan solve give the
+    oracle's status and iteration count and its state within the stated tolerances, and the
+    camera step of one system within 1e-9 of the default pipelined LDL^T's."""
+    from rsvio import synthetic as S
+    if variant == "gj1" and n_kf > 10:
+        pytest.skip("gj1 is instantiated up to 9 free keyframes")
+    prob = S.ba_problem(n_kf=n_kf, n_lm=40 * n_kf, kf_per_lm=min(n_kf, 4), seed=300 + n_kf, init_seed=400 + n_kf)
+    ref = _adjuster(gpu, prob)
+    dc_ref = ref.camera_step(1e-4)
+    monkeypatch.setenv("RSVIO_K5", variant)
+    ba = _adjuster(gpu, prob)
+    monkeypatch.delenv("RSVIO_K5")
+    dc = ba.camera_step(1e-4)
+    assert np.abs(dc - dc_ref).max() <= 1e-9 * max(np.abs(dc_ref).max(), 1e-12)
+    res = ba.run()
+    pose, pw = ba.state()
+    po, pwo, ro = oracle.ba_solve(prob)
+    assert res.status == ro.status and res.iterations == ro.iterations
+    assert np.abs(pose - po).max() < 1e-7
+    assert np.abs(pw - pwo).max() < 1e-6
+    ba.close()
+    ref.close()
+
+
+def test_camera_solve_mfma_config3(gpu, oracle, cfg3, monkeypatch):
+    """Config 3 (9 free keyframes, n = 54) with the MFMA camera solve: oracle parity."""
+    monkeypatch.setenv("RSVIO_K5", "mfma")
+    ba = _adjuster(gpu, cfg3)
+    monkeypatch.delenv("RSVIO_K5")
+    res = ba.run()
+    pose, pw = ba.state()
+    po, pwo, ro = oracle.ba_solve(cfg3)
+    assert res.status == ro.status and res.iterations == ro.iterations
+    assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6
+    ba.close()
+
+
 def test_sharded_code_path_single_rank(gpu, cfg3):
     """The sharded path (RCCL all-reduce of sys, per-rank trial scalars + 32-B all-reduce,
     pre-reduced LM decision) on a 1-rank communicator equals the unsharded path bit for bit."""

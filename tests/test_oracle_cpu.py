@@ -115,3 +115,25 @@ def test_stereo_tracker_canonical_ids(oracle):
         ids_seen.append(set(ids))
     # ids are never reused
     assert max(max(s) for s in ids_seen if s) < 10_000
+
+
+def test_threaded_oracle_legs_match_sequential(oracle):
+    """The all-cores CPU baseline legs: the threaded Schur BA (landmark ranges summed in range
+    order) is tolerance-equal to the sequential reference order, and the threaded tracker
+    (pyramid levels and features in parallel) is bit-identical."""
+    from rsvio import synthetic as S
+    prob = S.ba_problem(n_kf=6, n_lm=300, kf_per_lm=4, seed=21, init_seed=22)
+    p1, w1, r1 = oracle.ba_solve(prob)
+    oracle.set_ba_threads(4)
+    try:
+        p4, w4, r4 = oracle.ba_solve(prob)
+    finally:
+        oracle.set_ba_threads(1)
+    assert (r1.status, r1.iterations) == (r4.status, r4.iterations)
+    assert np.abs(p1 - p4).max() < 1e-9 and np.abs(w1 - w4).max() < 1e-8
+    frames = list(S.stereo_sequence(2, 320, 240))
+    outs = []
+    for threads in (1, 4):
+        t = oracle.StereoTracker(320, 240, 3, 30, 20, 0.01, threads=threads)
+        outs.append([t.process_frame(l, r) for l, r in frames])
+    assert outs[0] == outs[1]

@@ -37,6 +37,28 @@ def main(reps=40):
         if k >= 5:
             for key, v in zip(t, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5)):
                 t[key].append(1e3 * v)
+    t2x = []
+    for k in range(20):
+        ba.set_problem_from(wins[k % 2])
+        t0 = time.perf_counter()
+        ba.set_problem_from(wins[(k + 1) % 2])   # no graph to drop, stream settled
+        t2x.append(1e3 * (time.perf_counter() - t0))
+    print(f"set_problem right after set_problem: {np.median(t2x):.4f} ms", flush=True)
+    import ctypes as C
+    from rsvio import _lib
+    lib = _lib.load()
+    p = wins[0]
+    arrs = [np.ascontiguousarray(a) for a in (p.pose7, p.kf_fixed, p.p_W, p.obs_lm, p.obs_kf, p.obs_cam, p.obs_uv,
+                                              p.T_C_B2)]
+    tc = []
+    for k in range(20):
+        ba.set_problem_from(wins[1])
+        t0 = time.perf_counter()
+        lib.rsvio_ba_set_problem(ba._h, p.n_kf, arrs[0].ctypes.data, arrs[1].ctypes.data, p.n_lm, arrs[2].ctypes.data,
+                                 p.n_obs, arrs[3].ctypes.data, arrs[4].ctypes.data, arrs[5].ctypes.data,
+                                 arrs[6].ctypes.data, arrs[7].ctypes.data)
+        tc.append(1e3 * (time.perf_counter() - t0))
+    print(f"bare C call after set_problem: {np.median(tc):.4f} ms", flush=True)
     print(f"RSVIO_BA_GRAPHS={os.environ.get('RSVIO_BA_GRAPHS', '1')}: " +
           ", ".join(f"{k} {np.median(v):.4f} ms" for k, v in t.items()), flush=True)
     ba.close()
