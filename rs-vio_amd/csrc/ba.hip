@@ -197,6 +197,7 @@ struct Prob {
     const int4* pairs;       // n_chunk x pair_stride: {slot a, slot b, landmark, 0}, padding a = -1
     const int* pb_fa;
     const int* pb_fb;
+    const int* dmap;         // MFMA camera solve: packed-system entry -> dense LDS position (see kMfMap*)
 };
 
 struct Work {
@@ -385,6 +386,89 @@ __device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda
 #pragma unroll
             for (int c = 0; c < 3; ++c) Vi[a][c] = 0.0;
     return ok;
+}
+
+// ---------------------------------------------------------------------------------------
+// Pair lists of the Schur chunks, built on the device by set_problem from the uploaded slot
+// headers: chunk c = 8 pb + x lists, in ascending landmark order, every landmark of group x (the
+// landmarks of the waves w % 8 == x) that has slots in both keyframes (fa, fb) of camera block pb
+// -- a landmark has at most one slot per keyframe, so at most one pair per chunk -- as
+// {slot a, slot b, landmark, 0}, and {-1, 0, 0, 0} past the count (the host sizes the stride by
+// the largest group).  One 256-thread workgroup per chunk, each wave a contiguous run of the
+// group's waves: count, prefix over the four runs, write.
+// ---------------------------------------------------------------------------------------
+constexpr int kPairKU = 8;  // slot waves per lane whose headers are in flight together
+
+// lane's partner lane for (fa, fb) in its slot wave, or -1; sh is this wave's [64] scratch
+__device__ __forceinline__ int pair_partner(const int4 h0, const int4 h1, int fa, int fb, int lane, int* sh) {
+    sh[lane] = h1.y > 0 ? h1.x : -1;  // free index of the slot's keyframe (or -1)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int partner = -1;
+    if (h1.y > 0 && h1.x == fa) {
+        const int first = h0.z, nk = h0.w;
+        for (int j = first; j < first + nk; ++j)
+            if (sh[j] == fb) partner = j;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return partner;
+}
+
+__global__ __launch_bounds__(256) void ba_build_pairs(Geometry G, Prob Pr, int4* pairs) {
+    __shared__ int sh[4][64];
+    __shared__ int cnt[4];
+    const int c = blockIdx.x, pb = c / kGrp, x = c % kGrp;
+    const int fa = Pr.pb_fa[pb], fb = Pr.pb_fb[pb];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nw = G.n_wave > x ? (G.n_wave - x + kGrp - 1) / kGrp : 0;  // slot waves x + 8k of the group
+    const int k0 = nw * wave / 4, k1 = nw * (wave + 1) / 4;
+    int4* out = pairs + (size_t)c * G.pair_stride;
+    int n = 0;  // pass 1: this run's pair count
+    for (int kb = k0; kb < k1; kb += kPairKU) {
+        int4 h0[kPairKU], h1[kPairKU];
+#pragma unroll
+        for (int u = 0; u < kPairKU; ++u) {
+            const int k = min(kb + u, k1 - 1);
+            const size_t s = (size_t)64 * (x + kGrp * k) + lane;
+            h0[u] = Pr.slot_hdr[2 * s];
+            h1[u] = Pr.slot_hdr[2 * s + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kPairKU; ++u) {
+            if (kb + u >= k1) break;
+            const int p = pair_partner(h0[u], h1[u], fa, fb, lane, sh[wave]);
+            n += __popcll(__ballot(p >= 0));
+        }
+    }
+    if (lane == 0) cnt[wave] = n;
+    __syncthreads();
+    int base = 0;
+    for (int v = 0; v < wave; ++v) base += cnt[v];
+    const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    for (int kb = k0; kb < k1; kb += kPairKU) {  // pass 2: (slot wave, lane) order = landmark order
+        int4 h0[kPairKU], h1[kPairKU];
+#pragma unroll
+        for (int u = 0; u < kPairKU; ++u) {
+            const int k = min(kb + u, k1 - 1);
+            const size_t s = (size_t)64 * (x + kGrp * k) + lane;
+            h0[u] = Pr.slot_hdr[2 * s];
+            h1[u] = Pr.slot_hdr[2 * s + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kPairKU; ++u) {
+            if (kb + u >= k1) break;
+            const int w = x + kGrp * (kb + u);
+            const int p = pair_partner(h0[u], h1[u], fa, fb, lane, sh[wave]);
+            const unsigned long long m = __ballot(p >= 0);
+            if (p >= 0) {
+                const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                out[pos] = make_int4(64 * w + lane, 64 * w + p, h0[u].y, 0);
+            }
+            base += __popcll(m);
+        }
+    }
+    for (int i = total + tid; i < G.pair_stride; i += 256) out[i] = make_int4(-1, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1242,114 +1326,47 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve(Geometry G, Prob P
 // Tolerance parity like pipe4 (same pivots; the trailing sums reassociated by the MFMA).
 // ---------------------------------------------------------------------------------------
 typedef double mf_dbl4 __attribute__((ext_vector_type(4)));
-constexpr int kMfLd = 65;  // f64 leading dimension of M and Up (odd: column reads spread banks)
+constexpr int kMfLd = 65;  // f64 leading dimension of the LDS matrices (odd: column reads spread banks)
+constexpr int kMfPanel = 8;  // panel width: 8 pivots of in-panel VALU work between matrix-core updates
 
+// The augmented system [[S, .], [b^T, .]] padded to NPP = 16 NT >= NP + 1 rows: row NP is b, so
+// eliminating the augmented matrix turns row NP into z^T = (D^-1 L^-1 b)^T on the fly (one more
+// row of every panel).  Rows past NP are never initialised: elimination is row-local (a row's
+// update uses its own multiplier and the pivot rows' values), so they cannot leak into the
+// result; the same holds for the upper halves of the diagonal tiles.
 template <int NF>
 struct MfDims {
     static constexpr int NP = 6 * NF;
-    static constexpr int NT = (NP + 15) / 16;
+    static constexpr int NT = NP / 16 + 1;
     static constexpr int NPP = 16 * NT;
+    static constexpr int NH = (NP + kMfPanel - 1) / kMfPanel;  // panels
 };
 
-// pivot J of panel PK (width PW) by wave 0: inv = 1 / d_K ready.  Column J+1 (the next pivot's)
-// and column J+2 are updated from readlanes of the unscaled column u; columns >= J+3 from LDS
-// broadcasts of u issued this step and consumed one step later (uq, with the pivot's l as lp), so
-// neither the readlane issue cost nor the LDS latency sits on the 1/d chain.
-template <int PK, int J, int PW>
-__device__ __forceinline__ void mf_pivot(double (&a)[16], double (&uq)[16], double lp, double& b, double& myinv,
-                                         double inv, double* M, double* Up, int lane, bool& bad) {
-    constexpr int K = 16 * PK + J;
-    const double u = a[J];
-    const double l = u * inv;
-    double inv_next = 1.0;
-    if constexpr (J + 1 < PW) {  // the next pivot first: its 1/d chain overlaps the rest
-        a[J + 1] = fma(-l, rl64(u, K + 1), a[J + 1]);
-        const double piv = rl64(a[J + 1], K + 1);
-        bad |= !(piv > 0.0) || !isfinite(piv);
-        inv_next = rcp_f64(piv);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // the previous pivot's deferred updates (columns >= J+2), then this pivot's column J+2
-    if constexpr (J > 0)
-#pragma unroll
-        for (int jj = J + 2; jj < PW; ++jj) a[jj] = fma(-lp, uq[jj], a[jj]);
-    if constexpr (J + 2 < PW) a[J + 2] = fma(-l, rl64(u, K + 2), a[J + 2]);
-    M[K * kMfLd + lane] = l;   // column K of L (rows > K; the upper part is never read)
-    Up[J * kMfLd + lane] = u;  // column J of the panel's U = D L
-#pragma unroll
-    for (int jj = J + 3; jj < PW; ++jj) uq[jj] = Up[J * kMfLd + 16 * PK + jj];  // broadcasts
-    const double bK = rl64(b, K);
-    myinv = lane == K ? inv : myinv;
-    b = lane > K ? fma(-l, bK, b) : b;
-    if constexpr (J + 1 < PW) mf_pivot<PK, J + 1, PW>(a, uq, l, b, myinv, inv_next, M, Up, lane, bad);
+// Per packed-system entry (sys layout: n_pb x 36 S | 6 n_free b | 6 n_free g_c) its destination
+// in K5's LDS: >= 0 a column-major position of M (bit 30: + lambda after the sum), -1 none (the
+// upper half of a diagonal block), -2 - i the i-th g_c.  Built on the host per problem.
+constexpr int kMfMapLambda = 1 << 30;
+inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, int* map) {
+    const int np = 6 * nf;
+    for (int pb = 0; pb < n_pb; ++pb)
+        for (int k = 0; k < 36; ++k) {
+            const int ra = k / 6, ca = k % 6, fa = pb_fa[pb], fb = pb_fb[pb];
+            int v;
+            if (fa == fb)
+                v = ra >= ca ? ((6 * fa + ca) * kMfLd + 6 * fa + ra) | (ra == ca ? kMfMapLambda : 0) : -1;
+            else
+                v = (6 * fa + ra) * kMfLd + 6 * fb + ca;  // S[6fa+ra][6fb+ca] -> its lower mirror
+            map[36 * pb + k] = v;
+        }
+    for (int i = 0; i < np; ++i) map[36 * n_pb + i] = i * kMfLd + np;  // b_i -> row NP, column i
+    for (int i = 0; i < np; ++i) map[36 * n_pb + np + i] = -2 - i;
 }
 
-template <int NF, int PK>
-__device__ __forceinline__ void mf_panel(double* M, double* Up, int tid, double& b, double& myinv, bool& bad) {
-    constexpr int NP = MfDims<NF>::NP, NT = MfDims<NF>::NT;
-    constexpr int PW = (NP - 16 * PK) < 16 ? (NP - 16 * PK) : 16;
-    const int lane = tid & 63, wave = tid >> 6;
-    if (wave == 0) {
-        double a[16], uq[16];
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            a[jj] = jj < PW ? M[(16 * PK + jj) * kMfLd + lane] : 0.0;
-            uq[jj] = 0.0;
-        }
-        const double piv = rl64(a[0], 16 * PK);
-        bad |= !(piv > 0.0) || !isfinite(piv);
-        mf_pivot<PK, 0, PW>(a, uq, 0.0, b, myinv, rcp_f64(piv), M, Up, lane, bad);
-    }
-    // diagnostic stamps (stamps build): panel PK factored (9, 15, 30 / 7 for the last)
-    if constexpr (PK == 0) STAMP(9); else if constexpr (PK == 1) STAMP(15); else if constexpr (PK == 2) STAMP(30);
-    if constexpr (PK + 1 == NT) STAMP(7);
-    if constexpr (PK + 1 < NT) {
-        __syncthreads();
-        // trailing lower tiles (I, J), PK < J <= I < NT; wave 0 (the panel's) takes the fewest
-        constexpr int R = NT - 1 - PK;  // tile rows / columns left
-        constexpr int NTILE = R * (R + 1) / 2;
-        const int i16 = lane & 15, k4 = lane >> 4;
-        for (int t = 3 - wave; t < NTILE; t += 4) {
-            int J = 0, rem = t;
-            while (rem >= R - J) {
-                rem -= R - J;
-                ++J;
-            }
-            const int TJ = PK + 1 + J, TI = TJ + rem;
-            double av[4], bv[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int kk = 4 * m + k4;
-                av[m] = -Up[kk * kMfLd + 16 * TI + i16];
-                bv[m] = M[(16 * PK + kk) * kMfLd + 16 * TJ + i16];
-            }
-            mf_dbl4 c0, c1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c0[r] = M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r];
-            // two independent accumulation chains (columns 0-7 and 8-15 of the panel)
-            c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], c1, 0, 0, 0);
-            c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], c1, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r] = c0[r] + c1[r];
-        }
-        __syncthreads();
-        if constexpr (PK == 0) STAMP(13); else if constexpr (PK == 1) STAMP(19); else if constexpr (PK == 2) STAMP(31);
-        mf_panel<NF, PK + 1>(M, Up, tid, b, myinv, bad);
-    }
-}
-
-// The reduced system straight into the dense column-major lower triangle M (single rank):
-// combine_system's sums (8 partial systems in slot order, + lambda on the diagonal after the sum)
-// scattered to M[col][row], row >= col; b and g_c into bsh / gsh; M's other entries zero, the
-// padding diagonal one (written while the partial systems' loads are in flight).
+// combine_system with the sums scattered straight into M (and g_c into gsh) by the map
 template <int NF>
-__device__ void combine_dense(const Geometry& G, const Work& Wk, double* M, double* bsh, double* gsh, double lambda,
-                              int* fail) {
-    constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
-    constexpr int NPB = NF * (NF + 1) / 2;
-    constexpr int SB0 = NPB * 36, SG0 = SB0 + 6 * NF, NE = SG0 + 6 * NF;
+__device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
+                               double lambda, int* fail) {
+    constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
     constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
     const size_t L = sys_len(G);
     const int tid = threadIdx.x;
@@ -1361,42 +1378,25 @@ __device__ void combine_dense(const Geometry& G, const Work& Wk, double* M, doub
         sing = *Wk.singular;
     }
     double v[kE][kGrp];
+    int dst[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
+        dst[i] = e < NE ? Pr.dmap[e] : -1;
 #pragma unroll
         for (int x = 0; x < kGrp; ++x) v[i][x] = e < NE ? Wk.cpart[(size_t)x * L + e] : 0.0;
     }
-    for (int e = tid; e < NPP * kMfLd; e += T) {
-        const int c = e / kMfLd, r = e - c * kMfLd;
-        M[e] = (r == c && r >= NP) ? 1.0 : 0.0;
-    }
-    __syncthreads();
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
-        const int e = tid + T * i;
-        if (e >= NE) break;
         double a = v[i][0];
 #pragma unroll
         for (int x = 1; x < kGrp; ++x) a += v[i][x];
-        if (e < SB0) {
-            const int pb = e / 36, k = e - 36 * pb, ra = k / 6, ca = k - 6 * ra;
-            int fa = 0, rem = pb;
-            while (rem >= NF - fa) {
-                rem -= NF - fa;
-                ++fa;
-            }
-            const int fb = fa + rem;
-            if (fa == fb) {
-                if (ra == ca) a += lambda;
-                if (ra >= ca) M[(6 * fa + ca) * kMfLd + 6 * fa + ra] = a;
-            } else {
-                M[(6 * fa + ra) * kMfLd + 6 * fb + ca] = a;
-            }
-        } else if (e < SG0) {
-            bsh[e - SB0] = a;
-        } else {
-            gsh[e - SG0] = a;
+        const int d = dst[i];
+        if (d >= 0) {
+            if (d & kMfMapLambda) a += lambda;
+            M[d & (kMfMapLambda - 1)] = a;
+        } else if (d <= -2) {
+            gsh[-2 - d] = a;
         }
     }
     if (tid < 64) {
@@ -1412,13 +1412,105 @@ __device__ void combine_dense(const Geometry& G, const Work& Wk, double* M, doub
     }
 }
 
+// pivot J of panel H (width PW) by wave 0: inv = 1 / d_K ready.  Column J+1 (the next pivot's)
+// and column J+2 are updated from readlanes of the unscaled column u; columns >= J+3 from LDS
+// broadcasts of u issued this step and consumed one step later (uq, with the pivot's l as lp), so
+// neither the readlane issue cost nor the LDS latency sits on the 1/d chain.
+template <int H, int J, int PW>
+__device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMfPanel], double lp, double inv,
+                                         double* Lf, double* Up, int lane, bool& bad) {
+    constexpr int K = kMfPanel * H + J;
+    const double u = a[J];
+    double inv_next = 1.0;
+    double uk1 = 0.0;
+    if constexpr (J + 1 < PW) {
+        // the next pivot on the shortest chain: d_{K+1} = a_{K+1,K+1} - u_{K+1,K}^2 / d_K, with
+        // u_{K+1,K} and a_{K+1,K+1} read before 1/d_K is known -- inv -> fma -> rcp (+ Newton),
+        // uniform on every lane, no readlane on the chain
+        uk1 = rl64(u, K + 1);
+        const double piv = fma(-(uk1 * uk1), inv, rl64(a[J + 1], K + 1));
+        bad |= !(piv > 0.0) || !isfinite(piv);
+        inv_next = rcp_f64(piv);
+    }
+    const double l = u * inv;
+    if constexpr (J + 1 < PW) a[J + 1] = fma(-l, uk1, a[J + 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (J > 0)
+#pragma unroll
+        for (int jj = J + 2; jj < PW; ++jj) a[jj] = fma(-lp, uq[jj], a[jj]);
+    if constexpr (J + 2 < PW) a[J + 2] = fma(-l, rl64(u, K + 2), a[J + 2]);
+    Lf[K * kMfLd + lane] = l;  // column K of L (rows > K; row NP: z_K); the upper part is never read
+    Up[J * kMfLd + lane] = u;  // column J of the panel's U = D L
+#pragma unroll
+    for (int jj = J + 3; jj < PW; ++jj) uq[jj] = Up[J * kMfLd + kMfPanel * H + jj];  // broadcasts
+    if constexpr (J + 1 < PW) mf_pivot<H, J + 1, PW>(a, uq, l, inv_next, Lf, Up, lane, bad);
+}
+
+// Panel H (columns 8H .. 8H + PW - 1): wave 0 factors it from M into Lf / Up, then every wave
+// updates its share of the trailing lower tiles (I, J), J >= (8H + 8) / 16, on the matrix cores:
+// C_IJ += (-U_I) L_J^T over the panel (2 MFMAs per tile).  A tile holding factored columns gets
+// garbage there (their L lives in Lf).
+template <int NF, int H>
+__device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int tid, bool& bad) {
+    constexpr int NP = MfDims<NF>::NP, NT = MfDims<NF>::NT, NH = MfDims<NF>::NH;
+    constexpr int C0 = kMfPanel * H;
+    constexpr int PW = (NP - C0) < kMfPanel ? (NP - C0) : kMfPanel;
+    const int lane = tid & 63, wave = tid >> 6;
+    if (wave == 0) {
+        double a[kMfPanel], uq[kMfPanel];
+#pragma unroll
+        for (int jj = 0; jj < kMfPanel; ++jj) {
+            a[jj] = jj < PW ? M[(C0 + jj) * kMfLd + lane] : 0.0;
+            uq[jj] = 0.0;
+        }
+        const double piv = rl64(a[0], C0);
+        bad |= !(piv > 0.0) || !isfinite(piv);
+        mf_pivot<H, 0, PW>(a, uq, 0.0, rcp_f64(piv), Lf, Up, lane, bad);
+    }
+    if constexpr (H == 0) STAMP(9); else if constexpr (H == 2) STAMP(15); else if constexpr (H == 4) STAMP(30);
+    if constexpr (H + 1 == NH) STAMP(7);
+    if constexpr (H + 1 < NH) {
+        __syncthreads();
+        constexpr int T0 = (C0 + kMfPanel) / 16;  // first tile column with unfactored columns
+        constexpr int R = NT - T0;
+        constexpr int NTILE = R * (R + 1) / 2;
+        const int i16 = lane & 15, k4 = lane >> 4;
+        for (int t = 3 - wave; t < NTILE; t += 4) {  // wave 0 (the panel's) takes the fewest
+            int J = 0, rem = t;
+            while (rem >= R - J) {
+                rem -= R - J;
+                ++J;
+            }
+            const int TJ = T0 + J, TI = TJ + rem;
+            double av[2], bv[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int kk = 4 * m + k4;
+                av[m] = -Up[kk * kMfLd + 16 * TI + i16];
+                bv[m] = Lf[(C0 + kk) * kMfLd + 16 * TJ + i16];
+            }
+            mf_dbl4 c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[r] = M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r];
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r] = c[r];
+        }
+        __syncthreads();
+        if constexpr (H == 0) STAMP(13); else if constexpr (H == 2) STAMP(19); else if constexpr (H == 4) STAMP(31);
+        mf_panel<NF, H + 1>(M, Lf, Up, tid, bad);
+    }
+}
+
 template <int NF>
 __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, Prob Pr, Work Wk, int combine) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
     constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
     __shared__ __attribute__((aligned(16))) double M[NPP * kMfLd];
-    __shared__ __attribute__((aligned(16))) double Up[16 * kMfLd];
-    __shared__ double bsh[NP], gsh[NP];
+    __shared__ __attribute__((aligned(16))) double Lf[NPP * kMfLd];
+    __shared__ __attribute__((aligned(16))) double Up[kMfPanel * kMfLd];
+    __shared__ double gsh[NP];
     __shared__ int fail;
     RTSTAMP(4);
     LmState* st = Wk.st;
@@ -1436,22 +1528,16 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
     }
     STAMP(0);
     if (combine) {
-        combine_dense<NF>(G, Wk, M, bsh, gsh, st->lambda, &fail);
-    } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys
+        combine_mapped<NF>(G, Pr, Wk, M, gsh, st->lambda, &fail);
+    } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
         const double* sys = Wk.sys;
-        for (int e = tid; e < NPP * kMfLd; e += kK5Threads) {
-            const int c = e / kMfLd, r = e - c * kMfLd;
-            double v = 0.0;
-            if (r < NP && c < NP) {
-                if (r >= c) v = *sys_lower<NF>(sys, r, c);
-            } else if (r == c) {
-                v = 1.0;
-            }
-            M[e] = v;
-        }
-        if (tid < NP) {
-            bsh[tid] = *sys_lower<NF>(sys, NP, tid);
-            gsh[tid] = sys[(NF * (NF + 1) / 2) * 36 + 6 * NF + tid];
+        constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
+        for (int e = tid; e < NE; e += kK5Threads) {
+            const int d = Pr.dmap[e];
+            if (d >= 0)
+                M[d & (kMfMapLambda - 1)] = sys[e];
+            else if (d <= -2)
+                gsh[-2 - d] = sys[e];
         }
         if (tid == 0) fail = sys[SC0 + 1] != 0.0;
     }
@@ -1462,28 +1548,27 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
         *Wk.singular = 0;
     }
     const double gcl_v = (wave == 0 && lane < n) ? gsh[lane] : 0.0;
-    double b = (wave == 0 && lane < NP) ? bsh[lane] : 0.0;
     __syncthreads();
     STAMP(2);
     if (fail) {
         if (tid == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
-    double myinv = 0.0;
     bool bad = false;
-    mf_panel<NF, 0>(M, Up, tid, b, myinv, bad);
+    mf_panel<NF, 0>(M, Lf, Up, tid, bad);
     if (wave != 0) return;
     if (bad) {
         if (lane == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
-    // z = D^-1 L^-1 b; L^T x = z (unit diagonal): lane j, L[i][j] = M[j][i] column-major, zero
-    // for i <= j so the update needs no select
-    double yv = lane < NP ? b * myinv : 0.0;
+    // z_j = L[NP][j] (row NP of the eliminated augmented matrix); L^T x = z (unit diagonal):
+    // lane j, L[i][j] = Lf[j][i] column-major, zero for i <= j so the update needs no select
+    const int lj = lane < NP ? lane : 0;
+    double yv = lane < NP ? Lf[lj * kMfLd + NP] : 0.0;
     double lt[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const double m = M[(lane < NP ? lane : 0) * kMfLd + j];
+        const double m = Lf[lj * kMfLd + j];
         lt[j] = lane < j ? m : 0.0;
     }
 #pragma unroll
@@ -2066,8 +2151,8 @@ struct BundleAdjuster {
     int g_k = -1;
     rsvio_lm_cfg g_cfg{};
     bool graphs_ok = true;
-    int k5_variant = 0;  // camera solve for n_free <= 10: 0 pipelined 4-wave LDL^T, 1 one-wave Gauss-Jordan,
-                         // 2 blocked LDL^T with MFMA trailing updates
+    int k5_variant = 2;  // camera solve for n_free <= 10: 2 blocked LDL^T with MFMA trailing updates (default),
+                         // 0 pipelined 4-wave LDL^T (RSVIO_K5=pipe4), 1 one-wave Gauss-Jordan (gj1)
     // an exec whose launch may still run is never destroyed: the stream settles first (a ticket
     // wait returns before the last decision kernel has exited)
     void drop_graph() {
@@ -2131,13 +2216,13 @@ struct BundleAdjuster {
     hipEvent_t ev_up = nullptr;
     bool up_pending = false;
     struct ArenaLayout {
-        size_t pose_init, pw_init, free_idx, hdr, uv, pairs, pb_fa, pb_fb, total;
+        size_t pose_init, pw_init, free_idx, hdr, uv, pairs, pb_fa, pb_fb, dmap, total;
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
     bool state_fresh = false;  // set_problem without a run since: get_state resets the buffers first
     // host scratch of set_problem, kept across problems (no per-problem allocations)
     std::vector<int> hs_free, hs_cnt, hs_order, hs_slot_kf, hs_slot_lm, hs_slot_obs, hs_lm_slot, hs_wave_slot,
-        hs_pslot, hs_lm_group, hs_pb_of, hs_pair_cnt, hs_pb_fa, hs_pb_fb;
+        hs_pslot, hs_lm_group, hs_pb_of, hs_pb_fa, hs_pb_fb;
     DevBuf<double> d_raws, d_rawl, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
     DevBuf<int> d_singular;
     size_t n_pad = 0;
@@ -2218,6 +2303,7 @@ struct BundleAdjuster {
         p.pairs = reinterpret_cast<const int4*>(d_arena.p + lay.pairs);
         p.pb_fa = reinterpret_cast<const int*>(d_arena.p + lay.pb_fa);
         p.pb_fb = reinterpret_cast<const int*>(d_arena.p + lay.pb_fb);
+        p.dmap = reinterpret_cast<const int*>(d_arena.p + lay.dmap);
         return p;
     }
     // the kernels of LM iteration `it` read state copy it & 1 and work on copy (it + 1) & 1
@@ -2364,21 +2450,16 @@ struct BundleAdjuster {
                 lm_group[slot_lm[sl]] = w % kGrp;
                 pslot[sl] = 64 * w + (sl - wave_slot[w]);
             }
-        // slot pairs per chunk 8 pb + x: counted first (the stride), filled in landmark order below
+        // Schur chunk pairs: built on the device (ba_build_pairs) after the upload; the stride is
+        // the largest group's landmark count (at most one pair per landmark and chunk)
         const int n_chunk = kGrp * n_pb;
-        auto& pcnt = hs_pair_cnt;
-        pcnt.assign((size_t)n_chunk, 0);
-        for (int l = 0; l < n_lm; ++l)
-            for (int sa = lm_slot[l]; sa < lm_slot[l + 1]; ++sa) {
-                const int fa = free_idx[slot_kf[sa]];
-                if (fa < 0) continue;
-                for (int sb = sa; sb < lm_slot[l + 1]; ++sb) {
-                    const int fb = free_idx[slot_kf[sb]];
-                    if (fb >= 0) pcnt[kGrp * pb_of[fa * n_free + fb] + lm_group[l]] += 1;
-                }
-            }
         int stride = 1;
-        for (int c : pcnt) stride = std::max(stride, c);
+        {
+            int gl[kGrp] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int l = 0; l < n_lm; ++l)
+                if (lm_slot[l + 1] > lm_slot[l]) gl[lm_group[l]] += 1;
+            for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
+        }
         n_pad = (size_t)64 * n_wave;
         mark();
         // arena layout
@@ -2390,9 +2471,11 @@ struct BundleAdjuster {
         L.free_idx = off;  off += al(sizeof(int) * (size_t)n_kf);
         L.hdr = off;       off += al(sizeof(int4) * 2 * std::max<size_t>(n_pad, 1));
         L.uv = off;        off += al(sizeof(double2) * 2 * std::max<size_t>(n_pad, 1));
-        L.pairs = off;     off += al(sizeof(int4) * (size_t)n_chunk * stride);
         L.pb_fa = off;     off += al(sizeof(int) * (size_t)n_pb);
         L.pb_fb = off;     off += al(sizeof(int) * (size_t)n_pb);
+        L.dmap = off;      off += al(sizeof(int) * ((size_t)36 * n_pb + 12 * n_free));
+        const size_t upload = off;  // everything before the pairs comes from the host
+        L.pairs = off;     off += al(sizeof(int4) * (size_t)n_chunk * stride);
         L.total = off;
         if (up_pending) {  // the previous upload still reads the staging image
             RSVIO_HIP(hipEventSynchronize(ev_up));
@@ -2407,51 +2490,34 @@ struct BundleAdjuster {
         if (n_lm) std::memcpy(hb + L.pw_init, pW, sizeof(double) * 3 * (size_t)n_lm);
         std::memcpy(hb + L.free_idx, free_idx.data(), sizeof(int) * (size_t)n_kf);
         // padded slot layout (64 per wave): two int4 headers + 2 double2 observations per slot
-        int* hdr = reinterpret_cast<int*>(hb + L.hdr);
-        double* huv = reinterpret_cast<double*>(hb + L.uv);
-        std::memset(hdr, 0, sizeof(int4) * 2 * n_pad);
-        std::memset(huv, 0, sizeof(double2) * 2 * n_pad);
-        for (size_t ps = 0; ps < n_pad; ++ps) hdr[8 * ps + 4] = -1;
-        for (int w = 0; w < n_wave; ++w)
-            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
-                const size_t ps = (size_t)pslot[sl];
+        // every entry written once, in order (real slots, then the wave's padding lanes)
+        int4* hdr = reinterpret_cast<int4*>(hb + L.hdr);
+        double2* huv = reinterpret_cast<double2*>(hb + L.uv);
+        for (int w = 0; w < n_wave; ++w) {
+            const int s0 = wave_slot[w], s1 = wave_slot[w + 1];
+            for (int sl = s0; sl < s1; ++sl) {
+                const size_t ps = (size_t)64 * w + (sl - s0);
                 const int l = slot_lm[sl];
-                int* h = hdr + 8 * ps;
                 const int no = slot_obs[sl + 1] - slot_obs[sl];
-                h[0] = slot_kf[sl];
-                h[1] = l;
-                h[2] = lm_slot[l] - wave_slot[w];
-                h[3] = lm_slot[l + 1] - lm_slot[l];
-                h[4] = no ? free_idx[slot_kf[sl]] : -1;
-                h[5] = no;
-                for (int q = 0; q < no; ++q) {
-                    const int o = order[slot_obs[sl] + q];
-                    h[6] |= obs_cam[o] << q;
-                    huv[4 * ps + 2 * q] = obs_uv[2 * (size_t)o];
-                    huv[4 * ps + 2 * q + 1] = obs_uv[2 * (size_t)o + 1];
-                }
+                const int o0 = order[slot_obs[sl]], o1 = no > 1 ? order[slot_obs[sl] + 1] : o0;
+                hdr[2 * ps] = make_int4(slot_kf[sl], l, lm_slot[l] - s0, lm_slot[l + 1] - lm_slot[l]);
+                hdr[2 * ps + 1] = make_int4(free_idx[slot_kf[sl]], no, obs_cam[o0] | (no > 1 ? obs_cam[o1] << 1 : 0), 0);
+                huv[2 * ps] = make_double2(obs_uv[2 * (size_t)o0], obs_uv[2 * (size_t)o0 + 1]);
+                huv[2 * ps + 1] = no > 1 ? make_double2(obs_uv[2 * (size_t)o1], obs_uv[2 * (size_t)o1 + 1])
+                                         : make_double2(0.0, 0.0);
             }
-        mark();
-        {  // pairs: {slot a, slot b, landmark, 0} at a fixed stride per chunk, padding a = -1
-            int4* pq = reinterpret_cast<int4*>(hb + L.pairs);
-            for (size_t i = 0; i < (size_t)n_chunk * stride; ++i) pq[i] = make_int4(-1, 0, 0, 0);
-            std::fill(pcnt.begin(), pcnt.end(), 0);  // reused as fill cursors
-            for (int l = 0; l < n_lm; ++l)
-                for (int sa = lm_slot[l]; sa < lm_slot[l + 1]; ++sa) {
-                    const int fa = free_idx[slot_kf[sa]];
-                    if (fa < 0) continue;
-                    for (int sb = sa; sb < lm_slot[l + 1]; ++sb) {
-                        const int fb = free_idx[slot_kf[sb]];
-                        if (fb < 0) continue;
-                        const int c = kGrp * pb_of[fa * n_free + fb] + lm_group[l];
-                        pq[(size_t)c * stride + pcnt[c]++] = make_int4(pslot[sa], pslot[sb], l, 0);
-                    }
-                }
+            for (size_t ps = (size_t)64 * w + (s1 - s0); ps < (size_t)64 * (w + 1); ++ps) {
+                hdr[2 * ps] = make_int4(0, 0, 0, 0);
+                hdr[2 * ps + 1] = make_int4(-1, 0, 0, 0);
+                huv[2 * ps] = huv[2 * ps + 1] = make_double2(0.0, 0.0);
+            }
         }
+        mark();
         std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
+        mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
         mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.total, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, upload, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
         mark();
@@ -2459,6 +2525,9 @@ struct BundleAdjuster {
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
+        hipLaunchKernelGGL(ba_build_pairs, dim3(n_chunk), dim3(256), 0, stream, G, prob(),
+                           reinterpret_cast<int4*>(d_arena.p + L.pairs));
+        RSVIO_HIP(hipGetLastError());
         grow(d_pose2, 14 * (size_t)n_kf);
         grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
         {  // partial systems: every entry of every slot is written by K4c each iteration; zeroed

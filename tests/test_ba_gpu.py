@@ -199,13 +199,13 @@ def test_window_sizes_match_oracle(gpu, oracle, n_kf):
     ba.close()
 
 
-@pytest.mark.parametrize("variant", ["mfma", "gj1"])
+@pytest.mark.parametrize("variant", ["pipe4", "gj1"])
 @pytest.mark.parametrize("n_kf", [2, 3, 4, 5, 7, 8, 10, 11])
 def test_camera_solve_variants_match_oracle(gpu, oracle, monkeypatch, variant, n_kf):
     """The K5 A/B variants (RSVIO_K5, read at handle creation) for 1..10 free keyframes: the
-    blocked LDL^T with MFMA trailing updates and the one-wave Gauss-Jordan solve give the
-    oracle's status and iteration count and its state within the stated tolerances, and the
-    camera step of one system within 1e-9 of the default pipelined LDL^T's."""
+    pipelined 4-wave VALU LDL^T and the one-wave Gauss-Jordan solve give the oracle's status and
+    iteration count and its state within the stated tolerances, and the camera step of one
+    system within 1e-9 of the default blocked LDL^T with MFMA trailing updates."""
     from rsvio import synthetic as S
     if variant == "gj1" and n_kf > 10:
         pytest.skip("gj1 is instantiated up to 9 free keyframes")
@@ -227,9 +227,10 @@ def test_camera_solve_variants_match_oracle(gpu, oracle, monkeypatch, variant, n
     ref.close()
 
 
-def test_camera_solve_mfma_config3(gpu, oracle, cfg3, monkeypatch):
-    """Config 3 (9 free keyframes, n = 54) with the MFMA camera solve: oracle parity."""
-    monkeypatch.setenv("RSVIO_K5", "mfma")
+def test_camera_solve_pipe4_config3(gpu, oracle, cfg3, monkeypatch):
+    """Config 3 (9 free keyframes, n = 54) with the pipelined VALU camera solve (RSVIO_K5=pipe4,
+    the A/B alternative to the default MFMA solve): oracle parity."""
+    monkeypatch.setenv("RSVIO_K5", "pipe4")
     ba = _adjuster(gpu, cfg3)
     monkeypatch.delenv("RSVIO_K5")
     res = ba.run()

@@ -24,10 +24,11 @@ for rep in range(5):
 buf = (C.c_ulonglong * 64)()
 lib.rsvio_dbg_ba_stamps(buf, 64)
 st = np.array(buf[:32], dtype=np.int64)
-seq = [("prologue", 0), ("combine", 1), ("fill M", 2), ("panel0 factor", 9), ("panel0 trailing", 13),
-       ("panel1 factor", 15), ("panel1 trailing", 19), ("panel2 factor", 30), ("panel2 trailing", 31),
-       ("panel3 factor", 7), ("back subst", 3), ("finish", 4), ("poses", 5), ("result", 6)]
-prev = st[0]
-for name, k in seq:
-    print(f"{name:18s} {st[k] - prev:7d} cycles (t = {st[k] - st[0]})")
-    prev = st[k]
+names = {0: "start", 1: "combine", 2: "fail check", 9: "panel 0 factored", 13: "panel 0 trailing",
+         15: "panel 2 factored", 19: "panel 2 trailing", 30: "panel 4 factored", 31: "panel 4 trailing",
+         7: "last panel factored", 3: "back substitution", 4: "finish sums", 5: "trial poses", 6: "result"}
+ev = sorted((int(st[k]), k) for k in names if st[k] > 0)
+prev = ev[0][0]
+for t, k in ev:
+    print(f"{names[k]:22s} +{t - prev:6d} cycles (t = {t - ev[0][0]})")
+    prev = t
