@@ -169,52 +169,55 @@ def measure_rows(device: int, cpu: bool, reps: int = 200):
     out["track_motion"] = row
     mt.close()
     out["ba_config5"] = measure_config5_row(device, cpu)
-    out["ba_batched"] = measure_ba_batched_row(device)
+    out["ba_batched"] = measure_ba_batched_row(device, 16)
+    out["ba_batched_64"] = measure_ba_batched_row(device, 64, reps=5)
     out["ft_tracker"] = measure_ft_row(device, cpu)
     return out
 
 
 def measure_ba_batched_row(device: int, n_windows: int = 16, reps: int = 10):
     """SURVEY 8d "batched mode" for HP-B: B independent config-3 windows (10 KF x 2,000
-    landmarks, distinct seeds) solved concurrently -- one BundleAdjuster handle and HIP stream
-    per window, every solve enqueued (rsvio_ba_run_async) before any is awaited.  value = solves
-    per second over `reps` rounds of B solves (host wall time, every solve to convergence);
-    roofline: FP64 work of the LM iterations actually run / that time."""
+    landmarks, distinct seeds) solved by ONE launch chain (rsvio_ba_batch_run: the window is a
+    grid dimension of every LM kernel, one camera-solve workgroup per window), every window to
+    convergence.  value = solves per second over `reps` batch solves (host wall time around
+    rsvio_ba_batch_run); roofline: FP64 work of the LM iterations every window ran / that time,
+    and the chain's device time (HIP events on the batch stream, solve_ms)."""
     from rsvio import synthetic as S
-    from rsvio.ba import BundleAdjuster
+    from rsvio.ba import BundleAdjuster, BundleBatch
     probs = [S.ba_problem(seed=7 + 101 * i, init_seed=11 + 101 * i) for i in range(n_windows)]
     bas = [BundleAdjuster(max_keyframes=p.n_kf, max_landmarks=p.n_lm, max_observations=p.n_obs, device=device)
            for p in probs]
     for b, p in zip(bas, probs):
         b.set_problem_from(p)
-    for _ in range(2):                                   # warm-up (and sets each handle's chunk size)
-        for b in bas:
-            b.run_async()
-        for b in bas:
-            b.wait()
-    iters = 0
+    batch = BundleBatch(bas)
+    for _ in range(2):                                   # warm-up (and sets the chunk size)
+        batch.run()
+    iters, dev_ms, chain_its = 0, [], []
     t0 = time.perf_counter()
     for _ in range(reps):
-        for b in bas:
-            b.run_async()
-        for b in bas:
-            iters += b.wait().iterations
+        res = batch.run()
+        iters += sum(r.iterations for r in res)
+        dev_ms.append(res[0].solve_ms)
+        chain_its.append(max(r.iterations for r in res))
     el = time.perf_counter() - t0
     p0 = probs[0]
     flops = ba_flops_per_iter(p0.n_obs, p0.n_lm, 6, int((p0.kf_fixed == 0).sum())) * iters
     ach = flops / el / 1e12
+    ach_dev = flops / (1e-3 * sum(dev_ms)) / 1e12
+    batch.close()
     for b in bas:
         b.close()
     n = n_windows * reps
     return {"workload": f"{n_windows} independent config-3 windows (10 KF x 2,000 landmarks, 24,000 observations "
-                        f"each) solved concurrently, one handle + stream per window",
+                        "each) solved by one batched launch chain (rsvio_ba_batch_run)",
             "value": round(n / el, 1), "unit": "solves/s", "windows": n_windows,
-            "ms_per_round": round(1e3 * el / reps, 4), "lm_iterations_mean": round(iters / n, 2),
+            "ms_per_batch": round(1e3 * el / reps, 4), "device_ms_per_batch": round(float(np.median(dev_ms)), 4),
+            "lm_iterations_mean": round(iters / n, 2), "chain_iterations_mean": round(float(np.mean(chain_its)), 2),
             "roofline": {"bound": "fp64", "achieved": round(ach, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(ach / FP64_PEAK_TFLOPS, 6),
-                         "note": "host-enqueue and latency bound: ~17 launches per solve from one host thread, "
-                                 "4 hardware queues"}}
-
+                         "frac": round(ach / FP64_PEAK_TFLOPS, 6), "achieved_device_time": round(ach_dev, 4),
+                         "frac_device_time": round(ach_dev / FP64_PEAK_TFLOPS, 6),
+                         "note": "one launch chain for all windows: K4, then per LM iteration K4c (B x 360 "
+                                 "workgroups), K5 (B workgroups), K6 (B x waves), K7 per chunk"}}
 
 def measure_config5_row(device: int, cpu: bool, reps: int = 10):
     """BASELINE config 5: TUM-VI EUCM, window 20 x 5,000 landmarks (80,000 observations).  The

@@ -336,6 +336,19 @@ int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W);
 int rsvio_ba_build_system(rsvio_ba* ba, double lambda, double huber_delta, double* S, double* b,
                           double* cost);
 
+/* Batched mode: n independent windows -- each a handle whose problem was
+ * uploaded by rsvio_ba_set_problem -- solved by ONE launch chain (the window is a grid dimension
+ * of every LM kernel; one camera-solve workgroup per window), each window exactly as its own
+ * rsvio_ba_run would solve it (SlidingWindow::optimize, sliding_window.rs:159-381, per window).
+ * Windows may differ in keyframes (<= 10 free each), landmarks and observations; a window the
+ * guards of sliding_window.rs:303-319 skip reports RSVIO_LM_SKIPPED.  results[i] is window i's;
+ * solve_ms is the whole batch's.  rsvio_ba_get_state on a window handle reads its solution.  The
+ * batch borrows the handles (they must outlive it) and runs on its own stream. */
+typedef struct rsvio_ba_batch rsvio_ba_batch;
+int rsvio_ba_batch_create(rsvio_ba* const* windows, int32_t n, rsvio_ba_batch** out);
+int rsvio_ba_batch_run(rsvio_ba_batch* batch, const rsvio_lm_cfg* cfg, rsvio_ba_result* results);
+void rsvio_ba_batch_destroy(rsvio_ba_batch* batch);
+
 /* Landmark sharding over ranks: each rank uploads only its own
  * landmarks/observations; the reduced system and costs are summed with RCCL over xGMI. */
 int rsvio_rccl_unique_id(uint8_t* out, size_t cap);   /* cap >= 128 */

@@ -478,12 +478,13 @@ __global__ __launch_bounds__(256) void ba_build_pairs(Geometry G, Prob Pr, int4*
 // with_reset: K0 folded in (one kernel boundary less per solve): the grid also copies the
 // initial state into both state buffers and initialises the LM state; the linearisation reads
 // the initial state directly (the same values K0 copies).
-__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk, int with_reset, double lambda0) {
+__device__ void linearize_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w, int with_reset,
+                               double lambda0) {
     __shared__ double sh[10][64];
-    const int w = blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
     const int s = 64 * w + lane;
     if (with_reset) {
-        const int nt = (int)gridDim.x * 64;
+        const int nt = G.n_wave * 64;  // the window's own waves (a batched grid may be wider)
         for (int i = s; i < 7 * G.n_kf; i += nt) {
             Wk.pose[0][i] = Wk.pose_init[i];
             Wk.pose[1][i] = Wk.pose_init[i];
@@ -528,6 +529,10 @@ __global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk,
         Wk.partA[w * kPartA + 1] = 0.0;
     }
     STAMP(14);
+}
+
+__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk, int with_reset, double lambda0) {
+    linearize_body(G, Pr, Wk, blockIdx.x, with_reset, lambda0);
 }
 
 // Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
@@ -794,10 +799,10 @@ __device__ __forceinline__ void schur_chunk_pairs(const Geometry& G, const Work&
     }
 }
 
-__global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, LmArgs la,
-                                                                  int pre_reduced) {
+__device__ void schur_chunks_body(const Geometry& G, const Prob& Pr, const Work& Wk, const LmArgs& la,
+                                  int pre_reduced, int c) {
     __shared__ double red[kSchurThreads / 64][kBlockF];
-    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pb = c / kGrp, x = c % kGrp;
     RTSTAMP(0);
     STAMP(26);
@@ -846,6 +851,11 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Pro
     }
     STAMP(18);
     RTSTAMP(2);
+}
+
+__global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, LmArgs la,
+                                                                  int pre_reduced) {
+    schur_chunks_body(G, Pr, Wk, la, pre_reduced, blockIdx.x);
 }
 
 // The reduced system of this rank into dst (sys layout): S, b, g_c summed over the kGrp partial
@@ -1346,8 +1356,8 @@ struct MfDims {
 // in K5's LDS: >= 0 a column-major position of M (bit 30: + lambda after the sum), -1 none (the
 // upper half of a diagonal block), -2 - i the i-th g_c.  Built on the host per problem.
 constexpr int kMfMapLambda = 1 << 30;
-inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, int* map) {
-    const int np = 6 * nf;
+inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, int* map, int np_target = 0) {
+    const int np = np_target > 0 ? np_target : 6 * nf;  // the b row (the template's NP)
     for (int pb = 0; pb < n_pb; ++pb)
         for (int k = 0; k < 36; ++k) {
             const int ra = k / 6, ca = k % 6, fa = pb_fa[pb], fb = pb_fb[pb];
@@ -1358,17 +1368,18 @@ inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, i
                 v = (6 * fa + ra) * kMfLd + 6 * fb + ca;  // S[6fa+ra][6fb+ca] -> its lower mirror
             map[36 * pb + k] = v;
         }
-    for (int i = 0; i < np; ++i) map[36 * n_pb + i] = i * kMfLd + np;  // b_i -> row NP, column i
-    for (int i = 0; i < np; ++i) map[36 * n_pb + np + i] = -2 - i;
+    for (int i = 0; i < 6 * nf; ++i) map[36 * n_pb + i] = i * kMfLd + np;  // b_i -> row NP, column i
+    for (int i = 0; i < 6 * nf; ++i) map[36 * n_pb + 6 * nf + i] = -2 - i;
 }
 
 // combine_system with the sums scattered straight into M (and g_c into gsh) by the map
 template <int NF>
 __device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
                                double lambda, int* fail) {
-    constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
+    constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;  // the template's (upper bound)
     constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
     const size_t L = sys_len(G);
+    const int ne = G.n_pb * 36 + 12 * G.n_free;  // this window's entries (batched: may be fewer)
     const int tid = threadIdx.x;
     double pa[16];
     int sing = 0;
@@ -1382,9 +1393,9 @@ __device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
-        dst[i] = e < NE ? Pr.dmap[e] : -1;
+        dst[i] = e < ne ? Pr.dmap[e] : -1;
 #pragma unroll
-        for (int x = 0; x < kGrp; ++x) v[i][x] = e < NE ? Wk.cpart[(size_t)x * L + e] : 0.0;
+        for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
@@ -1504,7 +1515,7 @@ __device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int 
 }
 
 template <int NF>
-__global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, Prob Pr, Work Wk, int combine) {
+__device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
     constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
     __shared__ __attribute__((aligned(16))) double M[NPP * kMfLd];
@@ -1531,8 +1542,8 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
         combine_mapped<NF>(G, Pr, Wk, M, gsh, st->lambda, &fail);
     } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
         const double* sys = Wk.sys;
-        constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
-        for (int e = tid; e < NE; e += kK5Threads) {
+        const int ne = G.n_pb * 36 + 12 * nF;
+        for (int e = tid; e < ne; e += kK5Threads) {
             const int d = Pr.dmap[e];
             if (d >= 0)
                 M[d & (kMfMapLambda - 1)] = sys[e];
@@ -1540,6 +1551,14 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
                 gsh[-2 - d] = sys[e];
         }
         if (tid == 0) fail = sys[SC0 + 1] != 0.0;
+    }
+    if (n < NP) {
+        // a window with fewer free keyframes than the template (batched mode): its rows and
+        // columns [n, NP) are identity padding, and the b row is zero there
+        for (int e = tid; e < NP * (NP + 1); e += kK5Threads) {
+            const int c = e / (NP + 1), r = e - c * (NP + 1);
+            if (r >= c && ((r >= n && r < NP) || (c >= n && c < NP))) M[c * kMfLd + r] = r == c ? 1.0 : 0.0;
+        }
     }
     __syncthreads();
     STAMP(1);
@@ -1576,6 +1595,11 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
     STAMP(3);
     k5_finish<NF>(G, Wk, Up, lane < n ? yv : 0.0, gcl_v, n, lane, p7, fidx);
     RTSTAMP(5);
+}
+
+template <int NF>
+__global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, Prob Pr, Work Wk, int combine) {
+    camera_solve_mfma_body<NF>(G, Pr, Wk, combine);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2025,6 +2049,60 @@ __global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk,
         __hip_atomic_store(htick, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     STAMP(10);
+}
+
+// ---------------------------------------------------------------------------------------
+// Batched mode (SURVEY 8d "expected regime"): B independent windows solved by ONE launch chain --
+// the window is the grid's y dimension of every LM kernel (K4, then per iteration K4c, K5, K6, and
+// K7 per chunk), each block reads its window's descriptor (geometry, problem and the four state
+// views) from a device table.  Grids are as wide as the widest window; a block past its window's
+// waves / chunks, or of a window that is skipped or has terminated, returns at once.  Every window
+// takes exactly the single-window operations, so its result equals its own solve bit for bit.
+// ---------------------------------------------------------------------------------------
+struct WinDesc {
+    Geometry G;
+    Prob Pr;
+    Work W[4];  // work(0), work(1) (iteration parity), work_at(0), work_at(1)
+    int skip;
+};
+
+__global__ __launch_bounds__(64) void bab_linearize(const WinDesc* __restrict__ D, double lambda0) {
+    const WinDesc& d = D[blockIdx.y];
+    if (d.skip || (int)blockIdx.x >= d.G.n_wave) return;
+    linearize_body(d.G, d.Pr, d.W[2], blockIdx.x, 1, lambda0);
+}
+
+__global__ __launch_bounds__(kSchurThreads) void bab_schur_chunks(const WinDesc* __restrict__ D, int wi, LmArgs la) {
+    const WinDesc& d = D[blockIdx.y];
+    if (d.skip || (int)blockIdx.x >= d.G.n_chunk) return;
+    schur_chunks_body(d.G, d.Pr, d.W[wi], la, 0, blockIdx.x);
+}
+
+template <int NF>
+__global__ __launch_bounds__(kK5Threads) void bab_camera_solve(const WinDesc* __restrict__ D, int wi) {
+    const WinDesc& d = D[blockIdx.x];
+    if (d.skip) return;
+    camera_solve_mfma_body<NF>(d.G, d.Pr, d.W[wi], 1);
+}
+
+__global__ __launch_bounds__(64) void bab_backsub_relinearize(const WinDesc* __restrict__ D, int wi) {
+    const WinDesc& d = D[blockIdx.y];
+    if (d.skip || (int)blockIdx.x >= d.G.n_wave) return;
+    __shared__ double sh[10][64];
+    __shared__ double shp[3][64];
+    __shared__ double shs[4][64];
+    k6_body<false>(d.G, d.Pr, d.W[wi], blockIdx.x, threadIdx.x, sh, shp, shs);
+}
+
+// K7 per window: the pending decision in place and into the pinned host copy host[window]
+__global__ __launch_bounds__(64) void bab_lm_decide(const WinDesc* __restrict__ D, int wi, LmArgs la, LmState* host) {
+    const WinDesc& d = D[blockIdx.x];
+    if (d.skip) return;
+    const LmState s = lm_decide(d.G, d.Pr, d.W[wi], d.W[wi].st, 0, la);
+    if (threadIdx.x == 0) {
+        *d.W[wi].st = s;
+        host[blockIdx.x] = s;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2967,10 +3045,169 @@ struct BundleAdjuster {
     }
 };
 
+// Batched mode over B window handles (their problems uploaded by rsvio_ba_set_problem): one
+// launch chain on the batch's stream, the host reading the B LM states once per chunk.
+struct BundleBatch {
+    std::vector<BundleAdjuster*> win;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    DevBuf<WinDesc> d_desc;
+    HostBuf<WinDesc> h_desc;
+    HostBuf<LmState> h_states;
+    DevBuf<int> d_dmap;
+    HostBuf<int> h_dmap;
+    int last_iterations = 3;
+
+    void init(BundleAdjuster* const* w, int n) {
+        if (n < 1) throw std::invalid_argument("a batch needs at least one window");
+        for (int i = 0; i < n; ++i) {
+            if (!w[i]) throw std::invalid_argument("null window handle");
+            if (i && w[i]->P.device != w[0]->P.device) throw std::invalid_argument("windows on different devices");
+            if (w[i]->sharded()) throw std::invalid_argument("a sharded window cannot join a batch");
+            win.push_back(w[i]);
+        }
+        device = w[0]->P.device;
+        RSVIO_HIP(hipSetDevice(device));
+        RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        RSVIO_HIP(hipEventCreate(&ev0));
+        RSVIO_HIP(hipEventCreate(&ev1));
+        d_desc.alloc(n);
+        h_desc.alloc(n);
+        h_states.alloc(n, hipHostMallocCoherent);
+    }
+    ~BundleBatch() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    void launch_k5(int nf, int wi) {
+        const int B = (int)win.size();
+        switch (nf) {
+#define RSVIO_BAB(NF) \
+    case NF: hipLaunchKernelGGL(bab_camera_solve<NF>, dim3(B), dim3(kK5Threads), 0, stream, d_desc.p, wi); break;
+            RSVIO_BAB(1) RSVIO_BAB(2) RSVIO_BAB(3) RSVIO_BAB(4) RSVIO_BAB(5)
+            RSVIO_BAB(6) RSVIO_BAB(7) RSVIO_BAB(8) RSVIO_BAB(9) RSVIO_BAB(10)
+#undef RSVIO_BAB
+            default: throw std::invalid_argument("batched mode: at most 10 free keyframes per window");
+        }
+        RSVIO_HIP(hipGetLastError());
+    }
+
+    void run(const rsvio_lm_cfg& cfg, rsvio_ba_result* res) {
+        const int B = (int)win.size();
+        int nf = 1, max_wave = 1, max_chunk = 1, active = 0;
+        std::vector<int> skip(B, 0);
+        size_t ne_total = 0;
+        for (int i = 0; i < B; ++i) {
+            BundleAdjuster& w = *win[i];
+            w.require_idle("rsvio_ba_batch_run");
+            if (!w.has_problem) throw std::invalid_argument("batch window without a problem");
+            const Geometry& G = w.G;
+            // sliding_window.rs:303-319 guards, as the single-window start()
+            skip[i] = (G.n_obs < 6 || G.n_obs < G.n_kf + G.n_lm || G.n_wave == 0) ? 1 : 0;
+            if (skip[i]) continue;
+            ++active;
+            nf = std::max(nf, G.n_free);
+            max_wave = std::max(max_wave, G.n_wave);
+            max_chunk = std::max(max_chunk, G.n_chunk);
+            ne_total += (size_t)36 * G.n_pb + 12 * G.n_free;
+        }
+        if (nf > 10) throw std::invalid_argument("batched mode: at most 10 free keyframes per window");
+        max_wave = (max_wave + kGrp - 1) / kGrp * kGrp;  // wave w on XCD w % 8 in every window
+        // descriptors and the camera-solve maps for the batch's template (b row at 6 nf)
+        if (h_dmap.n < std::max<size_t>(ne_total, 1)) {
+            h_dmap.alloc(ne_total + 1);
+            d_dmap.alloc(ne_total + 1);
+        }
+        size_t off = 0;
+        for (int i = 0; i < B; ++i) {
+            BundleAdjuster& w = *win[i];
+            WinDesc& d = h_desc.p[i];
+            d.skip = skip[i];
+            d.G = w.G;
+            d.G.huber_delta = cfg.huber_delta;
+            d.G.chol = cfg.linear_solver == RSVIO_SOLVER_CHOLESKY ? 1 : 0;
+            d.Pr = w.prob();
+            d.W[0] = w.work(0);
+            d.W[1] = w.work(1);
+            d.W[2] = w.work_at(0);
+            d.W[3] = w.work_at(1);
+            if (skip[i]) continue;
+            const size_t ne = (size_t)36 * w.G.n_pb + 12 * w.G.n_free;
+            mf_dense_map(w.G.n_free, w.G.n_pb, w.hs_pb_fa.data(), w.hs_pb_fb.data(), h_dmap.p + off, 6 * nf);
+            d.Pr.dmap = d_dmap.p + off;
+            off += ne;
+        }
+        for (int i = 0; i < B; ++i) {
+            if (skip[i]) {
+                res[i] = rsvio_ba_result{};
+                res[i].status = RSVIO_LM_SKIPPED;
+            }
+        }
+        if (!active) return;
+        RSVIO_HIP(hipMemcpyAsync(d_dmap.p, h_dmap.p, sizeof(int) * std::max<size_t>(off, 1), hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipMemcpyAsync(d_desc.p, h_desc.p, sizeof(WinDesc) * B, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipEventRecord(ev0, stream));
+        hipLaunchKernelGGL(bab_linearize, dim3(max_wave, B), dim3(64), 0, stream, d_desc.p, cfg.lambda_init);
+        RSVIO_HIP(hipGetLastError());
+        const LmArgs la{cfg.max_iterations, cfg.cost_tolerance, cfg.parameter_tolerance};
+        const int max_it = std::max(cfg.max_iterations, 1);
+        int enq = 0;
+        int k = std::min(std::max(last_iterations, 1), max_it);
+        int max_iter_seen = 0;
+        while (true) {
+            for (int i = 0; i < k; ++i, ++enq) {
+                const int wi = enq & 1;
+                hipLaunchKernelGGL(bab_schur_chunks, dim3(max_chunk, B), dim3(kSchurThreads), 0, stream, d_desc.p, wi, la);
+                RSVIO_HIP(hipGetLastError());
+                launch_k5(nf, wi);
+                hipLaunchKernelGGL(bab_backsub_relinearize, dim3(max_wave, B), dim3(64), 0, stream, d_desc.p, wi);
+                RSVIO_HIP(hipGetLastError());
+            }
+            hipLaunchKernelGGL(bab_lm_decide, dim3(B), dim3(64), 0, stream, d_desc.p, 2 + (enq & 1), la, h_states.p);
+            RSVIO_HIP(hipGetLastError());
+            RSVIO_HIP(hipEventRecord(ev1, stream));
+            RSVIO_HIP(hipStreamSynchronize(stream));
+            bool all_done = true;
+            for (int i = 0; i < B; ++i)
+                if (!skip[i]) {
+                    all_done = all_done && h_states.p[i].done;
+                    max_iter_seen = std::max(max_iter_seen, h_states.p[i].iter);
+                }
+            if (all_done || enq >= max_it) break;
+            k = std::min(2, max_it - enq);
+        }
+        float ms = 0.0f;
+        RSVIO_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+        last_iterations = std::max(max_iter_seen, 1);
+        for (int i = 0; i < B; ++i) {
+            if (skip[i]) continue;
+            BundleAdjuster& w = *win[i];
+            const LmState& st = h_states.p[i];
+            *w.h_state.p = st;
+            w.state_fresh = false;
+            w.settled = true;
+            w.last_iterations = st.iter;
+            res[i].status = st.status;
+            res[i].iterations = st.iter;
+            res[i].initial_cost = st.initial_cost;
+            res[i].final_cost = st.cost;
+            res[i].solve_ms = ms;
+        }
+    }
+};
+
 }  // namespace rsvio
 
 struct rsvio_ba {
     rsvio::BundleAdjuster b;
+};
+
+struct rsvio_ba_batch {
+    rsvio::BundleBatch b;
 };
 
 using rsvio::guarded;
@@ -3084,6 +3321,33 @@ int rsvio_ba_build_system(rsvio_ba* ba, double lambda, double huber_delta, doubl
         return (int)RSVIO_OK;
     });
 }
+
+int rsvio_ba_batch_create(rsvio_ba* const* windows, int32_t n, rsvio_ba_batch** out) {
+    if (!windows || n < 1 || !out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        std::vector<rsvio::BundleAdjuster*> w(n);
+        for (int i = 0; i < n; ++i) w[i] = windows[i] ? &windows[i]->b : nullptr;
+        auto* h = new rsvio_ba_batch();
+        try {
+            h->b.init(w.data(), n);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_batch_run(rsvio_ba_batch* batch, const rsvio_lm_cfg* cfg, rsvio_ba_result* results) {
+    if (!batch || !cfg || !results) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        batch->b.run(*cfg, results);
+        return (int)RSVIO_OK;
+    });
+}
+
+void rsvio_ba_batch_destroy(rsvio_ba_batch* batch) { delete batch; }
 
 int rsvio_rccl_unique_id(uint8_t* out, size_t cap) {
     if (!out || cap < sizeof(ncclUniqueId)) return RSVIO_ERR_INVALID_ARG;

@@ -135,6 +135,9 @@ SIG = {
     "rsvio_ba_run": (C.c_int, [P, C.POINTER(LmCfg), C.POINTER(BaResult)]),
     "rsvio_ba_run_async": (C.c_int, [P, C.POINTER(LmCfg)]),
     "rsvio_ba_set_stream": (C.c_int, [P, P]),
+    "rsvio_ba_batch_create": (C.c_int, [P, C.c_int32, C.POINTER(P)]),
+    "rsvio_ba_batch_run": (C.c_int, [P, C.POINTER(LmCfg), P]),
+    "rsvio_ba_batch_destroy": (None, [P]),
     "rsvio_ba_p2p_export": (C.c_int, [P, C.c_int32, C.POINTER(C.c_uint8), C.c_size_t]),
     "rsvio_ba_attach_p2p": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
     "rsvio_ba_detach_p2p": (C.c_int, [P]),

@@ -221,6 +221,34 @@ def se3_matrix(p7) -> np.ndarray:
     return T
 
 
+class BundleBatch:
+    """Batched mode (rsvio_ba_batch_*): the problems of several BundleAdjuster handles solved by
+    one launch chain; run() returns one BaResult per window, state() is read on each handle."""
+
+    def __init__(self, adjusters):
+        self.adjusters = list(adjusters)
+        arr = (C.c_void_p * len(self.adjusters))(*[a._h.value for a in self.adjusters])
+        h = C.c_void_p()
+        check(_lib.load().rsvio_ba_batch_create(arr, len(self.adjusters), C.byref(h)))
+        self._h = h
+
+    def run(self, cfg=None):
+        res = (_lib.BaResult * len(self.adjusters))()
+        check(_lib.load().rsvio_ba_batch_run(self._h, C.byref(cfg or lm_cfg()), res))
+        return list(res)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().rsvio_ba_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SlidingWindow:
     """Keyframe FIFO + BA problem assembly (sliding_window.rs:21-486) over the GPU solver."""
 

@@ -480,3 +480,38 @@ def test_singular_landmark_block_linear_solve_failed(gpu, oracle):
     _, _, ro = oracle.ba_solve(prob, oracle.lm_cfg())
     assert r.status > 0 and (r.status, r.iterations) == (ro.status, ro.iterations)
     ba.close()
+
+
+def test_batched_windows_match_single_and_oracle(gpu, oracle):
+    """Batched mode (rsvio_ba_batch_*): ragged windows -- 2..11 keyframes, different landmark and
+    observation counts, one window the guards skip -- solved by one launch chain; every window
+    equals its own single-handle solve (status, iterations, state within 1e-10) and the oracle's
+    solve of it within the stated tolerances."""
+    from rsvio import synthetic as S
+    from rsvio.ba import BundleAdjuster, BundleBatch
+    shapes = [(3, 60, 2), (5, 150, 4), (8, 300, 5), (10, 2000, 6), (11, 400, 6), (4, 90, 3), (2, 1, 1)]
+    probs = [S.ba_problem(n_kf=k, n_lm=m, kf_per_lm=p, seed=500 + i, init_seed=600 + i)
+             for i, (k, m, p) in enumerate(shapes)]
+    wins = [_adjuster(gpu, pr) for pr in probs]
+    batch = BundleBatch(wins)
+    for rep in range(2):                     # twice: the second run re-uses the chunk size
+        for w, pr in zip(wins, probs):
+            w.set_problem_from(pr)
+        res = batch.run()
+        for i, (w, pr, r) in enumerate(zip(wins, probs, res)):
+            if i == len(probs) - 1:
+                assert r.status == -2        # too few residuals: skipped
+                continue
+            pose, pw = w.state()
+            one = _adjuster(gpu, pr)
+            r1 = one.run()
+            p1, w1 = one.state()
+            one.close()
+            assert (r.status, r.iterations) == (r1.status, r1.iterations), i
+            assert np.abs(pose - p1).max() <= 1e-10 and np.abs(pw - w1).max() <= 1e-10, i
+            po, pwo, ro = oracle.ba_solve(pr)
+            assert r.status == ro.status and r.iterations == ro.iterations, i
+            assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6, i
+    batch.close()
+    for w in wins:
+        w.close()
