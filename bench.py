@@ -689,21 +689,26 @@ class TrackerWorkload:
         self.h_out = torch.empty(self.out.shape, dtype=self.out.dtype).pin_memory()
         self.h_valid = torch.empty(self.valid.shape, dtype=self.valid.dtype).pin_memory()
 
-    def step(self, timed: bool, pcie: bool = False, wait: bool = True):
-        """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches.  pcie:
-        the two images are uploaded from pinned host memory first and the three tracked
-        feature lists (+ valid flags) are downloaded before the step returns (wait=False: they
-        are enqueued and sync() completes the frame)."""
-        C = self.C
-        t = self.seq[self.k % len(self.seq)]
-        t2 = self.seq[(self.k + 1) % len(self.seq)]
-        prev, cur = self.slot, 1 - self.slot
-        if pcie:
-            with self.torch.cuda.stream(self.stream):
-                self.d_stage.copy_(self.h_imgs[t2], non_blocking=True)
-            self._pyramids(t2, cur, self.d_stage)
-        else:
-            self._pyramids(t2, cur)
+    def _plan(self, phase: int, pcie: bool):
+        """The C arguments of one step, built once per (phase of the frame sequence, pcie): the
+        sequence has period len(seq) (even, so the pyramid slot parity repeats with it).  A Rust
+        caller passes these as they are; building ctypes structures and taking tensor pointers
+        costs tens of microseconds of Python per step, which is harness overhead, not tracker
+        work.  The copies go through the HIP runtime the library is bound to (hipMemcpyAsync on
+        the tracker stream)."""
+        key = (phase, pcie)
+        plan = self._plans.get(key) if hasattr(self, "_plans") else None
+        if plan is not None:
+            return plan
+        if not hasattr(self, "_plans"):
+            self._plans = {}
+            C = self.C
+            self._memcpy = self.lib.hipMemcpyAsync
+            self._memcpy.restype = C.c_int
+            self._memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        t = self.seq[phase]
+        t2 = self.seq[(phase + 1) % len(self.seq)]
+        prev, cur = phase % 2, 1 - phase % 2
         b = (self.L.TrackBatch * 3)()
         spec = [(self.pyr[prev, 0], self.pyr[cur, 0], self.aff0[t]),
                 (self.pyr[prev, 1], self.pyr[cur, 1], self.aff1[t]),
@@ -711,21 +716,40 @@ class TrackerWorkload:
         for i, (p0, p1, a) in enumerate(spec):
             b[i] = self.L.TrackBatch(p0.data_ptr(), p1.data_ptr(), a.data_ptr(), self.out[i].data_ptr(),
                                      self.valid[i].data_ptr(), NFEAT)
+        src = self.d_stage if pcie else self.imgs[t2]
+        plan = {"batches": b, "src": src.data_ptr(), "dst": self.pyr[cur].data_ptr(),
+                "h_img": self.h_imgs[t2].data_ptr() if pcie else None, "img_bytes": src.numel()}
+        self._plans[key] = plan
+        return plan
+
+    def step(self, timed: bool, pcie: bool = False, wait: bool = True):
+        """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches.  pcie:
+        the two images are uploaded from pinned host memory first and the three tracked
+        feature lists (+ valid flags) are downloaded before the step returns (wait=False: they
+        are enqueued and sync() completes the frame)."""
+        C = self.C
+        phase = self.k % len(self.seq)
+        assert self.slot == phase % 2
+        plan = self._plan(phase, pcie)
+        s = self.stream.cuda_stream
+        if pcie:
+            self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, s))
+        self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, plan["src"], 2, plan["dst"], s))
+        timed = timed and self.k % 4 == 0  # LK launch time sampled on every 4th frame (event overhead)
         if timed:
             e0 = self.torch.cuda.Event(enable_timing=True)
             e1 = self.torch.cuda.Event(enable_timing=True)
             e0.record(self.stream)
-        self.L.check(self.lib.rsvio_track_points_d(self.ctx, b, 3, MAX_IT, C.c_float(THRESH), self.stream.cuda_stream))
+        self.L.check(self.lib.rsvio_track_points_d(self.ctx, plan["batches"], 3, MAX_IT, C.c_float(THRESH), s))
         if timed:
             e1.record(self.stream)
             self.ev.append((e0, e1))
         if pcie:
-            with self.torch.cuda.stream(self.stream):
-                self.h_out.copy_(self.out, non_blocking=True)
-                self.h_valid.copy_(self.valid, non_blocking=True)
+            self.L.check(self._memcpy(self.h_out.data_ptr(), self.out.data_ptr(), self.out.numel() * 4, 2, s))
+            self.L.check(self._memcpy(self.h_valid.data_ptr(), self.valid.data_ptr(), self.valid.numel(), 2, s))
             if wait:
                 self.stream.synchronize()
-        self.slot = cur
+        self.slot = 1 - self.slot
         self.k += 1
 
     def sync(self):
@@ -1032,15 +1056,18 @@ def main():
         ba.finish(timed)
 
     def protocol_step(timed):
-        """BASELINE.md protocol step: the frame's 2 images go up from pinned host memory, the
-        tracker is enqueued (pyramids, LK, the three feature lists + valid flags back to pinned
-        host memory); meanwhile the host uploads the new keyframe window (rsvio_ba_set_problem:
-        observation sort, slot / pair tables, pinned staging, H2D) and starts its solve (graph
-        re-capture + launch); then the frame's features, the solve and its optimised state
-        (48.6 KB D2H) are waited for."""
-        trk.step(timed, pcie=True, wait=False)
+        """BASELINE.md protocol step, pipelined as the config-4 Estimator is (a keyframe's solve
+        overlaps the next frame's tracking; resident_step has the same order): the host uploads
+        a new keyframe window (rsvio_ba_set_problem: validation, per-landmark masks, wave
+        packing, pinned staging, one H2D copy, slot headers and pair lists built on the device)
+        and starts its solve (graph re-capture + launch); meanwhile the frame's 2 images go up
+        from pinned host memory and the tracker is enqueued (pyramids, LK, the three feature
+        lists + valid flags back to pinned host memory); then the frame's features, the solve
+        and its optimised state (48.6 KB, published to pinned host memory with the solve's last
+        decision) are waited for."""
         ba.next_window()
         ba.start()
+        trk.step(timed, pcie=True, wait=False)
         trk.sync()
         ba.finish(timed)
         ba.ba.state()

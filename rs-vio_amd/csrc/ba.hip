@@ -415,6 +415,65 @@ __device__ __forceinline__ int pair_partner(const int4 h0, const int4 h1, int fa
     return partner;
 }
 
+// The padded slot layout of a problem, built on the device from what set_problem uploads: per
+// landmark the (keyframe, camera) bit mask (bit 2 kf + cam) and the padded position of its first
+// slot (the host's greedy wave packing), per wave its real slot count, per observation its packed
+// key and (u, v).  A landmark's slots are its keyframes in ascending order; a slot's observations
+// are camera 0 then camera 1 -- the layout of a stable (landmark, keyframe, camera) sort.
+struct SlotSrc {
+    const unsigned long long* mask;  // n_lm
+    const int* lm_base;              // n_lm: padded slot of the landmark's first slot, -1 unobserved
+    const int* wave_fill;            // n_wave: real slots of the wave (the rest are padding lanes)
+    const unsigned* key;             // n_obs: landmark << 6 | kf << 1 | cam
+    const double2* uv;               // n_obs
+    int nb_lm, nb_pad;               // blocks of the landmark and padding parts of the grid
+};
+constexpr unsigned long long kEvenBits = 0x5555555555555555ull;
+
+// blocks [0, nb_lm): one thread per landmark -- its slot headers {kf, landmark, lane of the
+// landmark's first slot, slots of the landmark} {free block of kf or -1, observations, camera
+// bits, 0}; [nb_lm, nb_lm + nb_pad): one thread per padded slot -- the waves' padding lanes
+// {0, 0, 0, 0} {-1, 0, 0, 0} with zero observations; the rest: one thread per observation -- its
+// (u, v) into its slot (first = camera 0 if present, second = camera 1; an absent second zero).
+__global__ __launch_bounds__(256) void ba_build_slots(Geometry G, Prob Pr, SlotSrc S, int4* hdr, double2* huv) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const double2 z2 = make_double2(0.0, 0.0);
+    if (b < S.nb_lm) {
+        const int l = 256 * b + t;
+        if (l >= G.n_lm) return;
+        const int base = S.lm_base[l];
+        if (base < 0) return;
+        const unsigned long long m = S.mask[l];
+        unsigned long long kb = (m | (m >> 1)) & kEvenBits;
+        const int ns = __popcll(kb);
+        for (size_t ps = (size_t)base; kb; kb &= kb - 1, ++ps) {
+            const int k = (__ffsll((long long)kb) - 1) >> 1;
+            const int c0 = (int)(m >> (2 * k)) & 1, c1 = (int)(m >> (2 * k + 1)) & 1;
+            const int no = c0 + c1;
+            hdr[2 * ps] = make_int4(k, l, base & 63, ns);
+            hdr[2 * ps + 1] = make_int4(Pr.free_idx[k], no, no == 2 ? 2 : c1, 0);
+            if (no == 1) huv[2 * ps + 1] = z2;
+        }
+    } else if (b < S.nb_lm + S.nb_pad) {
+        const int ps = 256 * (b - S.nb_lm) + t;
+        if (ps >= 64 * G.n_wave || (ps & 63) < S.wave_fill[ps >> 6]) return;
+        hdr[2 * (size_t)ps] = make_int4(0, 0, 0, 0);
+        hdr[2 * (size_t)ps + 1] = make_int4(-1, 0, 0, 0);
+        huv[2 * (size_t)ps] = z2;
+        huv[2 * (size_t)ps + 1] = z2;
+    } else {
+        const int i = 256 * (b - S.nb_lm - S.nb_pad) + t;
+        if (i >= G.n_obs) return;
+        const unsigned key = S.key[i];
+        const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
+        const unsigned long long m = S.mask[l];
+        const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
+        const size_t q = (size_t)S.lm_base[l] + __popcll(below);
+        const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
+        huv[2 * q + sub] = S.uv[i];
+    }
+}
+
 __global__ __launch_bounds__(256) void ba_build_pairs(Geometry G, Prob Pr, int4* pairs) {
     __shared__ int sh[4][64];
     __shared__ int cnt[4];
@@ -2033,14 +2092,34 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 // directly (system-scope release), so no copy follows the solve on the stream
 // host: the pinned LmState copy; htick (pinned, fine-grained): [1] solve start, [2] this
 // decision's wall clock, then [0] = the decision's ticket, a system-scope release the host polls
-// (rsvio_ba_wait returns on it, before the kernel's end-of-kernel signal).
-__global__ __launch_bounds__(64) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
-                                                   LmState* host, unsigned long long* htick) {
+// (rsvio_ba_wait returns on it, before the kernel's end-of-kernel signal).  hout (pinned,
+// fine-grained, or null): when the decision ends the solve, the whole block first copies the
+// optimised state -- poses then points of the current buffers -- into it, so the ticket also
+// publishes what rsvio_ba_get_state returns (no stream sync and no copy after the solve).
+constexpr int kK7Threads = 256;
+__global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
+                                                           LmState* host, unsigned long long* htick, double* hout) {
     STAMP(8);
-    const LmState s = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
+    __shared__ LmState sd;
+    if (threadIdx.x < 64) {  // the decision by wave 0
+        const LmState d = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
+        if (threadIdx.x == 0) {
+            sd = d;
+            *Wk.st = d;
+            *host = d;
+        }
+    }
+    __syncthreads();
+    const LmState s = sd;
+    if (hout && s.done) {
+        const double* pose = Wk.pose[s.cur];
+        const double* pw = Wk.pw[s.cur];
+        const int np = 7 * G.n_kf, n = np + 3 * G.n_lm;
+        for (int i = threadIdx.x; i < n; i += kK7Threads) hout[i] = i < np ? pose[i] : pw[i - np];
+        __threadfence_system();
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        *Wk.st = s;
-        *host = s;
         const unsigned long long t = Wk.tick[0] + 1;
         Wk.tick[0] = t;
         htick[1] = Wk.tick[1];
@@ -2213,6 +2292,11 @@ RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 RSVIO_RT_READER(rsvio_dbg_ba_rt)
 
 // ======================================================================================
+// slots of a landmark = keyframes with any of its observations (bits 2 kf, 2 kf + 1 of its mask)
+__attribute__((target("popcnt"))) static inline int slot_count(unsigned long long m) {
+    return __builtin_popcountll((m | (m >> 1)) & kEvenBits);
+}
+
 struct BundleAdjuster {
     rsvio_ba_params P{};
     hipStream_t stream = nullptr;
@@ -2231,15 +2315,27 @@ struct BundleAdjuster {
     bool graphs_ok = true;
     int k5_variant = 2;  // camera solve for n_free <= 10: 2 blocked LDL^T with MFMA trailing updates (default),
                          // 0 pipelined 4-wave LDL^T (RSVIO_K5=pipe4), 1 one-wave Gauss-Jordan (gj1)
-    // an exec whose launch may still run is never destroyed: the stream settles first (a ticket
-    // wait returns before the last decision kernel has exited)
+    // an exec whose launch may still run is never destroyed (a ticket wait returns before the
+    // last decision kernel has exited): unless the stream is idle (known, or queried without
+    // waiting) it is retired and destroyed once it is -- set_problem need not wait for the stream
+    std::vector<hipGraphExec_t> retired;
     void drop_graph() {
         if (gexec) {
-            settle();
-            (void)hipGraphExecDestroy(gexec);
+            if (!settled && hipStreamQuery(stream) == hipSuccess) settled = true;
+            if (settled) {
+                destroy_retired();
+                (void)hipGraphExecDestroy(gexec);
+            } else {
+                retired.push_back(gexec);
+                if (retired.size() > 4) settle();  // bounded: wait for the stream then
+            }
         }
         gexec = nullptr;
         g_k = -1;
+    }
+    void destroy_retired() {
+        for (hipGraphExec_t g : retired) (void)hipGraphExecDestroy(g);
+        retired.clear();
     }
     static bool same_cfg(const rsvio_lm_cfg& a, const rsvio_lm_cfg& b) {
         return a.max_iterations == b.max_iterations && a.cost_tolerance == b.cost_tolerance &&
@@ -2250,7 +2346,8 @@ struct BundleAdjuster {
     // device; RCCL calls stay out of the graph)
     bool start_graph(const rsvio_lm_cfg& cfg, int k) {
         if (coll == 1 || !graphs_ok) return false;
-        if (!(gexec && g_k == k && same_cfg(g_cfg, cfg))) {
+        if (!(gexec && g_k == k && same_cfg(g_cfg, cfg) && g_export == export_on)) {
+            const auto tg0 = std::chrono::steady_clock::now();
             drop_graph();
             if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
                 (void)hipGetLastError();
@@ -2267,11 +2364,18 @@ struct BundleAdjuster {
             }
             hipGraph_t g = nullptr;
             if (hipStreamEndCapture(stream, &g) != hipSuccess) ok = false;
+            const auto tg1 = std::chrono::steady_clock::now();
             if (ok && hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess) {
                 gexec = nullptr;
                 ok = false;
             }
+            const auto tg2 = std::chrono::steady_clock::now();
             if (g) (void)hipGraphDestroy(g);
+            if (prof_env)
+                fprintf(stderr, "[rsvio] graph us: drop+capture %.1f instantiate %.1f destroy %.1f\n",
+                        std::chrono::duration<double, std::micro>(tg1 - tg0).count(),
+                        std::chrono::duration<double, std::micro>(tg2 - tg1).count(),
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tg2).count());
             if (!ok) {
                 (void)hipGetLastError();
                 graphs_ok = false;
@@ -2279,6 +2383,7 @@ struct BundleAdjuster {
             }
             g_k = k;
             g_cfg = cfg;
+            g_export = export_on;
         }
         RSVIO_HIP(hipGraphLaunch(gexec, stream));
         return true;
@@ -2294,13 +2399,20 @@ struct BundleAdjuster {
     hipEvent_t ev_up = nullptr;
     bool up_pending = false;
     struct ArenaLayout {
-        size_t pose_init, pw_init, free_idx, hdr, uv, pairs, pb_fa, pb_fb, dmap, total;
+        size_t pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, key, ouv, upload;
+        size_t hdr, uv, pairs, total;  // built on the device
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
+    // the optimised state of the last solve, written by its final decision kernel (K7) before the
+    // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
+    // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
+    // caller that never reads the state back (re-solving a resident window) pays nothing for it
+    HostBuf<double> h_out;
+    bool state_export = false, export_on = false;
+    bool g_export = false;  // export_on of the captured graph
     bool state_fresh = false;  // set_problem without a run since: get_state resets the buffers first
     // host scratch of set_problem, kept across problems (no per-problem allocations)
-    std::vector<int> hs_free, hs_cnt, hs_order, hs_slot_kf, hs_slot_lm, hs_slot_obs, hs_lm_slot, hs_wave_slot,
-        hs_pslot, hs_lm_group, hs_pb_of, hs_pb_fa, hs_pb_fb;
+    std::vector<int> hs_free, hs_pb_fa, hs_pb_fb;
     DevBuf<double> d_raws, d_rawl, d_partA, d_partD, d_cpart, d_sys, d_dc, d_trial4;
     DevBuf<int> d_singular;
     size_t n_pad = 0;
@@ -2326,14 +2438,16 @@ struct BundleAdjuster {
 
     void init(const rsvio_ba_params& p) {
         P = p;
-        if (P.max_keyframes < 2 || P.max_keyframes > kMaxFree + 1 || P.max_landmarks < 1 || P.max_observations < 1)
-            throw std::invalid_argument("invalid BA capacities (max_keyframes in [2, 21])");
+        if (P.max_keyframes < 2 || P.max_keyframes > kMaxFree + 1 || P.max_landmarks < 1 ||
+            P.max_landmarks > (1 << 26) || P.max_observations < 1)
+            throw std::invalid_argument("invalid BA capacities (max_keyframes in [2, 21], max_landmarks <= 2^26)");
         RSVIO_HIP(hipSetDevice(P.device));
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_up, hipEventDisableTiming));
         h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
+        h_out.alloc((size_t)7 * P.max_keyframes + (size_t)3 * P.max_landmarks, hipHostMallocCoherent);
         d_tick.alloc(2);
         RSVIO_HIP(hipMemset(d_tick.p, 0, 2 * sizeof(unsigned long long)));
         RSVIO_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_tick), 4 * sizeof(unsigned long long),
@@ -2359,6 +2473,7 @@ struct BundleAdjuster {
         settled = true;
         if (h_tick) (void)hipHostFree(h_tick);
         drop_graph();
+        destroy_retired();
         if (comm) ncclCommDestroy(comm);
         for (int r = 0; r < kP2PMax; ++r)
             if (p2p_opened[r]) (void)hipIpcCloseMemHandle(p2p.peer[r]);
@@ -2409,11 +2524,15 @@ struct BundleAdjuster {
         return w;
     }
 
-    // sliding_window.rs:159-299 problem assembly, restated for the device layout (see Prob).  The
-    // host work is linear in the observations (counting sort by landmark, then each landmark's few
-    // (keyframe, camera) entries by insertion), written straight into the pinned staging image;
-    // no kernel and no stream synchronisation: the initial state is set by the solve's first
-    // kernel (K4 with K0 folded in).
+    // sliding_window.rs:159-299 problem assembly, restated for the device layout (see Prob).  No
+    // sort: one pass over the observations validates them, sets a bit per (keyframe, camera) in a
+    // 64-bit mask per landmark (n_kf <= 21) and packs each observation's key, all straight into
+    // the pinned staging image; one pass over the landmarks packs whole landmarks into waves
+    // (greedy, <= 64 slots).  The mask fixes the landmark's slots (its keyframes, ascending), each
+    // slot's observations and camera bits, and every observation's place in its slot, so the slot
+    // headers and the (u, v) layout are written on the device (ba_build_slots) after one H2D copy,
+    // then the Schur pair lists (ba_build_pairs).  No stream synchronisation: the initial state is
+    // set by the solve's first kernel (K4 with K0 folded in).
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
@@ -2427,10 +2546,12 @@ struct BundleAdjuster {
             tms[ntm++] = std::chrono::duration<double, std::micro>(t - tp0).count();
             tp0 = t;
         };
-        require_idle("set_problem");
-        mark();
-        mark();
+        // no stream synchronisation: the staging image is guarded by ev_up, the device buffers by
+        // stream order (a buffer that grows is freed by hipFree, which waits for the device), and
+        // the previous solve's graph is retired until the stream is next settled
+        if (pend.active) throw CallOrderError("set_problem: a solve is in flight (call rsvio_ba_wait first)");
         drop_graph();  // kernel arguments (sizes, buffers) change with the problem
+        state_export = false;
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
             throw std::invalid_argument("problem exceeds the handle's capacities");
@@ -2441,171 +2562,127 @@ struct BundleAdjuster {
             if (!kf_fixed[k]) free_idx[k] = n_free++;
         if (n_free > kMaxFree) throw std::invalid_argument("too many free keyframes");
         if (n_free < 1) throw std::invalid_argument("no free keyframe");
-        // observations sorted by (landmark, keyframe, camera), stable: counting sort by landmark,
-        // then insertion sort of each landmark's entries
-        auto& cnt = hs_cnt;
-        cnt.assign((size_t)n_lm + 1, 0);
-        for (int i = 0; i < n_obs; ++i) {
-            if (obs_lm[i] < 0 || obs_lm[i] >= n_lm || obs_kf[i] < 0 || obs_kf[i] >= n_kf || obs_cam[i] > 1)
-                throw std::invalid_argument("observation index out of range");
-            cnt[obs_lm[i] + 1] += 1;
-        }
-        for (int l = 0; l < n_lm; ++l) cnt[l + 1] += cnt[l];
-        auto& order = hs_order;
-        order.resize(n_obs);
-        {
-            auto& cur = hs_lm_slot;  // scratch cursor
-            cur.assign(cnt.begin(), cnt.end() - 1);
-            for (int i = 0; i < n_obs; ++i) order[cur[obs_lm[i]]++] = i;
-        }
-        for (int l = 0; l < n_lm; ++l) {
-            const int a0 = cnt[l], a1 = cnt[l + 1];
-            for (int q = a0 + 1; q < a1; ++q) {
-                const int o = order[q];
-                const int key = 2 * obs_kf[o] + obs_cam[o];
-                int r = q;
-                while (r > a0 && 2 * obs_kf[order[r - 1]] + obs_cam[order[r - 1]] > key) {
-                    order[r] = order[r - 1];
-                    --r;
-                }
-                order[r] = o;
-            }
-        }
-        mark();
-        // slots: (landmark, keyframe) runs of 1-2 observations
-        auto &slot_kf = hs_slot_kf, &slot_lm = hs_slot_lm, &slot_obs = hs_slot_obs, &lm_slot = hs_lm_slot;
-        slot_kf.clear();
-        slot_lm.clear();
-        slot_obs.clear();
-        lm_slot.assign((size_t)n_lm + 1, 0);
-        for (int q = 0; q < n_obs; ++q) {
-            const int o = order[q];
-            if (q == 0 || obs_lm[o] != obs_lm[order[q - 1]] || obs_kf[o] != obs_kf[order[q - 1]]) {
-                slot_kf.push_back(obs_kf[o]);
-                slot_lm.push_back(obs_lm[o]);
-                slot_obs.push_back(q);
-                lm_slot[obs_lm[o] + 1] += 1;
-            }
-        }
-        const int n_slot = (int)slot_kf.size();
-        slot_obs.push_back(n_obs);
-        for (int l = 0; l < n_lm; ++l) lm_slot[l + 1] += lm_slot[l];
-        // waves: whole landmarks, <= 64 slots each (greedy)
-        auto& wave_slot = hs_wave_slot;
-        wave_slot.assign(1, 0);
-        for (int l = 0; l < n_lm; ++l) {
-            const int nk = lm_slot[l + 1] - lm_slot[l];
-            if (nk > 64) throw std::invalid_argument("a landmark is observed by more than 64 keyframes");
-            if (nk && lm_slot[l + 1] - wave_slot.back() > 64) wave_slot.push_back(lm_slot[l]);
-        }
-        if (n_slot > wave_slot.back()) wave_slot.push_back(n_slot);
-        const int n_wave = (int)wave_slot.size() - 1;
-        for (int sl = 0; sl < n_slot; ++sl)
-            if (slot_obs[sl + 1] - slot_obs[sl] > 2)
-                throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
-        mark();
         // camera blocks (fa <= fb)
-        auto &pb_fa = hs_pb_fa, &pb_fb = hs_pb_fb, &pb_of = hs_pb_of;
+        auto &pb_fa = hs_pb_fa, &pb_fb = hs_pb_fb;
         pb_fa.clear();
         pb_fb.clear();
-        pb_of.assign((size_t)n_free * n_free, -1);
         for (int a = 0; a < n_free; ++a)
             for (int b = a; b < n_free; ++b) {
-                pb_of[a * n_free + b] = (int)pb_fa.size();
                 pb_fa.push_back(a);
                 pb_fb.push_back(b);
             }
         const int n_pb = (int)pb_fa.size();
-        // XCD groups: wave w (K4 / K6 workgroup w, whole landmarks) is dispatched to XCD w % 8, so
-        // the landmarks of group x are those of the waves w % 8 == x; their Schur chunks run on
-        // XCD x too (chunk c on XCD c % 8) and re-read what K6 wrote there
-        auto& lm_group = hs_lm_group;
-        lm_group.assign(std::max(n_lm, 1), 0);
-        auto& pslot = hs_pslot;
-        pslot.resize(n_slot);
-        for (int w = 0; w < n_wave; ++w)
-            for (int sl = wave_slot[w]; sl < wave_slot[w + 1]; ++sl) {
-                lm_group[slot_lm[sl]] = w % kGrp;
-                pslot[sl] = 64 * w + (sl - wave_slot[w]);
-            }
-        // Schur chunk pairs: built on the device (ba_build_pairs) after the upload; the stride is
-        // the largest group's landmark count (at most one pair per landmark and chunk)
         const int n_chunk = kGrp * n_pb;
-        int stride = 1;
-        {
-            int gl[kGrp] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int l = 0; l < n_lm; ++l)
-                if (lm_slot[l + 1] > lm_slot[l]) gl[lm_group[l]] += 1;
-            for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
-        }
-        n_pad = (size_t)64 * n_wave;
-        mark();
-        // arena layout
+        // the uploaded part of the arena (sizes known before the passes)
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t nl1 = (size_t)std::max(n_lm, 1);
         ArenaLayout L{};
         size_t off = 0;
         L.pose_init = off; off += al(sizeof(double) * 7 * (size_t)n_kf);
-        L.pw_init = off;   off += al(sizeof(double) * 3 * (size_t)std::max(n_lm, 1));
+        L.pw_init = off;   off += al(sizeof(double) * 3 * nl1);
         L.free_idx = off;  off += al(sizeof(int) * (size_t)n_kf);
-        L.hdr = off;       off += al(sizeof(int4) * 2 * std::max<size_t>(n_pad, 1));
-        L.uv = off;        off += al(sizeof(double2) * 2 * std::max<size_t>(n_pad, 1));
         L.pb_fa = off;     off += al(sizeof(int) * (size_t)n_pb);
         L.pb_fb = off;     off += al(sizeof(int) * (size_t)n_pb);
         L.dmap = off;      off += al(sizeof(int) * ((size_t)36 * n_pb + 12 * n_free));
-        const size_t upload = off;  // everything before the pairs comes from the host
-        L.pairs = off;     off += al(sizeof(int4) * (size_t)n_chunk * stride);
-        L.total = off;
+        L.mask = off;      off += al(sizeof(unsigned long long) * nl1);
+        L.lm_base = off;   off += al(sizeof(int) * nl1);
+        L.wave_fill = off; off += al(sizeof(int) * nl1);  // n_wave <= n_lm
+        L.key = off;       off += al(sizeof(unsigned) * std::max(n_obs, 1));
+        L.ouv = off;       off += al(sizeof(double2) * std::max(n_obs, 1));
+        L.upload = off;
         if (up_pending) {  // the previous upload still reads the staging image
             RSVIO_HIP(hipEventSynchronize(ev_up));
             up_pending = false;
         }
-        if (h_arena.n < L.total) h_arena.alloc(L.total + L.total / 4);
+        if (h_arena.n < L.upload) h_arena.alloc(L.upload + L.upload / 4);
+        uint8_t* hb = h_arena.p;
+        mark();
+        // observations: validated, a (keyframe, camera) bit per landmark, packed keys
+        auto* m2 = reinterpret_cast<unsigned long long*>(hb + L.mask);
+        auto* key = reinterpret_cast<unsigned*>(hb + L.key);
+        std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
+        for (int i = 0; i < n_obs; ++i) {
+            const int l = obs_lm[i], k = obs_kf[i], c = obs_cam[i];
+            if (l < 0 || l >= n_lm || k < 0 || k >= n_kf || c > 1)
+                throw std::invalid_argument("observation index out of range");
+            const unsigned long long b = 1ull << (2 * k + c);
+            if (m2[l] & b)
+                throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
+            m2[l] |= b;
+            key[i] = (unsigned)l << 6 | (unsigned)k << 1 | (unsigned)c;
+        }
+        std::memcpy(hb + L.ouv, obs_uv, sizeof(double2) * (size_t)n_obs);
+        mark();
+        // waves: whole landmarks, <= 64 slots each (greedy, in landmark order); the Schur pair
+        // stride is the largest XCD group's landmark count (at most one pair per landmark and
+        // chunk).  Wave w (K4 / K6 workgroup w, whole landmarks) is dispatched to XCD w % 8, so
+        // the landmarks of group x are those of the waves w % 8 == x; their Schur chunks run on
+        // XCD x too (chunk c on XCD c % 8) and re-read what K6 wrote there.
+        auto* lm_base = reinterpret_cast<int*>(hb + L.lm_base);
+        auto* wave_fill = reinterpret_cast<int*>(hb + L.wave_fill);
+        int n_wave = 0, fill = 0;
+        int gl[kGrp] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int l = 0; l < n_lm; ++l) {
+            const int ns = slot_count(m2[l]);
+            if (!ns) {
+                lm_base[l] = -1;
+                continue;
+            }
+            if (n_wave == 0 || fill + ns > 64) {
+                if (n_wave) wave_fill[n_wave - 1] = fill;
+                ++n_wave;
+                fill = 0;
+            }
+            lm_base[l] = 64 * (n_wave - 1) + fill;
+            gl[(n_wave - 1) % kGrp] += 1;
+            fill += ns;
+        }
+        if (n_wave) wave_fill[n_wave - 1] = fill;
+        int stride = 1;
+        for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
+        n_pad = (size_t)64 * n_wave;
+        mark();
+        // device-built part of the arena
+        L.hdr = off;   off += al(sizeof(int4) * 2 * std::max<size_t>(n_pad, 1));
+        L.uv = off;    off += al(sizeof(double2) * 2 * std::max<size_t>(n_pad, 1));
+        L.pairs = off; off += al(sizeof(int4) * (size_t)n_chunk * stride);
+        L.total = off;
         if (d_arena.n < L.total) d_arena.alloc(L.total + L.total / 4);
         lay = L;
-        mark();
-        uint8_t* hb = h_arena.p;
         std::memcpy(hb + L.pose_init, pose7, sizeof(double) * 7 * (size_t)n_kf);
         if (n_lm) std::memcpy(hb + L.pw_init, pW, sizeof(double) * 3 * (size_t)n_lm);
         std::memcpy(hb + L.free_idx, free_idx.data(), sizeof(int) * (size_t)n_kf);
-        // padded slot layout (64 per wave): two int4 headers + 2 double2 observations per slot
-        // every entry written once, in order (real slots, then the wave's padding lanes)
-        int4* hdr = reinterpret_cast<int4*>(hb + L.hdr);
-        double2* huv = reinterpret_cast<double2*>(hb + L.uv);
-        for (int w = 0; w < n_wave; ++w) {
-            const int s0 = wave_slot[w], s1 = wave_slot[w + 1];
-            for (int sl = s0; sl < s1; ++sl) {
-                const size_t ps = (size_t)64 * w + (sl - s0);
-                const int l = slot_lm[sl];
-                const int no = slot_obs[sl + 1] - slot_obs[sl];
-                const int o0 = order[slot_obs[sl]], o1 = no > 1 ? order[slot_obs[sl] + 1] : o0;
-                hdr[2 * ps] = make_int4(slot_kf[sl], l, lm_slot[l] - s0, lm_slot[l + 1] - lm_slot[l]);
-                hdr[2 * ps + 1] = make_int4(free_idx[slot_kf[sl]], no, obs_cam[o0] | (no > 1 ? obs_cam[o1] << 1 : 0), 0);
-                huv[2 * ps] = make_double2(obs_uv[2 * (size_t)o0], obs_uv[2 * (size_t)o0 + 1]);
-                huv[2 * ps + 1] = no > 1 ? make_double2(obs_uv[2 * (size_t)o1], obs_uv[2 * (size_t)o1 + 1])
-                                         : make_double2(0.0, 0.0);
-            }
-            for (size_t ps = (size_t)64 * w + (s1 - s0); ps < (size_t)64 * (w + 1); ++ps) {
-                hdr[2 * ps] = make_int4(0, 0, 0, 0);
-                hdr[2 * ps + 1] = make_int4(-1, 0, 0, 0);
-                huv[2 * ps] = huv[2 * ps + 1] = make_double2(0.0, 0.0);
-            }
-        }
-        mark();
         std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
         mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
         mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, upload, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.upload, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
-        mark();
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
+        {
+            SlotSrc S;
+            S.mask = reinterpret_cast<const unsigned long long*>(d_arena.p + L.mask);
+            S.lm_base = reinterpret_cast<const int*>(d_arena.p + L.lm_base);
+            S.wave_fill = reinterpret_cast<const int*>(d_arena.p + L.wave_fill);
+            S.key = reinterpret_cast<const unsigned*>(d_arena.p + L.key);
+            S.uv = reinterpret_cast<const double2*>(d_arena.p + L.ouv);
+            S.nb_lm = (n_lm + 255) / 256;
+            S.nb_pad = (int)((n_pad + 255) / 256);
+            const int nb = S.nb_lm + S.nb_pad + (n_obs + 255) / 256;
+            if (nb)
+                hipLaunchKernelGGL(ba_build_slots, dim3(nb), dim3(256), 0, stream, G, prob(), S,
+                                   reinterpret_cast<int4*>(d_arena.p + L.hdr),
+                                   reinterpret_cast<double2*>(d_arena.p + L.uv));
+            RSVIO_HIP(hipGetLastError());
+        }
         hipLaunchKernelGGL(ba_build_pairs, dim3(n_chunk), dim3(256), 0, stream, G, prob(),
                            reinterpret_cast<int4*>(d_arena.p + L.pairs));
         RSVIO_HIP(hipGetLastError());
+        mark();
         grow(d_pose2, 14 * (size_t)n_kf);
         grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
         {  // partial systems: every entry of every slot is written by K4c each iteration; zeroed
@@ -2625,15 +2702,14 @@ struct BundleAdjuster {
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
         grow(d_state, 2);
-        mark();
         *h_state.p = LmState{};  // cur = 0: buffer 0 holds the initial state once it is set
         state_fresh = true;
         has_problem = true;
         mark();
         if (prof)
-            fprintf(stderr, "[rsvio] set_problem us: idle %.1f - %.1f drop+sort %.1f slots+waves %.1f pairs-count %.1f "
-                    "layout+wait+alloc %.1f hdr %.1f pairs %.1f upload %.1f grow %.1f tail %.1f (bytes %zu)\n",
-                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], tms[6], tms[7], tms[8], tms[9], tms[10], L.total);
+            fprintf(stderr, "[rsvio] set_problem us: checks+layout %.1f observations %.1f waves %.1f tables %.1f "
+                    "enqueue %.1f grow %.1f (upload %zu B, arena %zu B)\n",
+                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], L.upload, L.total);
     }
 
     void allreduce(double* buf, size_t n) {
@@ -2742,8 +2818,8 @@ struct BundleAdjuster {
 
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
-        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(64), 0, stream, G, prob(), work_at(it & 1), sharded() ? 1 : 0,
-                           lm_args(cfg), h_state.p, h_tick);
+        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(kK7Threads), 0, stream, G, prob(), work_at(it & 1),
+                           sharded() ? 1 : 0, lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -2798,6 +2874,7 @@ struct BundleAdjuster {
         pend.active = true;
         pend.cfg = cfg;
         pend.by_tick = by_tick();
+        state_export = false;
         // sliding_window.rs:303-319: too few residuals / underconstrained -> skipped (Ok(false))
         if (!sharded() && (G.n_obs < 6 || G.n_obs < G.n_kf + G.n_lm)) {
             pend.skipped = true;
@@ -2854,6 +2931,7 @@ struct BundleAdjuster {
         }
         last_iterations = h_state.p->iter;
         if (coll == 2) p2p_check();
+        state_export = export_on && h_state.p->done != 0;  // the final K7 exported it with its ticket
         float ms = 0.0f;
         if (by_tick) {
             ms = (float)((double)(h_tick[2] - h_tick[1]) / wclk_khz);
@@ -2970,6 +3048,7 @@ struct BundleAdjuster {
             RSVIO_HIP(hipStreamSynchronize(stream));
             settled = true;
         }
+        destroy_retired();
     }
 
     // spin on the ticket of the last enqueued decision; a bounded spin (1 s) falls back to a
@@ -2990,6 +3069,13 @@ struct BundleAdjuster {
     }
 
     void get_state(double* pose7, double* pW) {
+        if (pend.active) throw CallOrderError("get_state: a solve is in flight (call rsvio_ba_wait first)");
+        if (state_export) {  // published with the final decision's ticket: no stream sync needed
+            std::memcpy(pose7, h_out.p, sizeof(double) * 7 * G.n_kf);
+            if (G.n_lm) std::memcpy(pW, h_out.p + 7 * G.n_kf, sizeof(double) * 3 * G.n_lm);
+            return;
+        }
+        export_on = true;  // from the next solve on, its final decision exports the state
         require_idle("get_state");
         if (state_fresh) {  // no solve since set_problem: the initial state into both buffers
             enqueue_reset(1e-4);
@@ -3005,6 +3091,7 @@ struct BundleAdjuster {
 
     void build_system(double lambda, double huber_delta, double* S, double* b, double* cost) {
         require_idle("build_system");
+        state_export = false;  // K4 below resets the state buffers
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
         G.chol = 0;
@@ -3034,6 +3121,7 @@ struct BundleAdjuster {
     // diagnostic: one reduced system at lambda and its camera solve (K4c + K5) -> dc
     void camera_step(double lambda, double huber_delta, double* dc) {
         require_idle("camera_step");
+        state_export = false;
         if (!has_problem) throw std::invalid_argument("no problem uploaded");
         G.huber_delta = huber_delta;
         G.chol = 0;
@@ -3104,6 +3192,7 @@ struct BundleBatch {
         for (int i = 0; i < B; ++i) {
             BundleAdjuster& w = *win[i];
             w.require_idle("rsvio_ba_batch_run");
+            w.state_export = false;  // the batch's decisions leave the state in device memory
             if (!w.has_problem) throw std::invalid_argument("batch window without a problem");
             const Geometry& G = w.G;
             // sliding_window.rs:303-319 guards, as the single-window start()

@@ -322,6 +322,78 @@ def test_recapture_after_ticket_wait(gpu, cfg3):
     a.close()
 
 
+def test_observation_order_is_irrelevant(gpu, cfg3):
+    """set_problem builds the slot layout from per-landmark (keyframe, camera) masks, not from the
+    input order: a shuffled observation list gives the same solve, bit for bit."""
+    import dataclasses
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(cfg3.n_obs)
+    shuf = dataclasses.replace(cfg3, obs_lm=cfg3.obs_lm[perm], obs_kf=cfg3.obs_kf[perm],
+                               obs_cam=cfg3.obs_cam[perm], obs_uv=cfg3.obs_uv[perm])
+    a, b = _adjuster(gpu, cfg3), _adjuster(gpu, shuf)
+    ra, rb = a.run(), b.run()
+    assert (ra.status, ra.iterations, ra.initial_cost, ra.final_cost) == \
+        (rb.status, rb.iterations, rb.initial_cost, rb.final_cost)
+    for x, y in zip(a.state(), b.state()):
+        assert np.array_equal(x, y)
+    a.close()
+    b.close()
+
+
+def test_duplicate_observation_refused(gpu, cfg3):
+    """Two observations of one landmark by the same camera of one keyframe (feature ids are unique
+    per camera and frame in the reference) are refused with RSVIO_ERR_INVALID_ARG."""
+    import dataclasses
+    i = np.arange(cfg3.n_obs)
+    dup = np.concatenate([i, i[:1]])
+    bad = dataclasses.replace(cfg3, obs_lm=cfg3.obs_lm[dup], obs_kf=cfg3.obs_kf[dup], obs_cam=cfg3.obs_cam[dup],
+                              obs_uv=cfg3.obs_uv[dup])
+    from rsvio.ba import BundleAdjuster
+    ba = BundleAdjuster(max_keyframes=21, max_landmarks=cfg3.n_lm, max_observations=cfg3.n_obs + 1)
+    with pytest.raises(gpu.RsvioError) as e:
+        ba.set_problem_from(bad)
+    assert e.value.code == -1 and "more than one observation" in str(e.value)
+    ba.set_problem_from(cfg3)  # the handle stays usable
+    assert ba.run().status > 0
+    ba.close()
+
+
+def test_state_export_equals_device_copy(gpu, cfg3):
+    """After the first rsvio_ba_get_state, each solve's final decision kernel publishes the
+    optimised state to pinned host memory with its ticket; get_state then copies it from there.
+    It equals the device-buffer copy of the same solve on a fresh handle, across a window change,
+    and a skipped solve or build_system fall back to the device buffers (never a stale export)."""
+    import dataclasses
+
+    from rsvio import synthetic as S
+    alt = S.ba_problem(seed=17, init_seed=23)
+    a = _adjuster(gpu, cfg3)
+    a.run()
+    a.state()                                   # device copy; turns the export on
+    for prob in (cfg3, alt, cfg3):
+        a.set_problem_from(prob)
+        ra = a.run()
+        pa, wa = a.state()                      # exported
+        f = _adjuster(gpu, prob)
+        rf = f.run()
+        pf, wf = f.state()                      # device copy
+        f.close()
+        assert (ra.status, ra.iterations, ra.final_cost) == (rf.status, rf.iterations, rf.final_cost)
+        assert np.array_equal(pa, pf) and np.array_equal(wa, wf)
+    few = dataclasses.replace(cfg3, obs_lm=cfg3.obs_lm[:5], obs_kf=cfg3.obs_kf[:5], obs_cam=cfg3.obs_cam[:5],
+                              obs_uv=cfg3.obs_uv[:5])
+    a.set_problem_from(few)
+    assert a.run().status == -2                 # skipped: the state is the initial one
+    p0, w0 = a.state()
+    assert np.array_equal(p0, few.pose7) and np.array_equal(w0, few.p_W)
+    a.set_problem_from(cfg3)
+    a.run()
+    a.build_system(1e-4)                        # resets the device state to the initial one
+    p1, w1 = a.state()
+    assert np.array_equal(p1, cfg3.pose7) and np.array_equal(w1, cfg3.p_W)
+    a.close()
+
+
 def test_skip_guard_counts_every_keyframe(gpu, oracle):
     """sliding_window.rs:304,315: num_variables counts every keyframe variable, the fixed KF_0
     included, so n_obs == n_free + n_lm is underconstrained (skipped) and n_obs == n_kf + n_lm
