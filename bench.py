@@ -706,6 +706,20 @@ class TrackerWorkload:
             self._memcpy = self.lib.hipMemcpyAsync
             self._memcpy.restype = C.c_int
             self._memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+            # the frame's completion: an event after the D2H copies, polled (hipEventQuery) --
+            # a blocking stream sync may put the thread to sleep and add its wake-up latency
+            self._ev_record = self.lib.hipEventRecord
+            self._ev_record.restype = C.c_int
+            self._ev_record.argtypes = [C.c_void_p, C.c_void_p]
+            self._ev_query = self.lib.hipEventQuery
+            self._ev_query.restype = C.c_int
+            self._ev_query.argtypes = [C.c_void_p]
+            ev = C.c_void_p()
+            create = self.lib.hipEventCreateWithFlags
+            create.restype = C.c_int
+            create.argtypes = [C.c_void_p, C.c_uint]
+            self.L.check(create(C.byref(ev), 2))  # hipEventDisableTiming
+            self._done_ev = ev.value
         t = self.seq[phase]
         t2 = self.seq[(phase + 1) % len(self.seq)]
         prev, cur = phase % 2, 1 - phase % 2
@@ -747,13 +761,24 @@ class TrackerWorkload:
         if pcie:
             self.L.check(self._memcpy(self.h_out.data_ptr(), self.out.data_ptr(), self.out.numel() * 4, 2, s))
             self.L.check(self._memcpy(self.h_valid.data_ptr(), self.valid.data_ptr(), self.valid.numel(), 2, s))
+            self.L.check(self._ev_record(self._done_ev, s))
+            self._pending = True
             if wait:
-                self.stream.synchronize()
+                self.sync()
         self.slot = 1 - self.slot
         self.k += 1
 
     def sync(self):
-        self.stream.synchronize()
+        if getattr(self, "_pending", False):
+            while True:
+                rc = self._ev_query(self._done_ev)
+                if rc != 600:  # hipErrorNotReady
+                    if rc:
+                        raise RuntimeError(f"hipEventQuery failed with HIP error {rc}")
+                    break
+            self._pending = False
+        else:
+            self.stream.synchronize()
 
     def close(self):
         # pinned blocks carry events recorded on the tracker stream: drain and release them while

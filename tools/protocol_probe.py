@@ -2,7 +2,9 @@
 keyframe window per step): tracker enqueue (image H2D, pyramids, LK, feature D2H), the window
 upload (rsvio_ba_set_problem), the solve start (graph capture/instantiate/launch) -- in that
 order, as bench.py's protocol_step -- the tracker sync, the solve wait and the state read-back.
-  python tools/protocol_probe.py [steps] [cu_split]"""
+  python tools/protocol_probe.py [steps] [cu_split] [resident]
+(resident = 1: the device-resident step instead -- the same window re-solved, no PCIe -- for
+kernel-trace comparisons of the two steps)"""
 import sys
 import time
 from pathlib import Path
@@ -14,7 +16,7 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 
 
-def main(steps=60, split=0.25):
+def main(steps=60, split=0.25, resident=False):
     import torch
 
     import rsvio
@@ -27,6 +29,15 @@ def main(steps=60, split=0.25):
     trk.enable_pcie()
     names = ("set_problem", "start", "trk_enqueue", "trk_sync", "finish", "state", "total")
     t = {k: [] for k in names}
+    if resident:
+        for k in range(steps + 10):
+            ba.start()
+            trk.step(False)
+            ba.finish(False)
+        trk.close()
+        ba.ba.close()
+        torch.cuda.synchronize()
+        return
     for k in range(steps + 10):
         t0 = time.perf_counter()
         ba.next_window()
@@ -52,4 +63,5 @@ def main(steps=60, split=0.25):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 60, float(sys.argv[2]) if len(sys.argv) > 2 else 0.25)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 60, float(sys.argv[2]) if len(sys.argv) > 2 else 0.25,
+         len(sys.argv) > 3 and sys.argv[3] == "1")
