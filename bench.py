@@ -789,6 +789,12 @@ class TrackerWorkload:
         host_empty = getattr(self.torch._C, "_host_emptyCache", None)
         if host_empty:
             host_empty()
+        if getattr(self, "_done_ev", None):
+            destroy = self.lib.hipEventDestroy
+            destroy.restype = self.C.c_int
+            destroy.argtypes = [self.C.c_void_p]
+            destroy(self._done_ev)
+            self._done_ev = None
         if self.ctx:
             self.lib.rsvio_track_ctx_destroy(self.ctx)
             self.ctx = None

@@ -389,32 +389,13 @@ __device__ __forceinline__ bool landmark_inverse(const double* Vp, double lambda
 }
 
 // ---------------------------------------------------------------------------------------
-// Pair lists of the Schur chunks, built on the device by set_problem from the uploaded slot
-// headers: chunk c = 8 pb + x lists, in ascending landmark order, every landmark of group x (the
-// landmarks of the waves w % 8 == x) that has slots in both keyframes (fa, fb) of camera block pb
-// -- a landmark has at most one slot per keyframe, so at most one pair per chunk -- as
-// {slot a, slot b, landmark, 0}, and {-1, 0, 0, 0} past the count (the host sizes the stride by
-// the largest group).  One 256-thread workgroup per chunk, each wave a contiguous run of the
-// group's waves: count, prefix over the four runs, write.
+// set_problem's device part (ba_build_layout, one launch): the padded slot layout and the pair
+// lists of the Schur chunks -- chunk c = 8 pb + x lists, in ascending landmark order, every
+// landmark of group x (the landmarks of the waves w % 8 == x) that has slots in both keyframes
+// (fa, fb) of camera block pb (a landmark has at most one slot per keyframe, so at most one pair
+// per chunk) as {slot a, slot b, landmark, 0}, and {-1, 0, 0, 0} past the count (the host sizes
+// the stride by the largest group).
 // ---------------------------------------------------------------------------------------
-constexpr int kPairKU = 8;  // slot waves per lane whose headers are in flight together
-
-// lane's partner lane for (fa, fb) in its slot wave, or -1; sh is this wave's [64] scratch
-__device__ __forceinline__ int pair_partner(const int4 h0, const int4 h1, int fa, int fb, int lane, int* sh) {
-    sh[lane] = h1.y > 0 ? h1.x : -1;  // free index of the slot's keyframe (or -1)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    int partner = -1;
-    if (h1.y > 0 && h1.x == fa) {
-        const int first = h0.z, nk = h0.w;
-        for (int j = first; j < first + nk; ++j)
-            if (sh[j] == fb) partner = j;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    return partner;
-}
-
 // The padded slot layout of a problem, built on the device from what set_problem uploads: per
 // landmark the (keyframe, camera) bit mask (bit 2 kf + cam) and the padded position of its first
 // slot (the host's greedy wave packing), per wave its real slot count, per observation its packed
@@ -424,6 +405,7 @@ struct SlotSrc {
     const unsigned long long* mask;  // n_lm
     const int* lm_base;              // n_lm: padded slot of the landmark's first slot, -1 unobserved
     const int* wave_fill;            // n_wave: real slots of the wave (the rest are padding lanes)
+    const int* wave_lm;              // n_wave + 1: first landmark of each wave, then n_lm
     const unsigned* key;             // n_obs: landmark << 6 | kf << 1 | cam
     const double2* uv;               // n_obs
     int nb_lm, nb_pad;               // blocks of the landmark and padding parts of the grid
@@ -435,8 +417,9 @@ constexpr unsigned long long kEvenBits = 0x5555555555555555ull;
 // bits, 0}; [nb_lm, nb_lm + nb_pad): one thread per padded slot -- the waves' padding lanes
 // {0, 0, 0, 0} {-1, 0, 0, 0} with zero observations; the rest: one thread per observation -- its
 // (u, v) into its slot (first = camera 0 if present, second = camera 1; an absent second zero).
-__global__ __launch_bounds__(256) void ba_build_slots(Geometry G, Prob Pr, SlotSrc S, int4* hdr, double2* huv) {
-    const int b = blockIdx.x, t = threadIdx.x;
+__device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSrc& S, int4* hdr, double2* huv,
+                                 int b) {
+    const int t = threadIdx.x;
     const double2 z2 = make_double2(0.0, 0.0);
     if (b < S.nb_lm) {
         const int l = 256 * b + t;
@@ -474,60 +457,86 @@ __global__ __launch_bounds__(256) void ba_build_slots(Geometry G, Prob Pr, SlotS
     }
 }
 
-__global__ __launch_bounds__(256) void ba_build_pairs(Geometry G, Prob Pr, int4* pairs) {
-    __shared__ int sh[4][64];
+// The Schur pair list of chunk c = 8 pb + x straight from the landmark masks (no slot headers
+// needed, so it runs in the same launch as the slot build): the landmarks of the group's waves
+// w = x + 8 k, in (wave, landmark) order -- the order K4c's chunk sums have always used -- that have a
+// slot in both keyframes of camera block pb give {slot a, slot b, landmark, 0}; {-1, 0, 0, 0}
+// past the count.  Four waves, each a contiguous run of the group's waves: count, prefix, write.
+constexpr int kPairU = 8;  // waves of a run whose landmark ranges and masks are in flight together
+
+__device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSrc& S, int4* pairs, int c) {
     __shared__ int cnt[4];
-    const int c = blockIdx.x, pb = c / kGrp, x = c % kGrp;
+    const int pb = c / kGrp, x = c % kGrp;
     const int fa = Pr.pb_fa[pb], fb = Pr.pb_fb[pb];
+    int kfa = 0, kfb = 0;
+    for (int k = 0; k < G.n_kf; ++k) {
+        const int f = Pr.free_idx[k];
+        if (f == fa) kfa = k;
+        if (f == fb) kfb = k;
+    }
+    const unsigned long long ma = 3ull << (2 * kfa), mb = 3ull << (2 * kfb);
+    const unsigned long long below_a = (1ull << (2 * kfa)) - 1ull, below_b = (1ull << (2 * kfb)) - 1ull;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nw = G.n_wave > x ? (G.n_wave - x + kGrp - 1) / kGrp : 0;  // slot waves x + 8k of the group
     const int k0 = nw * wave / 4, k1 = nw * (wave + 1) / 4;
     int4* out = pairs + (size_t)c * G.pair_stride;
+    // the run's waves kPairU at a time: their landmark ranges, then the first 64 landmarks' masks
+    // of each, every load of a round in flight together (a wave of more than 64 landmarks --
+    // unobserved ones between observed ones -- continues in a loop)
+    auto round = [&](int kb, bool write, int& acc) {
+        int l0[kPairU], l1[kPairU];
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u) {
+            const int w = x + kGrp * (kb + u);
+            const bool in = kb + u < k1;
+            l0[u] = in ? S.wave_lm[w] : 0;
+            l1[u] = in ? S.wave_lm[w + 1] : 0;
+        }
+        unsigned long long m[kPairU];
+        int lbs[kPairU];
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u) {
+            const bool in = l0[u] + lane < l1[u];
+            m[u] = in ? S.mask[l0[u] + lane] : 0ull;
+            lbs[u] = in && write ? S.lm_base[l0[u] + lane] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u) {
+            for (int l = l0[u] + lane; l - lane < l1[u]; l += 64) {
+                const bool first = l == l0[u] + lane;
+                const unsigned long long mm = first ? m[u] : (l < l1[u] ? S.mask[l] : 0ull);
+                const bool has = (mm & ma) && (mm & mb);
+                const unsigned long long bal = __ballot(has);
+                if (write && has) {
+                    const unsigned long long kbits = (mm | (mm >> 1)) & kEvenBits;
+                    const int lb = first ? lbs[u] : S.lm_base[l];
+                    out[acc + __popcll(bal & ((1ull << lane) - 1ull))] =
+                        make_int4(lb + __popcll(kbits & below_a), lb + __popcll(kbits & below_b), l, 0);
+                }
+                acc += __popcll(bal);
+            }
+        }
+    };
     int n = 0;  // pass 1: this run's pair count
-    for (int kb = k0; kb < k1; kb += kPairKU) {
-        int4 h0[kPairKU], h1[kPairKU];
-#pragma unroll
-        for (int u = 0; u < kPairKU; ++u) {
-            const int k = min(kb + u, k1 - 1);
-            const size_t s = (size_t)64 * (x + kGrp * k) + lane;
-            h0[u] = Pr.slot_hdr[2 * s];
-            h1[u] = Pr.slot_hdr[2 * s + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kPairKU; ++u) {
-            if (kb + u >= k1) break;
-            const int p = pair_partner(h0[u], h1[u], fa, fb, lane, sh[wave]);
-            n += __popcll(__ballot(p >= 0));
-        }
-    }
+    for (int kb = k0; kb < k1; kb += kPairU) round(kb, false, n);
     if (lane == 0) cnt[wave] = n;
     __syncthreads();
     int base = 0;
     for (int v = 0; v < wave; ++v) base += cnt[v];
     const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-    for (int kb = k0; kb < k1; kb += kPairKU) {  // pass 2: (slot wave, lane) order = landmark order
-        int4 h0[kPairKU], h1[kPairKU];
-#pragma unroll
-        for (int u = 0; u < kPairKU; ++u) {
-            const int k = min(kb + u, k1 - 1);
-            const size_t s = (size_t)64 * (x + kGrp * k) + lane;
-            h0[u] = Pr.slot_hdr[2 * s];
-            h1[u] = Pr.slot_hdr[2 * s + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kPairKU; ++u) {
-            if (kb + u >= k1) break;
-            const int w = x + kGrp * (kb + u);
-            const int p = pair_partner(h0[u], h1[u], fa, fb, lane, sh[wave]);
-            const unsigned long long m = __ballot(p >= 0);
-            if (p >= 0) {
-                const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-                out[pos] = make_int4(64 * w + lane, 64 * w + p, h0[u].y, 0);
-            }
-            base += __popcll(m);
-        }
-    }
+    for (int kb = k0; kb < k1; kb += kPairU) round(kb, true, base);  // pass 2
     for (int i = total + tid; i < G.pair_stride; i += 256) out[i] = make_int4(-1, 0, 0, 0);
+}
+
+// set_problem's device part in one launch: blocks [0, nb_slots) build the slot layout, the next
+// n_chunk blocks the Schur pair lists
+__global__ __launch_bounds__(256) void ba_build_layout(Geometry G, Prob Pr, SlotSrc S, int nb_slots, int4* hdr,
+                                                       double2* huv, int4* pairs) {
+    const int b = blockIdx.x;
+    if (b < nb_slots)
+        build_slots_body(G, Pr, S, hdr, huv, b);
+    else
+        build_pairs_body(G, Pr, S, pairs, b - nb_slots);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1516,56 +1525,80 @@ __device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMf
     if constexpr (J + 1 < PW) mf_pivot<H, J + 1, PW>(a, uq, l, inv_next, Lf, Up, lane, bad);
 }
 
-// Panel H (columns 8H .. 8H + PW - 1): wave 0 factors it from M into Lf / Up, then every wave
-// updates its share of the trailing lower tiles (I, J), J >= (8H + 8) / 16, on the matrix cores:
-// C_IJ += (-U_I) L_J^T over the panel (2 MFMAs per tile).  A tile holding factored columns gets
-// garbage there (their L lives in Lf).
+// Panel H (columns 8H .. 8H + PW - 1) factored by wave 0 from M into Lf and its U buffer Uh.
 template <int NF, int H>
-__device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int tid, bool& bad) {
-    constexpr int NP = MfDims<NF>::NP, NT = MfDims<NF>::NT, NH = MfDims<NF>::NH;
+__device__ __forceinline__ void mf_factor(const double* M, double* Lf, double* Uh, int lane, bool& bad) {
+    constexpr int NP = MfDims<NF>::NP;
     constexpr int C0 = kMfPanel * H;
     constexpr int PW = (NP - C0) < kMfPanel ? (NP - C0) : kMfPanel;
-    const int lane = tid & 63, wave = tid >> 6;
-    if (wave == 0) {
-        double a[kMfPanel], uq[kMfPanel];
+    double a[kMfPanel], uq[kMfPanel];
 #pragma unroll
-        for (int jj = 0; jj < kMfPanel; ++jj) {
-            a[jj] = jj < PW ? M[(C0 + jj) * kMfLd + lane] : 0.0;
-            uq[jj] = 0.0;
-        }
-        const double piv = rl64(a[0], C0);
-        bad |= !(piv > 0.0) || !isfinite(piv);
-        mf_pivot<H, 0, PW>(a, uq, 0.0, rcp_f64(piv), Lf, Up, lane, bad);
+    for (int jj = 0; jj < kMfPanel; ++jj) {
+        a[jj] = jj < PW ? M[(C0 + jj) * kMfLd + lane] : 0.0;
+        uq[jj] = 0.0;
     }
+    const double piv = rl64(a[0], C0);
+    bad |= !(piv > 0.0) || !isfinite(piv);
+    mf_pivot<H, 0, PW>(a, uq, 0.0, rcp_f64(piv), Lf, Uh, lane, bad);
+}
+
+// The trailing update of panel H on the matrix cores: lower tiles (I, J), I >= J, of tile columns
+// J0 <= J < J1, C_IJ += (-U_I) L_J^T over the panel's 8 columns (2 MFMAs per tile), tile t of the
+// flattened list taken by wave `wid` of `nw`.  A tile holding factored columns gets garbage there
+// (their L lives in Lf).
+template <int NF, int H>
+__device__ __forceinline__ void mf_update(double* M, const double* Lf, const double* Uh, int lane, int wid, int nw,
+                                          int J0, int J1) {
+    constexpr int NT = MfDims<NF>::NT;
+    constexpr int C0 = kMfPanel * H;
+    const int i16 = lane & 15, k4 = lane >> 4;
+    int ntile = 0;
+    for (int J = J0; J < J1; ++J) ntile += NT - J;
+    for (int t = wid; t < ntile; t += nw) {
+        int TJ = J0, rem = t;
+        while (rem >= NT - TJ) {
+            rem -= NT - TJ;
+            ++TJ;
+        }
+        const int TI = TJ + rem;
+        double av[2], bv[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const int kk = 4 * m + k4;
+            av[m] = -Uh[kk * kMfLd + 16 * TI + i16];
+            bv[m] = Lf[(C0 + kk) * kMfLd + 16 * TJ + i16];
+        }
+        mf_dbl4 c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r];
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r] = c[r];
+    }
+}
+
+// Panel H is factored (Lf, Up[H & 1]) and visible to every wave.  Look-ahead: wave 0 updates the
+// tile column T0 that holds panel H + 1's columns and factors panel H + 1 straight away (into the
+// other U buffer), while waves 1-3 update the tile columns past T0 -- disjoint columns of M, so
+// the next pivot chain starts without waiting for the rest of the trailing update.
+template <int NF, int H>
+__device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int tid, bool& bad) {
+    constexpr int NT = MfDims<NF>::NT, NH = MfDims<NF>::NH;
+    constexpr int C0 = kMfPanel * H;
+    const int lane = tid & 63, wave = tid >> 6;
     if constexpr (H == 0) STAMP(9); else if constexpr (H == 2) STAMP(15); else if constexpr (H == 4) STAMP(30);
     if constexpr (H + 1 == NH) STAMP(7);
     if constexpr (H + 1 < NH) {
-        __syncthreads();
-        constexpr int T0 = (C0 + kMfPanel) / 16;  // first tile column with unfactored columns
-        constexpr int R = NT - T0;
-        constexpr int NTILE = R * (R + 1) / 2;
-        const int i16 = lane & 15, k4 = lane >> 4;
-        for (int t = 3 - wave; t < NTILE; t += 4) {  // wave 0 (the panel's) takes the fewest
-            int J = 0, rem = t;
-            while (rem >= R - J) {
-                rem -= R - J;
-                ++J;
-            }
-            const int TJ = T0 + J, TI = TJ + rem;
-            double av[2], bv[2];
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const int kk = 4 * m + k4;
-                av[m] = -Up[kk * kMfLd + 16 * TI + i16];
-                bv[m] = Lf[(C0 + kk) * kMfLd + 16 * TJ + i16];
-            }
-            mf_dbl4 c;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c[r] = M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r];
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) M[(16 * TJ + i16) * kMfLd + 16 * TI + k4 + 4 * r] = c[r];
+        constexpr int T0 = (C0 + kMfPanel) / 16;  // the tile column of panel H + 1
+        double* Uh = Up + (H & 1) * kMfPanel * kMfLd;
+        if (wave == 0) {
+            mf_update<NF, H>(M, Lf, Uh, lane, 0, 1, T0, T0 + 1);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the column's updates before its reads
+            __builtin_amdgcn_wave_barrier();
+            mf_factor<NF, H + 1>(M, Lf, Up + ((H + 1) & 1) * kMfPanel * kMfLd, lane, bad);
+        } else {
+            mf_update<NF, H>(M, Lf, Uh, lane, wave - 1, kK5Threads / 64 - 1, T0 + 1, NT);
         }
         __syncthreads();
         if constexpr (H == 0) STAMP(13); else if constexpr (H == 2) STAMP(19); else if constexpr (H == 4) STAMP(31);
@@ -1579,7 +1612,7 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
     __shared__ __attribute__((aligned(16))) double M[NPP * kMfLd];
     __shared__ __attribute__((aligned(16))) double Lf[NPP * kMfLd];
-    __shared__ __attribute__((aligned(16))) double Up[kMfPanel * kMfLd];
+    __shared__ __attribute__((aligned(16))) double Up[2 * kMfPanel * kMfLd];  // U of panels H & 1
     __shared__ double gsh[NP];
     __shared__ int fail;
     RTSTAMP(4);
@@ -1633,6 +1666,8 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
         return;
     }
     bool bad = false;
+    if (wave == 0) mf_factor<NF, 0>(M, Lf, Up, lane, bad);
+    __syncthreads();
     mf_panel<NF, 0>(M, Lf, Up, tid, bad);
     if (wave != 0) return;
     if (bad) {
@@ -2085,28 +2120,33 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 }
 
 // ---------------------------------------------------------------------------------------
-// K7: the pending decision at the end of a chunk of iterations (one wave, in place: the state
-// the host reads back, and the next chunk's K4c finds nothing pending).
-// ---------------------------------------------------------------------------------------
-// host: the pinned host copy of the state the host reads at the end of a chunk -- written here
-// directly (system-scope release), so no copy follows the solve on the stream
+// K7: the pending decision at the end of a chunk of iterations.  Like K4c it reads the state
+// copy the last iteration left (st_prev, its trial pending) and writes the decided state to the
+// other copy (st): the next chunk's first K4c decides the same pending trial again from st_prev
+// (identical bits), so no block ever reads a copy another block of the launch writes.
 // host: the pinned LmState copy; htick (pinned, fine-grained): [1] solve start, [2] this
 // decision's wall clock, then [0] = the decision's ticket, a system-scope release the host polls
-// (rsvio_ba_wait returns on it, before the kernel's end-of-kernel signal).  hout (pinned,
-// fine-grained, or null): when the decision ends the solve, the whole block first copies the
-// optimised state -- poses then points of the current buffers -- into it, so the ticket also
-// publishes what rsvio_ba_get_state returns (no stream sync and no copy after the solve).
+// (rsvio_ba_wait returns on it, before the kernel's end-of-kernel signal) -- all by block 0.
+// hout (pinned, fine-grained, or null; then the grid is one block): when the decision ends the
+// solve, the kK7Blocks blocks (each deciding redundantly) copy one slice each of the optimised
+// state -- poses then points of the current buffers -- into it, and each publishes the solve's
+// start stamp in its own slot htick[4 + block] (release): rsvio_ba_get_state waits for the slots
+// and copies from host memory.  A slice per CU keeps each CU's PCIe writes within one round of
+// outstanding requests (one block writing all 48.6 KB took ~10 us).
 constexpr int kK7Threads = 256;
+constexpr int kK7Blocks = 16;
 __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
                                                            LmState* host, unsigned long long* htick, double* hout) {
     STAMP(8);
     __shared__ LmState sd;
-    if (threadIdx.x < 64) {  // the decision by wave 0
-        const LmState d = lm_decide(G, Pr, Wk, Wk.st, pre_reduced, la);
+    if (threadIdx.x < 64) {  // the decision by wave 0 of every block
+        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la);
         if (threadIdx.x == 0) {
             sd = d;
-            *Wk.st = d;
-            *host = d;
+            if (blockIdx.x == 0) {
+                *Wk.st = d;
+                *host = d;
+            }
         }
     }
     __syncthreads();
@@ -2115,11 +2155,15 @@ __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, 
         const double* pose = Wk.pose[s.cur];
         const double* pw = Wk.pw[s.cur];
         const int np = 7 * G.n_kf, n = np + 3 * G.n_lm;
-        for (int i = threadIdx.x; i < n; i += kK7Threads) hout[i] = i < np ? pose[i] : pw[i - np];
+        const int per = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+        const int i0 = (int)blockIdx.x * per, i1 = min(n, i0 + per);
+        for (int i = i0 + (int)threadIdx.x; i < i1; i += kK7Threads) hout[i] = i < np ? pose[i] : pw[i - np];
         __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(htick + 4 + blockIdx.x, Wk.tick[1], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         const unsigned long long t = Wk.tick[0] + 1;
         Wk.tick[0] = t;
         htick[1] = Wk.tick[1];
@@ -2399,7 +2443,7 @@ struct BundleAdjuster {
     hipEvent_t ev_up = nullptr;
     bool up_pending = false;
     struct ArenaLayout {
-        size_t pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, key, ouv, upload;
+        size_t pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, wave_lm, key, ouv, upload;
         size_t hdr, uv, pairs, total;  // built on the device
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
@@ -2450,9 +2494,9 @@ struct BundleAdjuster {
         h_out.alloc((size_t)7 * P.max_keyframes + (size_t)3 * P.max_landmarks, hipHostMallocCoherent);
         d_tick.alloc(2);
         RSVIO_HIP(hipMemset(d_tick.p, 0, 2 * sizeof(unsigned long long)));
-        RSVIO_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_tick), 4 * sizeof(unsigned long long),
+        RSVIO_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_tick), (4 + kK7Blocks) * sizeof(unsigned long long),
                                 hipHostMallocCoherent));
-        std::memset(h_tick, 0, 4 * sizeof(unsigned long long));
+        std::memset(h_tick, 0, (4 + kK7Blocks) * sizeof(unsigned long long));
         {
             int khz = 0;
             if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, P.device) == hipSuccess && khz > 0)
@@ -2530,8 +2574,8 @@ struct BundleAdjuster {
     // the pinned staging image; one pass over the landmarks packs whole landmarks into waves
     // (greedy, <= 64 slots).  The mask fixes the landmark's slots (its keyframes, ascending), each
     // slot's observations and camera bits, and every observation's place in its slot, so the slot
-    // headers and the (u, v) layout are written on the device (ba_build_slots) after one H2D copy,
-    // then the Schur pair lists (ba_build_pairs).  No stream synchronisation: the initial state is
+    // headers, the (u, v) layout and the Schur pair lists are written on the device in one launch
+    // (ba_build_layout) after one H2D copy.  No stream synchronisation: the initial state is
     // set by the solve's first kernel (K4 with K0 folded in).
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
@@ -2587,6 +2631,7 @@ struct BundleAdjuster {
         L.mask = off;      off += al(sizeof(unsigned long long) * nl1);
         L.lm_base = off;   off += al(sizeof(int) * nl1);
         L.wave_fill = off; off += al(sizeof(int) * nl1);  // n_wave <= n_lm
+        L.wave_lm = off;   off += al(sizeof(int) * (nl1 + 1));
         L.key = off;       off += al(sizeof(unsigned) * std::max(n_obs, 1));
         L.ouv = off;       off += al(sizeof(double2) * std::max(n_obs, 1));
         L.upload = off;
@@ -2620,6 +2665,7 @@ struct BundleAdjuster {
         // XCD x too (chunk c on XCD c % 8) and re-read what K6 wrote there.
         auto* lm_base = reinterpret_cast<int*>(hb + L.lm_base);
         auto* wave_fill = reinterpret_cast<int*>(hb + L.wave_fill);
+        auto* wave_lm = reinterpret_cast<int*>(hb + L.wave_lm);
         int n_wave = 0, fill = 0;
         int gl[kGrp] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int l = 0; l < n_lm; ++l) {
@@ -2630,6 +2676,7 @@ struct BundleAdjuster {
             }
             if (n_wave == 0 || fill + ns > 64) {
                 if (n_wave) wave_fill[n_wave - 1] = fill;
+                wave_lm[n_wave] = l;
                 ++n_wave;
                 fill = 0;
             }
@@ -2638,6 +2685,7 @@ struct BundleAdjuster {
             fill += ns;
         }
         if (n_wave) wave_fill[n_wave - 1] = fill;
+        wave_lm[n_wave] = n_lm;
         int stride = 1;
         for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
         n_pad = (size_t)64 * n_wave;
@@ -2670,18 +2718,15 @@ struct BundleAdjuster {
             S.wave_fill = reinterpret_cast<const int*>(d_arena.p + L.wave_fill);
             S.key = reinterpret_cast<const unsigned*>(d_arena.p + L.key);
             S.uv = reinterpret_cast<const double2*>(d_arena.p + L.ouv);
+            S.wave_lm = reinterpret_cast<const int*>(d_arena.p + L.wave_lm);
             S.nb_lm = (n_lm + 255) / 256;
             S.nb_pad = (int)((n_pad + 255) / 256);
             const int nb = S.nb_lm + S.nb_pad + (n_obs + 255) / 256;
-            if (nb)
-                hipLaunchKernelGGL(ba_build_slots, dim3(nb), dim3(256), 0, stream, G, prob(), S,
-                                   reinterpret_cast<int4*>(d_arena.p + L.hdr),
-                                   reinterpret_cast<double2*>(d_arena.p + L.uv));
+            hipLaunchKernelGGL(ba_build_layout, dim3(nb + n_chunk), dim3(256), 0, stream, G, prob(), S, nb,
+                               reinterpret_cast<int4*>(d_arena.p + L.hdr), reinterpret_cast<double2*>(d_arena.p + L.uv),
+                               reinterpret_cast<int4*>(d_arena.p + L.pairs));
             RSVIO_HIP(hipGetLastError());
         }
-        hipLaunchKernelGGL(ba_build_pairs, dim3(n_chunk), dim3(256), 0, stream, G, prob(),
-                           reinterpret_cast<int4*>(d_arena.p + L.pairs));
-        RSVIO_HIP(hipGetLastError());
         mark();
         grow(d_pose2, 14 * (size_t)n_kf);
         grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
@@ -2818,8 +2863,9 @@ struct BundleAdjuster {
 
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
-        hipLaunchKernelGGL(ba_lm_decide, dim3(1), dim3(kK7Threads), 0, stream, G, prob(), work_at(it & 1),
-                           sharded() ? 1 : 0, lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
+        // reads state copy it & 1 (the last iteration's pending trial), writes copy (it + 1) & 1
+        hipLaunchKernelGGL(ba_lm_decide, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, G, prob(),
+                           work(it), sharded() ? 1 : 0, lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
         RSVIO_HIP(hipGetLastError());
     }
 
@@ -3068,9 +3114,25 @@ struct BundleAdjuster {
         }
     }
 
+    // every export slot carries this solve's start stamp (h_tick[1], published with the ticket);
+    // false after a bounded spin (the caller then settles and copies from the device)
+    bool wait_export() {
+        const unsigned long long want = h_tick[1];
+        auto t0 = std::chrono::steady_clock::now();
+        for (int b = 0; b < kK7Blocks; ++b)
+            for (unsigned it = 1; __atomic_load_n(h_tick + 4 + b, __ATOMIC_ACQUIRE) != want; ++it) {
+                if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+                    state_export = false;
+                    return false;
+                }
+                __builtin_ia32_pause();
+            }
+        return true;
+    }
+
     void get_state(double* pose7, double* pW) {
         if (pend.active) throw CallOrderError("get_state: a solve is in flight (call rsvio_ba_wait first)");
-        if (state_export) {  // published with the final decision's ticket: no stream sync needed
+        if (state_export && wait_export()) {  // the final decision's slices: no stream sync needed
             std::memcpy(pose7, h_out.p, sizeof(double) * 7 * G.n_kf);
             if (G.n_lm) std::memcpy(pW, h_out.p + 7 * G.n_kf, sizeof(double) * 3 * G.n_lm);
             return;

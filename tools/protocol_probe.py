@@ -34,9 +34,11 @@ def main(steps=60, split=0.25, resident=False):
             ba.start()
             trk.step(False)
             ba.finish(False)
-        trk.close()
-        ba.ba.close()
         torch.cuda.synchronize()
+        ba.ba.close()
+        trk.close()
+        for st in streams:
+            st.close()
         return
     for k in range(steps + 10):
         t0 = time.perf_counter()
@@ -57,9 +59,11 @@ def main(steps=60, split=0.25, resident=False):
                 t[key].append(1e3 * v)
     print(f"iterations {r.iterations}, device solve {r.solve_ms:.4f} ms")
     print("protocol step ms (median): " + ", ".join(f"{k} {np.median(v):.4f}" for k, v in t.items()), flush=True)
-    trk.close()
-    ba.ba.close()
     torch.cuda.synchronize()
+    ba.ba.close()
+    trk.close()
+    for st in streams:
+        st.close()
 
 
 if __name__ == "__main__":
