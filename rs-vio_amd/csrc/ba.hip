@@ -599,8 +599,9 @@ __device__ void linearize_body(const Geometry& G, const Prob& Pr, const Work& Wk
     STAMP(14);
 }
 
-__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk, int with_reset, double lambda0) {
-    linearize_body(G, Pr, Wk, blockIdx.x, with_reset, lambda0);
+// (always with the reset folded in: a runtime flag here made the compiler keep 40 B of scratch)
+__global__ __launch_bounds__(64) void ba_linearize(Geometry G, Prob Pr, Work Wk, double lambda0) {
+    linearize_body(G, Pr, Wk, blockIdx.x, 1, lambda0);
 }
 
 // Trial scalars of this rank, one wave: the K6 wave partials (+ |x|^2 of the free poses on the
@@ -1441,9 +1442,12 @@ inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, i
 }
 
 // combine_system with the sums scattered straight into M (and g_c into gsh) by the map
+// The partial systems' loads are issued before the LM state's (whose done flag decides whether
+// anything is stored and whose lambda joins the diagonal), so the state's round trip overlaps
+// theirs.  Returns the state's done flag (nothing stored then).
 template <int NF>
-__device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
-                               double lambda, int* fail) {
+__device__ bool combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
+                               const LmState* st, int* fail) {
     constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;  // the template's (upper bound)
     constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
     const size_t L = sys_len(G);
@@ -1465,6 +1469,14 @@ __device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
 #pragma unroll
         for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
     }
+    const int done = st->done;
+    const double lambda = st->lambda;
+    // keep the compiler from sinking the partial systems' loads under the done branch
+#pragma unroll
+    for (int i = 0; i < kE; ++i)
+#pragma unroll
+        for (int x = 0; x < kGrp; ++x) __asm__ volatile("" ::"v"(v[i][x]));
+    if (done) return true;
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         double a = v[i][0];
@@ -1489,6 +1501,7 @@ __device__ void combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
             *fail = sing;
         }
     }
+    return false;
 }
 
 // pivot J of panel H (width PW) by wave 0: inv = 1 / d_K ready.  Column J+1 (the next pivot's)
@@ -1617,22 +1630,30 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     __shared__ int fail;
     RTSTAMP(4);
     LmState* st = Wk.st;
-    if (st->done) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nF = G.n_free, n = 6 * nF;
     const int SC0 = G.n_pb * 36 + 12 * nF;
-    const int cur = st->cur;
-    double p7[7] = {0, 0, 0, 1, 0, 0, 0};
+    // both pose buffers (the state's cur picks one), loaded with the partial systems, before the
+    // state itself
+    double p7b[2][7];
     int fidx = -1;
     if (wave == 0 && lane < G.n_kf) {
         fidx = Pr.free_idx[lane];
 #pragma unroll
-        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[cur][7 * lane + i];
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 7; ++i) p7b[b][i] = Wk.pose[b][7 * lane + i];
+    } else {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 7; ++i) p7b[b][i] = i == 3 ? 1.0 : 0.0;
     }
     STAMP(0);
     if (combine) {
-        combine_mapped<NF>(G, Pr, Wk, M, gsh, st->lambda, &fail);
+        if (combine_mapped<NF>(G, Pr, Wk, M, gsh, st, &fail)) return;
     } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
+        if (st->done) return;
         const double* sys = Wk.sys;
         const int ne = G.n_pb * 36 + 12 * nF;
         for (int e = tid; e < ne; e += kK5Threads) {
@@ -1644,6 +1665,10 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
         }
         if (tid == 0) fail = sys[SC0 + 1] != 0.0;
     }
+    const int cur = st->cur;
+    double p7[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) p7[i] = cur ? p7b[1][i] : p7b[0][i];
     if (n < NP) {
         // a window with fewer free keyframes than the template (batched mode): its rows and
         // columns [n, NP) are identity padding, and the b row is zero there
@@ -1995,39 +2020,65 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w
     const int4 h0 = Pr.slot_hdr[2 * s], h1 = Pr.slot_hdr[2 * s + 1];
     const double2 uvq[2] = {Pr.slot_uv[2 * s], Pr.slot_uv[2 * s + 1]};
     const LmState* st = Wk.st;
-    if (st->done || !st->solve_ok) return;  // no step: the decision (lambda up) is all there is
-    STAMP(20);
-    RTSTAMP(7);
     const bool act = h1.y > 0;
-    const int cur = st->cur;
-    const double lambda = st->lambda;
     const int kf = h0.x, l = h0.y, first = act ? h0.z : lane, nk = act ? h0.w : 1;
     const bool fr = h1.x >= 0;
-    // every global input of this lane in one round trip (indices clamped on padding lanes):
-    // the slot's W, the camera step, the landmark's raw record and point, the trial pose
+    // every global input of this lane in one round trip with the LM state's (indices clamped on
+    // padding lanes): the slot's record, the landmark's record and point and the trial pose of
+    // BOTH state buffers -- the state's cur picks one after they are in flight -- and the
+    // camera step
     const int kfc = act ? kf : 0, lc = act ? l : 0, fc = (act && fr) ? h1.x : 0;
-    double Wv[18], d6[6], Lm[10], pc[3], p7[7];
-    {
-        const double2* wr = reinterpret_cast<const double2*>(Wk.raws[cur] + (size_t)s * kRawF);
-        double rec[18];  // Vs, gp_s, Wr
+    double recb[2][18], Lmb[2][10], pcb[2][3], p7b[2][7], d6[6];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
+    for (int b = 0; b < 2; ++b) {
+        const double2* wr = reinterpret_cast<const double2*>(Wk.raws[b] + (size_t)s * kRawF);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {  // Vs, gp_s, Wr
             const double2 x = wr[i];
-            rec[2 * i] = x.x; rec[2 * i + 1] = x.y;
+            recb[b][2 * i] = x.x; recb[b][2 * i + 1] = x.y;
         }
-        slot_w(rec, Wv);
-        const double2* lr = reinterpret_cast<const double2*>(Wk.rawl[cur] + (size_t)lc * kLmF);
+        const double2* lr = reinterpret_cast<const double2*>(Wk.rawl[b] + (size_t)lc * kLmF);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
             const double2 x = lr[i];
-            Lm[2 * i] = x.x; Lm[2 * i + 1] = x.y;
+            Lmb[b][2 * i] = x.x; Lmb[b][2 * i + 1] = x.y;
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) d6[i] = Wk.dc[6 * fc + i];
+        for (int i = 0; i < 3; ++i) pcb[b][i] = Wk.pw[b][3 * lc + i];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) pc[i] = Wk.pw[cur][3 * lc + i];
+        for (int i = 0; i < 7; ++i) p7b[b][i] = Wk.pose[b][7 * kfc + i];
+    }
 #pragma unroll
-        for (int i = 0; i < 7; ++i) p7[i] = Wk.pose[1 - cur][7 * kfc + i];
+    for (int i = 0; i < 6; ++i) d6[i] = Wk.dc[6 * fc + i];
+    const int done = st->done, solve_ok = st->solve_ok, cur = st->cur;
+    const double lambda = st->lambda;
+    // keep the compiler from sinking the speculative loads under the branch below
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int i = 0; i < 18; ++i) __asm__ volatile("" ::"v"(recb[b][i]));
+#pragma unroll
+        for (int i = 0; i < 10; ++i) __asm__ volatile("" ::"v"(Lmb[b][i]));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) __asm__ volatile("" ::"v"(pcb[b][i]));
+#pragma unroll
+        for (int i = 0; i < 7; ++i) __asm__ volatile("" ::"v"(p7b[b][i]));
+    }
+    if (done || !solve_ok) return;  // no step: the decision (lambda up) is all there is
+    STAMP(20);
+    RTSTAMP(7);
+    double Wv[18], Lm[10], pc[3], p7[7];
+    {
+        double rec[18];
+#pragma unroll
+        for (int i = 0; i < 18; ++i) rec[i] = cur ? recb[1][i] : recb[0][i];
+        slot_w(rec, Wv);
+#pragma unroll
+        for (int i = 0; i < 10; ++i) Lm[i] = cur ? Lmb[1][i] : Lmb[0][i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pc[i] = cur ? pcb[1][i] : pcb[0][i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) p7[i] = cur ? p7b[0][i] : p7b[1][i];  // the trial pose: buffer 1 - cur
     }
     double t3[3] = {0.0, 0.0, 0.0};
     if (act && fr) {
@@ -2779,7 +2830,7 @@ struct BundleAdjuster {
     // K0 + K4: initial state and its linearisation (buffer 0); the LM state in copy 0
     void enqueue_start(double lambda0) {
         if (G.n_wave)  // K0 folded into K4
-            hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work_at(0), 1, lambda0);
+            hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work_at(0), lambda0);
         else
             enqueue_reset(lambda0);
         RSVIO_HIP(hipGetLastError());

@@ -147,9 +147,16 @@ class BundleAdjuster:
         check(_lib.load().rsvio_ba_wait(self._h, C.byref(res)))
         return res
 
-    def state(self):
-        pose = np.zeros((self.n_kf, 7))
-        pw = np.zeros((self.n_lm, 3))
+    def state(self, out=None):
+        """The optimised state (rsvio_ba_get_state): poses (n_kf x 7) and points (n_lm x 3), into
+        `out` = (pose, p_W) f64 C-contiguous arrays of those shapes when given (reused buffers)."""
+        if out is None:
+            pose, pw = np.empty((self.n_kf, 7)), np.empty((self.n_lm, 3))
+        else:
+            pose, pw = out
+            if pose.shape != (self.n_kf, 7) or pw.shape != (self.n_lm, 3) or pose.dtype != np.float64 \
+                    or pw.dtype != np.float64:
+                raise ValueError("state(out=...): arrays of shape (n_kf, 7) and (n_lm, 3), float64")
         check(_lib.load().rsvio_ba_get_state(self._h, ptr(pose), ptr(pw)))
         return pose, pw
 
