@@ -312,8 +312,12 @@ int rsvio_ba_solve(rsvio_ba* ba, int32_t n_kf, double* pose7, const uint8_t* kf_
                    const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                    const double* T_C_B2, const rsvio_lm_cfg* cfg, rsvio_ba_result* res);
 
-/* Split form for device-resident benchmarking: upload once, solve many times from the
- * uploaded initial state (nothing crosses PCIe inside rsvio_ba_run except the status). */
+/* Split form: upload a window, solve it (possibly many times from the uploaded initial state;
+ * nothing crosses PCIe inside rsvio_ba_run except the status).  Observations may come in any
+ * order; one per (landmark, keyframe, camera) -- a second is RSVIO_ERR_INVALID_ARG, as is an
+ * index out of range.  The host validates the observations and packs per-landmark (keyframe,
+ * camera) masks into pinned staging; the slot layout and Schur pair lists are built on the
+ * device after one H2D copy.  Does not wait for the previous solve's stream tail. */
 int rsvio_ba_set_problem(rsvio_ba* ba, int32_t n_kf, const double* pose7, const uint8_t* kf_fixed,
                          int32_t n_lm, const double* p_W, int32_t n_obs, const int32_t* obs_lm,
                          const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
@@ -330,6 +334,11 @@ int rsvio_ba_run_async(rsvio_ba* ba, const rsvio_lm_cfg* cfg);
 /* Enqueue the handle's work on a caller-owned stream (NULL: back to the handle's own stream). */
 int rsvio_ba_set_stream(rsvio_ba* ba, void* stream);
 int rsvio_ba_wait(rsvio_ba* ba, rsvio_ba_result* res);
+/* The current state (n_kf x 7 poses, n_lm x 3 points).  After the first call on a handle, each
+ * later solve's final decision kernel also publishes the optimised state to pinned host memory
+ * (one slice per workgroup, each with its own flag), and get_state copies it from there without
+ * a stream synchronisation; otherwise (or after rsvio_ba_build_system, a skipped solve, a batch
+ * run) it is copied from the device buffers. */
 int rsvio_ba_get_state(rsvio_ba* ba, double* pose7, double* p_W);
 /* Reduced camera system at `lambda` for the uploaded state (parity tests):
  * S is n x n row-major (n = 6 * free keyframes, ascending keyframe order), b is n. */
