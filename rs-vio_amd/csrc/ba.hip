@@ -171,6 +171,7 @@ struct LmState {
     int iter, status, done, solve_ok;
     int accepted, cur;                      // cur: which of the two state buffers is current
     int pending;                            // K5 produced a step (or failed) not yet decided
+    int p2p_err;                            // K7 (sharded over P2P): a peer did not arrive
 };
 
 struct Geometry {
@@ -208,6 +209,7 @@ struct Work {
     double* raws[2];         // n_slot x kRawF per state buffer
     double* rawl[2];         // n_lm x kLmF per state buffer
     int* singular;           // set by K4c when a landmark block (V + lambda I) is singular
+    const int* p2p_err;      // sharded over P2P: the exchange kernels' error flag (else null)
     double* partA;           // n_wave x kPartA
     double* partD;           // n_wave x kPartD
     double* cpart;           // kGrp x sys_len partial systems (slot g: landmark group g)
@@ -2195,8 +2197,10 @@ __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, 
         if (threadIdx.x == 0) {
             sd = d;
             if (blockIdx.x == 0) {
+                LmState h = d;
+                h.p2p_err = Wk.p2p_err ? *Wk.p2p_err : 0;  // the exchanges before this decision
                 *Wk.st = d;
-                *host = d;
+                *host = h;
             }
         }
     }
@@ -2416,7 +2420,12 @@ struct BundleAdjuster {
     std::vector<hipGraphExec_t> retired;
     void drop_graph() {
         if (gexec) {
-            if (!settled && hipStreamQuery(stream) == hipSuccess) settled = true;
+            if (!settled) {
+                if (hipStreamQuery(stream) == hipSuccess)
+                    settled = true;
+                else
+                    (void)hipGetLastError();  // hipErrorNotReady is no error here
+            }
             if (settled) {
                 destroy_retired();
                 (void)hipGraphExecDestroy(gexec);
@@ -2427,6 +2436,7 @@ struct BundleAdjuster {
         }
         gexec = nullptr;
         g_k = -1;
+        g_stale = false;
     }
     void destroy_retired() {
         for (hipGraphExec_t g : retired) (void)hipGraphExecDestroy(g);
@@ -2439,11 +2449,25 @@ struct BundleAdjuster {
     }
     // (single rank, or sharded over the P2P exchange, whose generation counter lives on the
     // device; RCCL calls stay out of the graph)
+    // A new problem keeps the exec (g_stale): the next start captures the new launch sequence and,
+    // when the topology is the same (chunk size, LM configuration, export, free keyframes, collective)
+    // and the exec's last launch has completed (ev_glaunch), updates the exec in place
+    // (hipGraphExecUpdate) instead of instantiating a new one.  RSVIO_BA_GRAPH_UPDATE=0: always
+    // instantiate (A/B switch).
+    bool g_stale = false, graph_update = true;
+    int g_nf = -1, g_coll = -1;
+    hipEvent_t ev_glaunch = nullptr;
     bool start_graph(const rsvio_lm_cfg& cfg, int k) {
         if (coll == 1 || !graphs_ok) return false;
-        if (!(gexec && g_k == k && same_cfg(g_cfg, cfg) && g_export == export_on)) {
+        const bool same_key = gexec && g_k == k && same_cfg(g_cfg, cfg) && g_export == export_on;
+        if (!same_key || g_stale) {
             const auto tg0 = std::chrono::steady_clock::now();
-            drop_graph();
+            bool try_update = same_key && graph_update && g_nf == G.n_free && g_coll == coll;
+            if (try_update && hipEventQuery(ev_glaunch) != hipSuccess) {
+                (void)hipGetLastError();  // hipErrorNotReady is no error here
+                try_update = false;
+            }
+            if (!try_update) drop_graph();
             if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
                 (void)hipGetLastError();
                 graphs_ok = false;
@@ -2460,15 +2484,26 @@ struct BundleAdjuster {
             hipGraph_t g = nullptr;
             if (hipStreamEndCapture(stream, &g) != hipSuccess) ok = false;
             const auto tg1 = std::chrono::steady_clock::now();
-            if (ok && hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+            bool updated = false;
+            if (ok && try_update) {
+                hipGraphNode_t err_node = nullptr;
+                hipGraphExecUpdateResult r = hipGraphExecUpdateError;
+                updated = hipGraphExecUpdate(gexec, g, &err_node, &r) == hipSuccess && r == hipGraphExecUpdateSuccess;
+                if (!updated) {
+                    (void)hipGetLastError();
+                    drop_graph();  // (its last launch has completed: destroyed at once)
+                }
+            }
+            if (ok && !updated && hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess) {
                 gexec = nullptr;
                 ok = false;
             }
             const auto tg2 = std::chrono::steady_clock::now();
             if (g) (void)hipGraphDestroy(g);
             if (prof_env)
-                fprintf(stderr, "[rsvio] graph us: drop+capture %.1f instantiate %.1f destroy %.1f\n",
+                fprintf(stderr, "[rsvio] graph us: drop+capture %.1f %s %.1f destroy %.1f\n",
                         std::chrono::duration<double, std::micro>(tg1 - tg0).count(),
+                        updated ? "update" : "instantiate",
                         std::chrono::duration<double, std::micro>(tg2 - tg1).count(),
                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tg2).count());
             if (!ok) {
@@ -2479,8 +2514,12 @@ struct BundleAdjuster {
             g_k = k;
             g_cfg = cfg;
             g_export = export_on;
+            g_nf = G.n_free;
+            g_coll = coll;
+            g_stale = false;
         }
         RSVIO_HIP(hipGraphLaunch(gexec, stream));
+        if (graph_update) RSVIO_HIP(hipEventRecord(ev_glaunch, stream));
         return true;
     }
     int last_iterations = 3;  // first chunk = previous solve's iteration count
@@ -2541,6 +2580,9 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_up, hipEventDisableTiming));
+        RSVIO_HIP(hipEventCreateWithFlags(&ev_glaunch, hipEventDisableTiming));
+        const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
+        graph_update = !(gu && gu[0] == '0');
         h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
         h_out.alloc((size_t)7 * P.max_keyframes + (size_t)3 * P.max_landmarks, hipHostMallocCoherent);
         d_tick.alloc(2);
@@ -2576,6 +2618,7 @@ struct BundleAdjuster {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev_up) (void)hipEventDestroy(ev_up);
+        if (ev_glaunch) (void)hipEventDestroy(ev_glaunch);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -2610,6 +2653,7 @@ struct BundleAdjuster {
         w.raws[0] = d_raws.p; w.raws[1] = d_raws.p + (size_t)kRawF * std::max<size_t>(n_pad, 1);
         w.rawl[0] = d_rawl.p; w.rawl[1] = d_rawl.p + (size_t)kLmF * std::max(G.n_lm, 1);
         w.singular = d_singular.p;
+        w.p2p_err = coll == 2 ? d_p2p_err.p : nullptr;
         w.partA = d_partA.p; w.partD = d_partD.p;
         w.cpart = d_cpart.p;
         w.sys = d_sys.p; w.dc = d_dc.p; w.trial4 = d_trial4.p;
@@ -2645,7 +2689,12 @@ struct BundleAdjuster {
         // stream order (a buffer that grows is freed by hipFree, which waits for the device), and
         // the previous solve's graph is retired until the stream is next settled
         if (pend.active) throw CallOrderError("set_problem: a solve is in flight (call rsvio_ba_wait first)");
-        drop_graph();  // kernel arguments (sizes, buffers) change with the problem
+        // kernel arguments (sizes, buffers) change with the problem: the exec is updated or
+        // replaced by the next start
+        if (graph_update && gexec)
+            g_stale = true;
+        else
+            drop_graph();
         state_export = false;
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
@@ -2679,15 +2728,21 @@ struct BundleAdjuster {
         L.pb_fa = off;     off += al(sizeof(int) * (size_t)n_pb);
         L.pb_fb = off;     off += al(sizeof(int) * (size_t)n_pb);
         L.dmap = off;      off += al(sizeof(int) * ((size_t)36 * n_pb + 12 * n_free));
-        L.mask = off;      off += al(sizeof(unsigned long long) * nl1);
         L.lm_base = off;   off += al(sizeof(int) * nl1);
         L.wave_fill = off; off += al(sizeof(int) * nl1);  // n_wave <= n_lm
         L.wave_lm = off;   off += al(sizeof(int) * (nl1 + 1));
+        // [mask, key, ouv] last: complete after the observation pass, so their copy (the bulk of
+        // the upload) starts while the host still packs waves and tables
+        L.mask = off;      off += al(sizeof(unsigned long long) * nl1);
         L.key = off;       off += al(sizeof(unsigned) * std::max(n_obs, 1));
         L.ouv = off;       off += al(sizeof(double2) * std::max(n_obs, 1));
         L.upload = off;
-        if (up_pending) {  // the previous upload still reads the staging image
-            RSVIO_HIP(hipEventSynchronize(ev_up));
+        mark();
+        if (up_pending) {  // the previous upload may still read the staging image
+            if (hipEventQuery(ev_up) != hipSuccess) {  // (a query costs less than a completed sync)
+                (void)hipGetLastError();
+                RSVIO_HIP(hipEventSynchronize(ev_up));
+            }
             up_pending = false;
         }
         if (h_arena.n < L.upload) h_arena.alloc(L.upload + L.upload / 4);
@@ -2697,17 +2752,34 @@ struct BundleAdjuster {
         auto* m2 = reinterpret_cast<unsigned long long*>(hb + L.mask);
         auto* key = reinterpret_cast<unsigned*>(hb + L.key);
         std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
-        for (int i = 0; i < n_obs; ++i) {
-            const int l = obs_lm[i], k = obs_kf[i], c = obs_cam[i];
-            if (l < 0 || l >= n_lm || k < 0 || k >= n_kf || c > 1)
-                throw std::invalid_argument("observation index out of range");
-            const unsigned long long b = 1ull << (2 * k + c);
-            if (m2[l] & b)
-                throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
-            m2[l] |= b;
-            key[i] = (unsigned)l << 6 | (unsigned)k << 1 | (unsigned)c;
+        {
+            // the mask of the current run of one landmark's observations stays in a register (a
+            // landmark-major list would otherwise chain every read-modify-write of m2[l] through
+            // store-to-load forwarding)
+            int cl = -1;
+            unsigned long long cm = 0;
+            for (int i = 0; i < n_obs; ++i) {
+                const int l = obs_lm[i], k = obs_kf[i], c = obs_cam[i];
+                if (l < 0 || l >= n_lm || k < 0 || k >= n_kf || c > 1)
+                    throw std::invalid_argument("observation index out of range");
+                if (l != cl) {
+                    if (cl >= 0) m2[cl] = cm;
+                    cl = l;
+                    cm = m2[l];
+                }
+                const unsigned long long b = 1ull << (2 * k + c);
+                if (cm & b)
+                    throw std::invalid_argument("more than one observation of a landmark per camera and keyframe");
+                cm |= b;
+                key[i] = (unsigned)l << 6 | (unsigned)k << 1 | (unsigned)c;
+            }
+            if (cl >= 0) m2[cl] = cm;
         }
         std::memcpy(hb + L.ouv, obs_uv, sizeof(double2) * (size_t)n_obs);
+        if (d_arena.n < L.upload) {  // (grown for the whole arena below once its size is known)
+            d_arena.alloc(2 * L.upload);
+        }
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice, stream));
         mark();
         // waves: whole landmarks, <= 64 slots each (greedy, in landmark order); the Schur pair
         // stride is the largest XCD group's landmark count (at most one pair per landmark and
@@ -2746,7 +2818,11 @@ struct BundleAdjuster {
         L.uv = off;    off += al(sizeof(double2) * 2 * std::max<size_t>(n_pad, 1));
         L.pairs = off; off += al(sizeof(int4) * (size_t)n_chunk * stride);
         L.total = off;
-        if (d_arena.n < L.total) d_arena.alloc(L.total + L.total / 4);
+        if (d_arena.n < L.total) {  // the observation copy above went to the old arena: redo it
+            d_arena.alloc(L.total + L.total / 4);
+            RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice,
+                                     stream));
+        }
         lay = L;
         std::memcpy(hb + L.pose_init, pose7, sizeof(double) * 7 * (size_t)n_kf);
         if (n_lm) std::memcpy(hb + L.pw_init, pW, sizeof(double) * 3 * (size_t)n_lm);
@@ -2755,7 +2831,7 @@ struct BundleAdjuster {
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
         mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
         mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.upload, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.mask, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
@@ -2803,9 +2879,9 @@ struct BundleAdjuster {
         has_problem = true;
         mark();
         if (prof)
-            fprintf(stderr, "[rsvio] set_problem us: checks+layout %.1f observations %.1f waves %.1f tables %.1f "
-                    "enqueue %.1f grow %.1f (upload %zu B, arena %zu B)\n",
-                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], L.upload, L.total);
+            fprintf(stderr, "[rsvio] set_problem us: checks+layout %.1f upload wait %.1f observations %.1f waves %.1f "
+                    "tables %.1f enqueue %.1f grow %.1f (upload %zu B, arena %zu B)\n",
+                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], tms[6], L.upload, L.total);
     }
 
     void allreduce(double* buf, size_t n) {
@@ -3027,7 +3103,16 @@ struct BundleAdjuster {
             enqueue_chunk(std::min(iter_chunk, pend.max_it - pend.enq));
         }
         last_iterations = h_state.p->iter;
-        if (coll == 2) p2p_check();
+        if (coll == 2) {  // the exchange error flag came with the ticket (K7); the sync path reads it
+            if (by_tick) {
+                if (h_state.p->p2p_err) {
+                    settle();
+                    throw std::runtime_error("P2P all-reduce: a peer did not arrive");
+                }
+            } else {
+                p2p_check();
+            }
+        }
         state_export = export_on && h_state.p->done != 0;  // the final K7 exported it with its ticket
         float ms = 0.0f;
         if (by_tick) {
@@ -3131,7 +3216,9 @@ struct BundleAdjuster {
     // entry points that read or replace what an in-flight solve uses (rsvio_ba_run_async before
     // rsvio_ba_wait) are refused, as set_stream is
     // single rank waits on the decision ticket (RSVIO_BA_WAIT=sync: on the stream + events)
-    bool by_tick() const { return tick_wait && coll == 0; }
+    // single rank or sharded over P2P (the exchanges are kernels of the stream; K7 publishes their
+    // error flag with the ticket); RCCL keeps the stream sync
+    bool by_tick() const { return tick_wait && coll != 1; }
 
     void require_idle(const char* what) {
         if (pend.active) throw CallOrderError(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");
