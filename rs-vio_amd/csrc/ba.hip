@@ -2188,8 +2188,9 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 // outstanding requests (one block writing all 48.6 KB took ~10 us).
 constexpr int kK7Threads = 256;
 constexpr int kK7Blocks = 16;
-__global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
-                                                           LmState* host, unsigned long long* htick, double* hout) {
+__device__ __forceinline__ void lm_decide_body(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced,
+                                               const LmArgs& la, LmState* host, unsigned long long* htick,
+                                               double* hout) {
     STAMP(8);
     __shared__ LmState sd;
     if (threadIdx.x < 64) {  // the decision by wave 0 of every block
@@ -2227,6 +2228,11 @@ __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, 
         __hip_atomic_store(htick, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     STAMP(10);
+}
+
+__global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
+                                                           LmState* host, unsigned long long* htick, double* hout) {
+    lm_decide_body(G, Pr, Wk, pre_reduced, la, host, htick, hout);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2270,6 +2276,15 @@ __global__ __launch_bounds__(64) void bab_backsub_relinearize(const WinDesc* __r
     __shared__ double shp[3][64];
     __shared__ double shs[4][64];
     k6_body<false>(d.G, d.Pr, d.W[wi], blockIdx.x, threadIdx.x, sh, shp, shs);
+}
+
+// Single-window front end of K7 (the handle's graph in descriptor mode, BundleAdjuster::start_graph):
+// the window's geometry, problem and state views from its device descriptor D[0], so the captured
+// launch sequence does not change with the window -- a new keyframe window only rewrites D[0]
+__global__ __launch_bounds__(kK7Threads) void bad_lm_decide(const WinDesc* __restrict__ D, int wi, LmArgs la,
+                                                            LmState* host, unsigned long long* htick, double* hout) {
+    const WinDesc& d = D[0];
+    lm_decide_body(d.G, d.Pr, d.W[wi], 0, la, host, htick, hout);
 }
 
 // K7 per window: the pending decision in place and into the pinned host copy host[window]
@@ -2408,9 +2423,23 @@ struct BundleAdjuster {
     // kernels) captured once as a HIP graph and replayed by one hipGraphLaunch -- the host
     // enqueue drops from ~80 us to a few us.  Keyed by k and the LM configuration; dropped when
     // set_problem may have moved buffers.  Any capture failure falls back to direct launches.
-    hipGraphExec_t gexec = nullptr;
-    int g_k = -1;
-    rsvio_lm_cfg g_cfg{};
+    // Two execs: gv captures the by-value kernels for the uploaded window (kernel arguments as
+    // immediates; keyed by k, the LM configuration, export, free keyframes and the collective, stale
+    // after set_problem); gd is the descriptor mode (below), keyed by the window's shape only.  The
+    // first solve of a new window runs gd (no capture: a new keyframe window costs one launch); a
+    // window solved again (a retry, a resident re-solve) captures gv once and replays it, which
+    // saves the descriptor's extra dependent load at the head of every kernel (~0.3 us each).
+    struct GraphSlot {
+        hipGraphExec_t exec = nullptr;
+        int k = -1;
+        rsvio_lm_cfg cfg{};
+        bool exp = false, stale = false;
+        int nf = -1, coll = -1, wcap = 0, chunk = -1;
+        const void* dptr = nullptr;
+        hipEvent_t ev_launch = nullptr;  // recorded after each launch: update in place once it completed
+    };
+    GraphSlot gv, gd;
+    int solves_of_problem = 0;  // starts since the last set_problem
     bool graphs_ok = true;
     int k5_variant = 2;  // camera solve for n_free <= 10: 2 blocked LDL^T with MFMA trailing updates (default),
                          // 0 pipelined 4-wave LDL^T (RSVIO_K5=pipe4), 1 one-wave Gauss-Jordan (gj1)
@@ -2418,8 +2447,8 @@ struct BundleAdjuster {
     // last decision kernel has exited): unless the stream is idle (known, or queried without
     // waiting) it is retired and destroyed once it is -- set_problem need not wait for the stream
     std::vector<hipGraphExec_t> retired;
-    void drop_graph() {
-        if (gexec) {
+    void drop_slot(GraphSlot& sl) {
+        if (sl.exec) {
             if (!settled) {
                 if (hipStreamQuery(stream) == hipSuccess)
                     settled = true;
@@ -2428,15 +2457,19 @@ struct BundleAdjuster {
             }
             if (settled) {
                 destroy_retired();
-                (void)hipGraphExecDestroy(gexec);
+                (void)hipGraphExecDestroy(sl.exec);
             } else {
-                retired.push_back(gexec);
+                retired.push_back(sl.exec);
                 if (retired.size() > 4) settle();  // bounded: wait for the stream then
             }
         }
-        gexec = nullptr;
-        g_k = -1;
-        g_stale = false;
+        sl.exec = nullptr;
+        sl.k = -1;
+        sl.stale = false;
+    }
+    void drop_graph() {
+        drop_slot(gv);
+        drop_slot(gd);
     }
     void destroy_retired() {
         for (hipGraphExec_t g : retired) (void)hipGraphExecDestroy(g);
@@ -2449,25 +2482,79 @@ struct BundleAdjuster {
     }
     // (single rank, or sharded over the P2P exchange, whose generation counter lives on the
     // device; RCCL calls stay out of the graph)
-    // A new problem keeps the exec (g_stale): the next start captures the new launch sequence and,
-    // when the topology is the same (chunk size, LM configuration, export, free keyframes, collective)
-    // and the exec's last launch has completed (ev_glaunch), updates the exec in place
-    // (hipGraphExecUpdate) instead of instantiating a new one.  RSVIO_BA_GRAPH_UPDATE=0: always
-    // instantiate (A/B switch).
-    bool g_stale = false, graph_update = true;
-    int g_nf = -1, g_coll = -1;
-    hipEvent_t ev_glaunch = nullptr;
+    // A new problem keeps gv (stale): its next capture, when the topology is the same (chunk size,
+    // LM configuration, export, free keyframes, collective) and the exec's last launch has completed
+    // (ev_launch), updates the exec in place (hipGraphExecUpdate) instead of instantiating a new
+    // one.  RSVIO_BA_GRAPH_UPDATE=0: always instantiate (A/B switch).
+    bool graph_update = true;
+    // Descriptor mode (single rank, MFMA camera solve): the graph's kernels (bab_* / bad_lm_decide)
+    // read the window's geometry, problem pointers and state views from a device descriptor at the
+    // head of the arena (WinDesc, written into the staging image by set_problem and uploaded with
+    // it), and K4 / K6 run on a grid of wcap >= n_wave workgroups (the rest return at once).  The
+    // launch sequence is then the same for every window of the same shape: a new keyframe window
+    // is solved by the exec as it stands -- no capture, no update, one hipGraphLaunch.
+    // RSVIO_BA_DESC=0: every window's first solve captures gv too (A/B switch).
+    bool desc_on = true;
+    WinDesc hdesc{};                      // the descriptor set_problem wrote (host copy)
+    double desc_huber = std::nan("");     // the LM configuration the device descriptor holds
+    int desc_chol = -1;
+    HostBuf<WinDesc> h_desc1;             // staging of a descriptor refresh (another LM configuration)
+    hipEvent_t ev_desc = nullptr;
+    bool desc_pending = false;
+    bool desc_mode() const { return desc_on && coll == 0 && k5_variant == 2 && G.n_free <= 10 && G.n_wave > 0; }
+    const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
+    void fill_desc(WinDesc& d) const {
+        d = WinDesc{};
+        d.G = G;
+        d.G.huber_delta = desc_huber;
+        d.G.chol = desc_chol;
+        d.Pr = prob();
+        d.W[0] = work(0);
+        d.W[1] = work(1);
+        d.W[2] = work_at(0);
+        d.W[3] = work_at(1);
+        d.skip = 0;
+    }
+    // the solve's LM configuration differs from the one the device descriptor holds: rewrite it
+    // (stream-ordered before the launch that reads it; the staging copy is guarded by ev_desc)
+    void refresh_desc() {
+        if (desc_pending && hipEventQuery(ev_desc) != hipSuccess) {
+            (void)hipGetLastError();
+            RSVIO_HIP(hipEventSynchronize(ev_desc));
+        }
+        desc_pending = false;
+        desc_huber = G.huber_delta;
+        desc_chol = G.chol;
+        hdesc.G.huber_delta = desc_huber;
+        hdesc.G.chol = desc_chol;
+        if (!h_desc1.p) h_desc1.alloc(1);
+        *h_desc1.p = hdesc;
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p + lay.desc, h_desc1.p, sizeof(WinDesc), hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipEventRecord(ev_desc, stream));
+        desc_pending = true;
+    }
     bool start_graph(const rsvio_lm_cfg& cfg, int k) {
         if (coll == 1 || !graphs_ok) return false;
-        const bool same_key = gexec && g_k == k && same_cfg(g_cfg, cfg) && g_export == export_on;
-        if (!same_key || g_stale) {
+        const bool dm = desc_mode() && solves_of_problem == 0;
+        ++solves_of_problem;
+        GraphSlot& sl = dm ? gd : gv;
+        if (dm && (G.huber_delta != desc_huber || G.chol != desc_chol)) refresh_desc();
+        // K4 / K6 grid of a capture: n_wave + 1/16 headroom (the next window of a similar shape
+        // replays it), a multiple of 8 (wave w on XCD w % 8 either way); spare workgroups return
+        const int wcap = (G.n_wave + G.n_wave / 16 + kGrp - 1) / kGrp * kGrp;
+        const bool topo = sl.exec && sl.k == k && same_cfg(sl.cfg, cfg) && sl.exp == export_on && sl.nf == G.n_free &&
+                          sl.coll == coll;
+        const bool hit = topo && (dm ? (sl.dptr == dptr() && sl.chunk == G.n_chunk && G.n_wave <= sl.wcap &&
+                                        8 * G.n_wave > 7 * sl.wcap)
+                                     : !sl.stale);
+        if (!hit) {
             const auto tg0 = std::chrono::steady_clock::now();
-            bool try_update = same_key && graph_update && g_nf == G.n_free && g_coll == coll;
-            if (try_update && hipEventQuery(ev_glaunch) != hipSuccess) {
+            bool try_update = topo && graph_update;
+            if (try_update && hipEventQuery(sl.ev_launch) != hipSuccess) {
                 (void)hipGetLastError();  // hipErrorNotReady is no error here
                 try_update = false;
             }
-            if (!try_update) drop_graph();
+            if (!try_update) drop_slot(sl);
             if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
                 (void)hipGetLastError();
                 graphs_ok = false;
@@ -2475,9 +2562,15 @@ struct BundleAdjuster {
             }
             bool ok = true;
             try {
-                enqueue_start(cfg.lambda_init);
-                for (int i = 0; i < k; ++i) enqueue_iteration(cfg, i);
-                enqueue_decide(cfg, k);
+                if (dm) {
+                    enqueue_start_d(cfg.lambda_init, wcap);
+                    for (int i = 0; i < k; ++i) enqueue_iteration_d(cfg, i, wcap);
+                    enqueue_decide_d(cfg, k);
+                } else {
+                    enqueue_start(cfg.lambda_init);
+                    for (int i = 0; i < k; ++i) enqueue_iteration(cfg, i);
+                    enqueue_decide(cfg, k);
+                }
             } catch (...) {
                 ok = false;
             }
@@ -2488,20 +2581,20 @@ struct BundleAdjuster {
             if (ok && try_update) {
                 hipGraphNode_t err_node = nullptr;
                 hipGraphExecUpdateResult r = hipGraphExecUpdateError;
-                updated = hipGraphExecUpdate(gexec, g, &err_node, &r) == hipSuccess && r == hipGraphExecUpdateSuccess;
+                updated = hipGraphExecUpdate(sl.exec, g, &err_node, &r) == hipSuccess && r == hipGraphExecUpdateSuccess;
                 if (!updated) {
                     (void)hipGetLastError();
-                    drop_graph();  // (its last launch has completed: destroyed at once)
+                    drop_slot(sl);  // (its last launch has completed: destroyed at once)
                 }
             }
-            if (ok && !updated && hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess) {
-                gexec = nullptr;
+            if (ok && !updated && hipGraphInstantiate(&sl.exec, g, nullptr, nullptr, 0) != hipSuccess) {
+                sl.exec = nullptr;
                 ok = false;
             }
             const auto tg2 = std::chrono::steady_clock::now();
             if (g) (void)hipGraphDestroy(g);
             if (prof_env)
-                fprintf(stderr, "[rsvio] graph us: drop+capture %.1f %s %.1f destroy %.1f\n",
+                fprintf(stderr, "[rsvio] graph us (%s): drop+capture %.1f %s %.1f destroy %.1f\n", dm ? "desc" : "value",
                         std::chrono::duration<double, std::micro>(tg1 - tg0).count(),
                         updated ? "update" : "instantiate",
                         std::chrono::duration<double, std::micro>(tg2 - tg1).count(),
@@ -2511,15 +2604,18 @@ struct BundleAdjuster {
                 graphs_ok = false;
                 return false;
             }
-            g_k = k;
-            g_cfg = cfg;
-            g_export = export_on;
-            g_nf = G.n_free;
-            g_coll = coll;
-            g_stale = false;
+            sl.k = k;
+            sl.cfg = cfg;
+            sl.exp = export_on;
+            sl.nf = G.n_free;
+            sl.coll = coll;
+            sl.stale = false;
+            sl.wcap = wcap;
+            sl.chunk = G.n_chunk;
+            sl.dptr = dm ? static_cast<const void*>(dptr()) : nullptr;
         }
-        RSVIO_HIP(hipGraphLaunch(gexec, stream));
-        if (graph_update) RSVIO_HIP(hipEventRecord(ev_glaunch, stream));
+        RSVIO_HIP(hipGraphLaunch(sl.exec, stream));
+        if (graph_update) RSVIO_HIP(hipEventRecord(sl.ev_launch, stream));
         return true;
     }
     int last_iterations = 3;  // first chunk = previous solve's iteration count
@@ -2533,7 +2629,7 @@ struct BundleAdjuster {
     hipEvent_t ev_up = nullptr;
     bool up_pending = false;
     struct ArenaLayout {
-        size_t pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, wave_lm, key, ouv, upload;
+        size_t desc, pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, wave_lm, key, ouv, upload;
         size_t hdr, uv, pairs, total;  // built on the device
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
@@ -2543,7 +2639,6 @@ struct BundleAdjuster {
     // caller that never reads the state back (re-solving a resident window) pays nothing for it
     HostBuf<double> h_out;
     bool state_export = false, export_on = false;
-    bool g_export = false;  // export_on of the captured graph
     bool state_fresh = false;  // set_problem without a run since: get_state resets the buffers first
     // host scratch of set_problem, kept across problems (no per-problem allocations)
     std::vector<int> hs_free, hs_pb_fa, hs_pb_fb;
@@ -2580,7 +2675,11 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_up, hipEventDisableTiming));
-        RSVIO_HIP(hipEventCreateWithFlags(&ev_glaunch, hipEventDisableTiming));
+        RSVIO_HIP(hipEventCreateWithFlags(&gv.ev_launch, hipEventDisableTiming));
+        RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
+        RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
+        const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
+        desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
         graph_update = !(gu && gu[0] == '0');
         h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
@@ -2618,7 +2717,9 @@ struct BundleAdjuster {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev_up) (void)hipEventDestroy(ev_up);
-        if (ev_glaunch) (void)hipEventDestroy(ev_glaunch);
+        if (gv.ev_launch) (void)hipEventDestroy(gv.ev_launch);
+        if (gd.ev_launch) (void)hipEventDestroy(gd.ev_launch);
+        if (ev_desc) (void)hipEventDestroy(ev_desc);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -2672,6 +2773,30 @@ struct BundleAdjuster {
     // headers, the (u, v) layout and the Schur pair lists are written on the device in one launch
     // (ba_build_layout) after one H2D copy.  No stream synchronisation: the initial state is
     // set by the solve's first kernel (K4 with K0 folded in).
+    // the per-problem work buffers, grown to the uploaded window (G set)
+    void grow_buffers() {
+        const int n_kf = G.n_kf, n_lm = G.n_lm, n_pb = G.n_pb, n_free = G.n_free, n_wave = G.n_wave;
+        grow(d_pose2, 14 * (size_t)n_kf);
+        grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
+        {  // partial systems: every entry of every slot is written by K4c each iteration; zeroed
+           // once when (re)allocated
+            const size_t nc = (size_t)kGrp * ((size_t)36 * n_pb + 12 * n_free + 2);
+            if (d_cpart.n < nc) {
+                grow(d_cpart, nc);
+                RSVIO_HIP(hipMemsetAsync(d_cpart.p, 0, sizeof(double) * d_cpart.n, stream));
+            }
+        }
+        grow(d_raws, (size_t)2 * kRawF * std::max<size_t>(n_pad, 1));
+        grow(d_rawl, (size_t)2 * kLmF * std::max(n_lm, 1));
+        grow(d_singular, 1);
+        grow(d_partA, (size_t)kPartA * std::max(n_wave, 1));
+        grow(d_partD, (size_t)kPartD * std::max(n_wave, 1));
+        grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
+        grow(d_dc, (size_t)6 * n_free);
+        grow(d_trial4, 4);
+        grow(d_state, 2);
+    }
+
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
                      const int32_t* obs_lm, const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,
                      const double* TCB2) {
@@ -2691,10 +2816,11 @@ struct BundleAdjuster {
         if (pend.active) throw CallOrderError("set_problem: a solve is in flight (call rsvio_ba_wait first)");
         // kernel arguments (sizes, buffers) change with the problem: the exec is updated or
         // replaced by the next start
-        if (graph_update && gexec)
-            g_stale = true;
+        if (graph_update && gv.exec)
+            gv.stale = true;
         else
-            drop_graph();
+            drop_slot(gv);
+        solves_of_problem = 0;
         state_export = false;
         if (n_kf < 1 || n_kf > P.max_keyframes || n_lm < 0 || n_lm > P.max_landmarks || n_obs < 0 ||
             n_obs > P.max_observations)
@@ -2722,6 +2848,7 @@ struct BundleAdjuster {
         const size_t nl1 = (size_t)std::max(n_lm, 1);
         ArenaLayout L{};
         size_t off = 0;
+        L.desc = off;      off += al(sizeof(WinDesc));  // descriptor mode's WinDesc (start_graph)
         L.pose_init = off; off += al(sizeof(double) * 7 * (size_t)n_kf);
         L.pw_init = off;   off += al(sizeof(double) * 3 * nl1);
         L.free_idx = off;  off += al(sizeof(int) * (size_t)n_kf);
@@ -2830,14 +2957,17 @@ struct BundleAdjuster {
         std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
         mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
-        mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.mask, hipMemcpyHostToDevice, stream));
-        RSVIO_HIP(hipEventRecord(ev_up, stream));
-        up_pending = true;
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
+        grow_buffers();  // (before the descriptor: it holds their addresses)
+        fill_desc(hdesc);
+        std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
+        mark();
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.mask, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipEventRecord(ev_up, stream));
+        up_pending = true;
         {
             SlotSrc S;
             S.mask = reinterpret_cast<const unsigned long long*>(d_arena.p + L.mask);
@@ -2855,25 +2985,6 @@ struct BundleAdjuster {
             RSVIO_HIP(hipGetLastError());
         }
         mark();
-        grow(d_pose2, 14 * (size_t)n_kf);
-        grow(d_pw2, 6 * (size_t)std::max(n_lm, 1));
-        {  // partial systems: every entry of every slot is written by K4c each iteration; zeroed
-           // once when (re)allocated
-            const size_t nc = (size_t)kGrp * ((size_t)36 * n_pb + 12 * n_free + 2);
-            if (d_cpart.n < nc) {
-                grow(d_cpart, nc);
-                RSVIO_HIP(hipMemsetAsync(d_cpart.p, 0, sizeof(double) * d_cpart.n, stream));
-            }
-        }
-        grow(d_raws, (size_t)2 * kRawF * std::max<size_t>(n_pad, 1));
-        grow(d_rawl, (size_t)2 * kLmF * std::max(n_lm, 1));
-        grow(d_singular, 1);
-        grow(d_partA, (size_t)kPartA * std::max(n_wave, 1));
-        grow(d_partD, (size_t)kPartD * std::max(n_wave, 1));
-        grow(d_sys, (size_t)36 * n_pb + 12 * n_free + 2);
-        grow(d_dc, (size_t)6 * n_free);
-        grow(d_trial4, 4);
-        grow(d_state, 2);
         *h_state.p = LmState{};  // cur = 0: buffer 0 holds the initial state once it is set
         state_fresh = true;
         has_problem = true;
@@ -2993,6 +3104,34 @@ struct BundleAdjuster {
         // reads state copy it & 1 (the last iteration's pending trial), writes copy (it + 1) & 1
         hipLaunchKernelGGL(ba_lm_decide, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, G, prob(),
                            work(it), sharded() ? 1 : 0, lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
+        RSVIO_HIP(hipGetLastError());
+    }
+
+    // descriptor mode (start_graph): K4, the LM iterations and K7 from the device descriptor, K4 / K6 on
+    // wcap >= n_wave workgroups -- the same kernels' bodies as enqueue_start / _iteration / _decide
+    void enqueue_start_d(double lambda0, int wcap) {
+        hipLaunchKernelGGL(bab_linearize, dim3(wcap, 1), dim3(64), 0, stream, dptr(), lambda0);
+        RSVIO_HIP(hipGetLastError());
+    }
+    void enqueue_iteration_d(const rsvio_lm_cfg& cfg, int it, int wcap) {
+        const int wi = it & 1;  // work(it) depends on the parity of it only
+        hipLaunchKernelGGL(bab_schur_chunks, dim3(G.n_chunk, 1), dim3(kSchurThreads), 0, stream, dptr(), wi, lm_args(cfg));
+        RSVIO_HIP(hipGetLastError());
+        switch (G.n_free) {
+#define RSVIO_CAMD(NF) \
+    case NF: hipLaunchKernelGGL(bab_camera_solve<NF>, dim3(1), dim3(kK5Threads), 0, stream, dptr(), wi); break;
+            RSVIO_CAMD(1) RSVIO_CAMD(2) RSVIO_CAMD(3) RSVIO_CAMD(4) RSVIO_CAMD(5)
+            RSVIO_CAMD(6) RSVIO_CAMD(7) RSVIO_CAMD(8) RSVIO_CAMD(9) RSVIO_CAMD(10)
+#undef RSVIO_CAMD
+            default: throw std::logic_error("descriptor mode: more than 10 free keyframes");
+        }
+        RSVIO_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bab_backsub_relinearize, dim3(wcap, 1), dim3(64), 0, stream, dptr(), wi);
+        RSVIO_HIP(hipGetLastError());
+    }
+    void enqueue_decide_d(const rsvio_lm_cfg& cfg, int it) {
+        hipLaunchKernelGGL(bad_lm_decide, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, dptr(), it & 1,
+                           lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
         RSVIO_HIP(hipGetLastError());
     }
 

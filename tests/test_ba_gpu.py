@@ -322,6 +322,75 @@ def test_recapture_after_ticket_wait(gpu, cfg3):
     a.close()
 
 
+def test_descriptor_graph_equals_by_value(gpu, cfg3, monkeypatch, capfd):
+    """The first solve of a new window runs the descriptor-mode graph (the window's geometry and
+    buffers read from its device descriptor, K4 / K6 over a rounded-up wave grid whose spare
+    workgroups return at once); a window solved again replays the by-value graph.  Over a sequence
+    of windows -- same shape (the exec replayed as it stands, no capture), fewer landmarks within
+    the rounded-up grid (replayed, spare workgroups), far smaller (re-captured), a changed LM
+    configuration (the descriptor refreshed) -- every solve equals, bit for bit, the same solve on
+    a handle with the descriptor mode off (RSVIO_BA_DESC=0: by-value kernels captured per window)."""
+    from rsvio import synthetic as S
+    from rsvio.ba import BundleAdjuster, fallback_cfg, lm_cfg
+    windows = [cfg3, S.ba_problem(seed=17, init_seed=23), S.ba_problem(n_lm=1900, seed=5, init_seed=6),
+               S.ba_problem(n_kf=6, n_lm=300, seed=7), cfg3]
+    cfgs = [lm_cfg(), lm_cfg(), lm_cfg(), lm_cfg(), fallback_cfg()]
+
+    def mk():
+        return BundleAdjuster(max_keyframes=21, max_landmarks=2000, max_observations=24000)
+
+    monkeypatch.setenv("RSVIO_BA_DESC", "0")
+    v = mk()
+    monkeypatch.delenv("RSVIO_BA_DESC")
+    monkeypatch.setenv("RSVIO_BA_PROFILE", "1")
+    d = mk()
+    monkeypatch.delenv("RSVIO_BA_PROFILE")
+    for h in (v, d):  # warm-up: the first chunk of a solve is the previous solve's iteration count,
+        h.set_problem_from(cfg3)  # and the state read-back turns the final decision's export on
+        h.run()
+        h.state()
+        last = h.run().iterations
+
+    def n_wave(p):  # set_problem's greedy packing: whole landmarks, <= 64 slots (keyframes) a wave
+        keys = np.unique(p.obs_lm.astype(np.int64) * 64 + p.obs_kf)
+        slots = np.bincount(keys // 64, minlength=p.n_lm)
+        n, fill = 0, 64
+        for ns in slots[slots > 0]:
+            if fill + ns > 64:
+                n, fill = n + 1, 0
+            fill += ns
+        return n
+
+    captures, expected = [], []
+    key, cap = None, 0
+    for w, c in zip(windows, cfgs):
+        for h in (v, d):
+            h.set_problem_from(w)
+        capfd.readouterr()
+        for rep in range(2):  # the descriptor graph, then the window re-solved by the by-value one
+            rv, rd = v.run(c), d.run(c)
+            assert (rv.status, rv.iterations, rv.initial_cost, rv.final_cost) == \
+                (rd.status, rd.iterations, rd.initial_cost, rd.final_cost)
+            assert rd.status > 0
+            pv, wv = v.state()
+            pd, wd = d.state()
+            assert np.array_equal(pv, pd) and np.array_equal(wv, wd)
+            if rep == 0:
+                captures.append(capfd.readouterr().err.count("graph us (desc)"))
+                # replayed iff the shape key agrees and the wave count fits the captured grid
+                nw, k = n_wave(w), min(last, c.max_iterations)
+                kk = (k, int((w.kf_fixed == 0).sum()), c.max_iterations, c.linear_solver)
+                hit = kk == key and nw <= cap and 8 * nw > 7 * cap
+                expected.append(0 if hit else 1)
+                if not hit:
+                    key, cap = kk, (nw + nw // 16 + 7) // 8 * 8
+            last = rd.iterations
+    assert captures == expected, (captures, expected)
+    assert expected[1] == 0 or expected[2] == 0  # a replay happened (same shape / fewer landmarks)
+    v.close()
+    d.close()
+
+
 def test_observation_order_is_irrelevant(gpu, cfg3):
     """set_problem builds the slot layout from per-landmark (keyframe, camera) masks, not from the
     input order: a shuffled observation list gives the same solve, bit for bit."""
