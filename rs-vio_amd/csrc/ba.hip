@@ -40,6 +40,8 @@
 #include <vector>
 
 #include "common.hpp"
+
+#include <immintrin.h>  // host: set_problem's vectorised observation pass
 #include "se3.hpp"
 #include "wave.hpp"
 
@@ -2406,6 +2408,88 @@ RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 RSVIO_RT_READER(rsvio_dbg_ba_rt)
 
 // ======================================================================================
+// set_problem's observation pass, fast path (host).  Keys l << 6 | k << 1 | c with the index
+// validation, 8 observations per AVX2 step (when the host has it); false if an index is out of
+// range (the exact pass then reports which).
+__attribute__((target("avx2"))) static bool obs_keys_avx2(int n_obs, const int32_t* lm, const int32_t* kf,
+                                                        const uint8_t* cam, int n_lm, int n_kf, unsigned* key) {
+    const __m256i nl1 = _mm256_set1_epi32(n_lm - 1), nk1 = _mm256_set1_epi32(n_kf - 1), one = _mm256_set1_epi32(1);
+    __m256i bad = _mm256_setzero_si256();
+    int i = 0;
+    for (; i + 8 <= n_obs; i += 8) {
+        const __m256i l = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(lm + i));
+        const __m256i k = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(kf + i));
+        const __m256i c = _mm256_cvtepu8_epi32(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(cam + i)));
+        // x > n - 1 (unsigned; negative indices are huge)  <=>  max(x, n - 1) != n - 1
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(l, nl1), nl1));
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(k, nk1), nk1));
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(c, one), one));
+        const __m256i kk = _mm256_or_si256(_mm256_or_si256(_mm256_slli_epi32(l, 6), _mm256_slli_epi32(k, 1)), c);
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(key + i), kk);
+    }
+    unsigned bad_t = 0;
+    for (; i < n_obs; ++i) {
+        const unsigned l = (unsigned)lm[i], k = (unsigned)kf[i], c = cam[i];
+        bad_t |= (unsigned)(l >= (unsigned)n_lm) | (unsigned)(k >= (unsigned)n_kf) | (unsigned)(c > 1);
+        key[i] = l << 6 | k << 1 | c;
+    }
+    return _mm256_testz_si256(bad, bad) && !bad_t;
+}
+
+static bool obs_keys(int n_obs, const int32_t* lm, const int32_t* kf, const uint8_t* cam, int n_lm, int n_kf,
+                     unsigned* key) {
+    if (n_lm <= 0 || n_kf <= 0) return false;
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) return obs_keys_avx2(n_obs, lm, kf, cam, n_lm, n_kf, key);
+    unsigned bad = 0;
+    for (int i = 0; i < n_obs; ++i) {
+        const unsigned l = (unsigned)lm[i], k = (unsigned)kf[i], c = cam[i];
+        bad |= (unsigned)(l >= (unsigned)n_lm) | (unsigned)(k >= (unsigned)n_kf) | (unsigned)(c > 1);
+        key[i] = l << 6 | k << 1 | c;
+    }
+    return !bad;
+}
+
+// Per-landmark (keyframe, camera) masks from the keys when each landmark's observations are
+// contiguous (a landmark-major list, as SlidingWindow builds it): four independent chains over
+// run-aligned quarters, each keeping its current run's mask in a register and storing it (no
+// load on the chain).  True iff the masks hold n_obs bits in total -- no duplicate observation and
+// no landmark in two runs; otherwise the exact pass rebuilds them (and reports a duplicate).
+__attribute__((target("popcnt"))) static bool obs_masks_runs(int n_obs, const unsigned* key, int n_lm,
+                                                            unsigned long long* m2) {
+    std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
+    int cut[5];
+    cut[0] = 0;
+    cut[4] = n_obs;
+    for (int q = 1; q < 4; ++q) {
+        int c = std::max((int)((long long)q * n_obs / 4), cut[q - 1]);
+        while (c > 0 && c < n_obs && (key[c] >> 6) == (key[c - 1] >> 6)) ++c;
+        cut[q] = c;
+    }
+    int len = n_obs;
+    for (int q = 0; q < 4; ++q) len = std::min(len, cut[q + 1] - cut[q]);
+    unsigned cl[4] = {~0u, ~0u, ~0u, ~0u};
+    unsigned long long cm[4] = {0, 0, 0, 0};
+    auto step = [&](int q, int i) {
+        const unsigned kj = key[i], l = kj >> 6;
+        const unsigned long long b = 1ull << (kj & 63);
+        cm[q] = l == cl[q] ? (cm[q] | b) : b;
+        cl[q] = l;
+        m2[l] = cm[q];
+    };
+    for (int j = 0; j < len; ++j) {
+        step(0, cut[0] + j);
+        step(1, cut[1] + j);
+        step(2, cut[2] + j);
+        step(3, cut[3] + j);
+    }
+    for (int q = 0; q < 4; ++q)
+        for (int i = cut[q] + len; i < cut[q + 1]; ++i) step(q, i);
+    long long bits = 0;
+    for (int l = 0; l < n_lm; ++l) bits += __builtin_popcountll(m2[l]);
+    return bits == n_obs;
+}
+
 // slots of a landmark = keyframes with any of its observations (bits 2 kf, 2 kf + 1 of its mask)
 __attribute__((target("popcnt"))) static inline int slot_count(unsigned long long m) {
     return __builtin_popcountll((m | (m >> 1)) & kEvenBits);
@@ -2878,8 +2962,11 @@ struct BundleAdjuster {
         // observations: validated, a (keyframe, camera) bit per landmark, packed keys
         auto* m2 = reinterpret_cast<unsigned long long*>(hb + L.mask);
         auto* key = reinterpret_cast<unsigned*>(hb + L.key);
-        std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
-        {
+        // fast path: vectorised keys + validation, masks by run-aligned chains (obs_masks_runs);
+        // anything else (an index out of range, a duplicate, a landmark in two runs) takes the
+        // exact pass below, which reports the error or builds the masks of any order
+        if (!(obs_keys(n_obs, obs_lm, obs_kf, obs_cam, n_lm, n_kf, key) && obs_masks_runs(n_obs, key, n_lm, m2))) {
+            std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
             // the mask of the current run of one landmark's observations stays in a register (a
             // landmark-major list would otherwise chain every read-modify-write of m2[l] through
             // store-to-load forwarding)
