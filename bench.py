@@ -736,17 +736,23 @@ class TrackerWorkload:
         self._plans[key] = plan
         return plan
 
-    def step(self, timed: bool, pcie: bool = False, wait: bool = True):
+    def upload(self):
+        """The next frame's two images up from pinned host memory (the first part of a pcie step:
+        issued as soon as the frame is there; step(..., uploaded=True) enqueues the rest)."""
+        plan = self._plan(self.k % len(self.seq), True)
+        self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, self.stream.cuda_stream))
+
+    def step(self, timed: bool, pcie: bool = False, wait: bool = True, uploaded: bool = False):
         """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches.  pcie:
-        the two images are uploaded from pinned host memory first and the three tracked
-        feature lists (+ valid flags) are downloaded before the step returns (wait=False: they
-        are enqueued and sync() completes the frame)."""
+        the two images are uploaded from pinned host memory first (unless upload() already did)
+        and the three tracked feature lists (+ valid flags) are downloaded before the step
+        returns (wait=False: they are enqueued and sync() completes the frame)."""
         C = self.C
         phase = self.k % len(self.seq)
         assert self.slot == phase % 2
         plan = self._plan(phase, pcie)
         s = self.stream.cuda_stream
-        if pcie:
+        if pcie and not uploaded:
             self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, s))
         self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, plan["src"], 2, plan["dst"], s))
         timed = timed and self.k % 4 == 0  # LK launch time sampled on every 4th frame (event overhead)
@@ -1051,7 +1057,7 @@ def main():
                          "best (round 2 sweep: K4c's 360 two-wave-per-SIMD workgroups fit the BA's 192 CUs "
                          "in one round)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
-    ap.add_argument("--order", default="ba-first", choices=["frame-first", "ba-first"],
+    ap.add_argument("--order", default="ba-first", choices=["frame-first", "ba-first", "split"],
                     help="protocol step: enqueue the frame (image upload, pyramids, LK, feature download) "
                          "before the keyframe window's upload + solve start, or after; both run concurrently "
                          "either way (the tracker does not depend on the solve); ba-first measured faster (3.93k vs 3.64-3.68k "
@@ -1101,13 +1107,16 @@ def main():
         launch); then the frame's features, the solve and its optimised state (48.6 KB, published
         to pinned host memory with the solve's last decision) are waited for.  Default order
         (ba-first): the window and the solve are enqueued before the frame; --order frame-first
-        the other way round."""
+        the other way round; --order split: the frame's image upload first (as soon as the frame
+        is there), then the window and the solve, then the frame's kernels and downloads."""
         if args.order == "frame-first":
             trk.step(timed, pcie=True, wait=False)
+        elif args.order == "split":
+            trk.upload()
         ba.next_window()
         ba.start()
-        if args.order == "ba-first":
-            trk.step(timed, pcie=True, wait=False)
+        if args.order != "frame-first":
+            trk.step(timed, pcie=True, wait=False, uploaded=args.order == "split")
         trk.sync()
         ba.finish(timed)
         ba.ba.state(state_out)

@@ -2617,23 +2617,31 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventRecord(ev_desc, stream));
         desc_pending = true;
     }
-    bool start_graph(const rsvio_lm_cfg& cfg, int k) {
+    // k: the first chunk wanted (the previous solve's iteration count); on return, the chunk the
+    // launched exec enqueues
+    bool start_graph(const rsvio_lm_cfg& cfg, int& k) {
         if (coll == 1 || !graphs_ok) return false;
         const bool dm = desc_mode() && solves_of_problem == 0;
         ++solves_of_problem;
         GraphSlot& sl = dm ? gd : gv;
         if (dm && (G.huber_delta != desc_huber || G.chol != desc_chol)) refresh_desc();
-        // K4 / K6 grid of a capture: n_wave + 1/16 headroom (the next window of a similar shape
-        // replays it), a multiple of 8 (wave w on XCD w % 8 either way); spare workgroups return
-        const int wcap = (G.n_wave + G.n_wave / 16 + kGrp - 1) / kGrp * kGrp;
-        const bool topo = sl.exec && sl.k == k && same_cfg(sl.cfg, cfg) && sl.exp == export_on && sl.nf == G.n_free &&
+        // K4 / K6 grid of a capture: n_wave + 1/4 headroom (the next windows of a similar shape
+        // replay it while n_wave > wcap / 2), a multiple of 8 (wave w on XCD w % 8 either way);
+        // spare workgroups return at once
+        const int wcap = (G.n_wave + G.n_wave / 4 + kGrp - 1) / kGrp * kGrp;
+        // descriptor mode: an exec whose first chunk is up to 2 iterations longer than wanted is
+        // replayed too (iterations past convergence return at once; cheaper than a re-capture when
+        // consecutive windows converge in slightly different counts, as the Estimator's do)
+        const bool k_ok = sl.k == k || (dm && sl.k > k && sl.k <= k + 2);
+        const bool topo = sl.exec && k_ok && same_cfg(sl.cfg, cfg) && sl.exp == export_on && sl.nf == G.n_free &&
                           sl.coll == coll;
         const bool hit = topo && (dm ? (sl.dptr == dptr() && sl.chunk == G.n_chunk && G.n_wave <= sl.wcap &&
-                                        8 * G.n_wave > 7 * sl.wcap)
+                                        2 * G.n_wave > sl.wcap)
                                      : !sl.stale);
+        if (hit) k = sl.k;
         if (!hit) {
             const auto tg0 = std::chrono::steady_clock::now();
-            bool try_update = topo && graph_update;
+            bool try_update = topo && sl.k == k && graph_update;
             if (try_update && hipEventQuery(sl.ev_launch) != hipSuccess) {
                 (void)hipGetLastError();  // hipErrorNotReady is no error here
                 try_update = false;
@@ -3283,7 +3291,7 @@ struct BundleAdjuster {
         settled = false;
         state_fresh = false;  // K4 (K0 folded in) sets both state buffers
         if (!pend.by_tick) RSVIO_HIP(hipEventRecord(ev0, stream));  // the ticket carries device stamps
-        const int k = std::min(std::max(last_iterations, 1), pend.max_it);
+        int k = std::min(std::max(last_iterations, 1), pend.max_it);
         // a new problem (every keyframe in the Estimator) is re-captured: capture + instantiate +
         // one launch measured cheaper in host time than its ~25 direct launches (config-4 BA stage
         // 0.100 vs 0.115 ms per frame, round 2), so graphs stay on for fresh problems too
