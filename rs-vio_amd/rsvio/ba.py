@@ -283,12 +283,28 @@ class SlidingWindow:
     def __init__(self, max_frames: int, device: int = 0, solver: BundleAdjuster | None = None):
         self.max_frames = max_frames
         self.keyframes: deque[Frame] = deque()
-        self.map_points: dict[int, np.ndarray] = {}  # feature id -> [f32; 3]
-        self.map_version = 0                           # bumped whenever map_points is replaced
+        # map_points (feature id -> [f32; 3], sliding_window.rs:466-475) as ascending ids + an f32
+        # n x 3 array: what the next problem build and the PnP map upload read, with no per-point
+        # Python work (map_points is the dict view of the same map)
+        self.map_ids = np.zeros(0, np.int64)
+        self.map_pw = np.zeros((0, 3), np.float32)
+        self.map_version = 0                           # bumped whenever the map is replaced
         self.fallbacks = 0                             # SparseCholesky retries (diagnostic)
         self.solver = solver or BundleAdjuster(max_keyframes=max(max_frames, 2), device=device)
         self.last_result = None
         self._pending = None                           # landmark ids of a solve in flight (optimize_async)
+
+    @property
+    def map_points(self) -> dict:
+        return dict(zip(self.map_ids.tolist(), self.map_pw))
+
+    @map_points.setter
+    def map_points(self, mp: dict):
+        ids = np.fromiter(mp.keys(), np.int64, len(mp))
+        pw = (np.stack([np.asarray(v, np.float32) for v in mp.values()]) if len(mp)
+              else np.zeros((0, 3), np.float32))
+        srt = np.argsort(ids, kind="stable")
+        self.map_ids, self.map_pw = ids[srt], pw[srt].reshape(-1, 3)
 
     def add_frame(self, frame: Frame) -> bool:
         if not frame.is_keyframe:
@@ -335,11 +351,8 @@ class SlidingWindow:
         lm_ids = uniq[order]
         p_init = np.zeros((len(lm_ids), 3))
         in_map = np.zeros(len(lm_ids), bool)
-        if self.map_points:
-            mid = np.fromiter(self.map_points.keys(), np.int64, len(self.map_points))
-            mpw = np.stack([np.asarray(v, np.float32) for v in self.map_points.values()]).astype(np.float64)
-            srt = np.argsort(mid)
-            mid, mpw = mid[srt], mpw[srt]
+        if len(self.map_ids):
+            mid, mpw = self.map_ids, self.map_pw.astype(np.float64)  # ascending ids
             pos = np.clip(np.searchsorted(mid, lm_ids), 0, len(mid) - 1)
             in_map = mid[pos] == lm_ids
             p_init[in_map] = mpw[pos[in_map]]
@@ -362,8 +375,7 @@ class SlidingWindow:
         kf_fixed = np.zeros(len(kfs), np.uint8)
         kf_fixed[0] = 1
         T_C_B2 = np.stack([T_Cl_B.reshape(16), T_Cr_B.reshape(16)])
-        return (pose7, kf_fixed, p_init, obs_lm, kf.astype(np.int32), cam, uv, T_C_B2,
-                [int(x) for x in lm_ids])
+        return (pose7, kf_fixed, p_init, obs_lm, kf.astype(np.int32), cam, uv, T_C_B2, lm_ids)
 
     def optimize(self, cfg=None) -> bool:
         """Returns Ok(true)/Ok(false) as a bool; raises RuntimeError for a non-full window (:137-149)."""
@@ -389,8 +401,8 @@ class SlidingWindow:
         self.last_result = res
         if res.status <= 0:
             return False  # revert: nothing was modified
-        pw32 = pw.astype(np.float32)
-        self.map_points = dict(zip(ids, pw32))
+        srt = np.argsort(ids, kind="stable")  # (ids are distinct)
+        self.map_ids, self.map_pw = np.asarray(ids, np.int64)[srt], pw.astype(np.float32)[srt]
         self.map_version += 1
         T_W_B = np.linalg.inv(np.stack([se3_matrix(pose[i]) for i in range(len(self.keyframes))]))
         for f, T in zip(self.keyframes, T_W_B):

@@ -122,9 +122,7 @@ class Estimator:
         self.flush()
         if self.window.is_full():
             if self.window.map_version != self._map_key:  # map_points changes only in optimize
-                mp = self.window.map_points
-                ids = np.array(sorted(mp), np.int64)
-                self.backend.set_map(ids, np.stack([mp[i] for i in ids]) if len(ids) else np.zeros((0, 3), np.float32))
+                self.backend.set_map(self.window.map_ids, self.window.map_pw)  # ascending ids, f32
                 self._map_key = self.window.map_version
             status, is_kf, T_W_B = self.backend.track_motion(self.window.get_keyframe_poses()[-1], self._T_C_B2())
             pnp_status = status

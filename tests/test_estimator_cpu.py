@@ -69,7 +69,7 @@ def test_build_problem_matches_loop(seed):
     sw.map_points = {int(i): rng.normal(0, 3, 3).astype(np.float32) for i in rng.choice(120, 50, replace=False)}
     pose7, fixed, p_init, lm, kf, cam, uv, tcb, ids = sw.build_problem()
     p_ref, lm_ref, kf_ref, cam_ref, uv_ref, ids_ref = _loop_build(list(sw.keyframes), sw.map_points)
-    assert ids == ids_ref
+    assert [int(x) for x in ids] == ids_ref
     assert np.array_equal(lm, lm_ref) and np.array_equal(kf, kf_ref) and np.array_equal(cam, cam_ref)
     assert np.array_equal(uv, uv_ref)
     assert np.abs(p_init - p_ref).max() <= 1e-12
@@ -88,7 +88,7 @@ def test_build_problem_array_features_equal_pairs():
     b = sw.build_problem()
     for x, y in zip(a[:-1], b[:-1]):
         assert np.array_equal(x, y)
-    assert a[-1] == b[-1]
+    assert np.array_equal(a[-1], b[-1])
 
 
 @pytest.mark.slow
