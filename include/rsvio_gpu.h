@@ -317,7 +317,10 @@ int rsvio_ba_solve(rsvio_ba* ba, int32_t n_kf, double* pose7, const uint8_t* kf_
  * order; one per (landmark, keyframe, camera) -- a second is RSVIO_ERR_INVALID_ARG, as is an
  * index out of range.  The host validates the observations and packs per-landmark (keyframe,
  * camera) masks into pinned staging; the slot layout and Schur pair lists are built on the
- * device after one H2D copy.  Does not wait for the previous solve's stream tail. */
+ * device after one H2D copy.  Does not wait for the previous solve's stream tail.  The window's
+ * geometry and buffer addresses also go up as a device descriptor: the first solve of a window
+ * replays a launch graph keyed only by the window's shape (free keyframes, LM configuration, wave
+ * count within a band), so a new keyframe window costs one graph launch, no capture. */
 int rsvio_ba_set_problem(rsvio_ba* ba, int32_t n_kf, const double* pose7, const uint8_t* kf_fixed,
                          int32_t n_lm, const double* p_W, int32_t n_obs, const int32_t* obs_lm,
                          const int32_t* obs_kf, const uint8_t* obs_cam, const double* obs_uv,

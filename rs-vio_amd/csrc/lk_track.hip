@@ -14,6 +14,7 @@
 // are evaluated in f64 and rounded to f32 (glibc sinf differs from that on < 1e-4 of the
 // |theta| < 2^-6 inputs the tracker produces; DESIGN.md "Tracker parity").
 #include "lk_track.hpp"
+#include "se3.hpp"
 #include "trig.hpp"
 
 namespace rsvio {
@@ -135,8 +136,17 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
     return C;
 }
 
+// The correctly rounded f32 quotient a / b as RN_f32(a * (1/b)) in f64, 1/b = rcp_f64 (se3.hpp:
+// ~2^-52 relative): the f64 product is within 2^-51 of a / b, and the quotient of two f32 values
+// is never a rounding midpoint nor within 2^-49 (relative) of one (|A 2^k - M B| >= 1 for the
+// 24-bit significands A, B and a 25-bit midpoint M), so rounding the product to f32 gives exactly
+// a / b -- with the reciprocal off the chain when b is known before a (theta before its sine, the
+// patch sum before the samples' products).
+__device__ __forceinline__ float div_rcp(float a, double rb) { return (float)((double)a * rb); }
+
 // image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos = glibc sinf/cosf (trig.hpp)
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
+    const double rth = rcp_f64((double)theta);  // beside sincosf (the quotients' divisor)
     float s, c;
     libm_trig::sincosf(theta, &s, &c);
     float sin_by, omc_by;
@@ -145,8 +155,8 @@ __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
         sin_by = 1.0f - (1.0f / 6.0f) * th2;
         omc_by = 0.5f * theta - (1.0f / 24.0f) * theta * th2;
     } else {
-        sin_by = s / theta;
-        omc_by = (1.0f - c) / theta;
+        sin_by = div_rcp(s, rth);          // s / theta
+        omc_by = div_rcp(1.0f - c, rth);   // (1 - c) / theta
     }
     Aff E;
     E.m00 = c; E.m01 = -s; E.m10 = s; E.m11 = c;
@@ -355,7 +365,7 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
             lane_chains<1, true>(x1, s1, sh, lane);
             sum = s1[0];
         }
-        const float r = use ? ((float)nv * v / sum - T.data) : 0.0f;
+        const float r = use ? (div_rcp((float)nv * v, rcp_f64((double)sum)) - T.data) : 0.0f;  // nv v / sum
         float inc[3];
         LK_CLK(t2);
         LK_ACC(17, t1, t2);

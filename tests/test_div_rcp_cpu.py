@@ -1,0 +1,34 @@
+"""The LK kernel's exact f32 quotients (csrc/lk_track.hip div_rcp): a / b for f32 a, b is formed
+as RN_f32(a * (1/b)) in f64 with a ~2^-52 reciprocal, which equals the correctly rounded f32
+division (patch.rs:222 nv v / sum, image_utilities.rs:96-97 sin / theta and (1 - cos) / theta)
+because an f32 quotient is never within 2^-49 (relative) of an f32 rounding midpoint.  Checked on
+the kernel's operand ranges and on random significands, with the reciprocal perturbed by up to
+2 f64 ulps (the device's rcp + Newton is within that of 1/b)."""
+import numpy as np
+
+
+def _check(a, b):
+    a, b = a.astype(np.float32), b.astype(np.float32)
+    ref = (a / b).astype(np.float32)
+    r = 1.0 / b.astype(np.float64)
+    for pert in (-2, -1, 0, 1, 2):
+        q = (a.astype(np.float64) * (r * (1.0 + pert * 2.0 ** -52))).astype(np.float32)
+        assert np.array_equal(q, ref)
+
+
+def test_div_rcp_kernel_ranges():
+    rng = np.random.default_rng(7)
+    n = 1_000_000
+    th = (np.exp(rng.uniform(np.log(1.2e-7), np.log(3.0), n)) * rng.choice([-1.0, 1.0], n)).astype(np.float32)
+    _check(np.sin(th).astype(np.float32), th)
+    _check((1.0 - np.cos(th)).astype(np.float32), th)
+    nv = rng.integers(27, 53, n).astype(np.float32)
+    v = rng.uniform(0.0, 255.0, n).astype(np.float32)
+    _check((nv * v).astype(np.float32), rng.uniform(1.0, 13260.0, n).astype(np.float32))
+
+
+def test_div_rcp_random_significands():
+    rng = np.random.default_rng(8)
+    n = 1_000_000
+    _check(rng.uniform(1.0, 2.0, n), rng.uniform(1.0, 2.0, n))
+    _check(rng.uniform(-1e3, 1e3, n), np.exp(rng.uniform(-20, 20, n)))
