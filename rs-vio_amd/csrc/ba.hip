@@ -2189,7 +2189,10 @@ __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work 
 // and copies from host memory.  A slice per CU keeps each CU's PCIe writes within one round of
 // outstanding requests (one block writing all 48.6 KB took ~10 us).
 constexpr int kK7Threads = 256;
-constexpr int kK7Blocks = 16;
+#ifndef RSVIO_K7_BLOCKS  // build-time A/B: 48 blocks measured no faster and less stable
+#define RSVIO_K7_BLOCKS 16  // (profiles/r03w_k7_blocks_ab.txt)
+#endif
+constexpr int kK7Blocks = RSVIO_K7_BLOCKS;
 __device__ __forceinline__ void lm_decide_body(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced,
                                                const LmArgs& la, LmState* host, unsigned long long* htick,
                                                double* hout) {
