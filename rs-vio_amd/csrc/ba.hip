@@ -485,35 +485,39 @@ __device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSr
     const int k0 = nw * wave / 4, k1 = nw * (wave + 1) / 4;
     int4* out = pairs + (size_t)c * G.pair_stride;
     // the run's waves kPairU at a time: their landmark ranges, then the first 64 landmarks' masks
-    // of each, every load of a round in flight together (a wave of more than 64 landmarks --
-    // unobserved ones between observed ones -- continues in a loop)
-    auto round = [&](int kb, bool write, int& acc) {
-        int l0[kPairU], l1[kPairU];
+    // and first slots of each, every load of a round in flight together (a wave of more than 64
+    // landmarks -- unobserved ones between observed ones -- continues in a loop).  The run's first
+    // round (the whole run at config-3 sizes) is loaded once and kept for both passes.
+    struct Round {
+        int l0[kPairU], l1[kPairU], lbs[kPairU];
+        unsigned long long m[kPairU];
+    };
+    auto load = [&](int kb, Round& R) {
 #pragma unroll
         for (int u = 0; u < kPairU; ++u) {
             const int w = x + kGrp * (kb + u);
             const bool in = kb + u < k1;
-            l0[u] = in ? S.wave_lm[w] : 0;
-            l1[u] = in ? S.wave_lm[w + 1] : 0;
-        }
-        unsigned long long m[kPairU];
-        int lbs[kPairU];
-#pragma unroll
-        for (int u = 0; u < kPairU; ++u) {
-            const bool in = l0[u] + lane < l1[u];
-            m[u] = in ? S.mask[l0[u] + lane] : 0ull;
-            lbs[u] = in && write ? S.lm_base[l0[u] + lane] : 0;
+            R.l0[u] = in ? S.wave_lm[w] : 0;
+            R.l1[u] = in ? S.wave_lm[w + 1] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kPairU; ++u) {
-            for (int l = l0[u] + lane; l - lane < l1[u]; l += 64) {
-                const bool first = l == l0[u] + lane;
-                const unsigned long long mm = first ? m[u] : (l < l1[u] ? S.mask[l] : 0ull);
+            const bool in = R.l0[u] + lane < R.l1[u];
+            R.m[u] = in ? S.mask[R.l0[u] + lane] : 0ull;
+            R.lbs[u] = in ? S.lm_base[R.l0[u] + lane] : 0;
+        }
+    };
+    auto scan = [&](const Round& R, bool write, int& acc) {
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u) {
+            for (int l = R.l0[u] + lane; l - lane < R.l1[u]; l += 64) {
+                const bool first = l == R.l0[u] + lane;
+                const unsigned long long mm = first ? R.m[u] : (l < R.l1[u] ? S.mask[l] : 0ull);
                 const bool has = (mm & ma) && (mm & mb);
                 const unsigned long long bal = __ballot(has);
                 if (write && has) {
                     const unsigned long long kbits = (mm | (mm >> 1)) & kEvenBits;
-                    const int lb = first ? lbs[u] : S.lm_base[l];
+                    const int lb = first ? R.lbs[u] : S.lm_base[l];
                     out[acc + __popcll(bal & ((1ull << lane) - 1ull))] =
                         make_int4(lb + __popcll(kbits & below_a), lb + __popcll(kbits & below_b), l, 0);
                 }
@@ -521,14 +525,26 @@ __device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSr
             }
         }
     };
+    Round R0;
+    load(k0, R0);
     int n = 0;  // pass 1: this run's pair count
-    for (int kb = k0; kb < k1; kb += kPairU) round(kb, false, n);
+    scan(R0, false, n);
+    for (int kb = k0 + kPairU; kb < k1; kb += kPairU) {
+        Round R;
+        load(kb, R);
+        scan(R, false, n);
+    }
     if (lane == 0) cnt[wave] = n;
     __syncthreads();
     int base = 0;
     for (int v = 0; v < wave; ++v) base += cnt[v];
     const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-    for (int kb = k0; kb < k1; kb += kPairU) round(kb, true, base);  // pass 2
+    scan(R0, true, base);  // pass 2
+    for (int kb = k0 + kPairU; kb < k1; kb += kPairU) {
+        Round R;
+        load(kb, R);
+        scan(R, true, base);
+    }
     for (int i = total + tid; i < G.pair_stride; i += 256) out[i] = make_int4(-1, 0, 0, 0);
 }
 
