@@ -327,12 +327,29 @@ __device__ void make_templates(const uint8_t* pyr, uint32_t w, uint32_t h, float
 // taken in the reference's order -- sum, residual count, finite increment, norm > 1e6 (all
 // "return false"), convergence ("break" before the update), in-bound after it -- so every outcome
 // and every kept value is the one the sequential code produces.
+// The norm tests without the square root: for x = i0^2 + i1^2 + i2^2 (f32, the reference's order)
+// and a positive normal f32 t, RN(sqrt(x)) < t  <=>  x < m^2 with m the midpoint of t and its
+// predecessor (m has a 25-bit odd significand, so sqrt(x) == m is impossible and m^2 is exact in
+// f64); likewise RN(sqrt(x)) > 1e6  <=>  x > m'^2, m' the midpoint of 1e6 and its successor.
+__device__ __forceinline__ double sq_mid(float a, float b) {
+    const double m = 0.5 * ((double)a + (double)b);
+    return m * m;
+}
+
 __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx, float paty, int lane,
                                Aff& A, int max_iter, float thresh, float* sh) {
     const bool act = lane < NP;
     const float wlim = (float)(im.w - 2), hlim = (float)(im.h - 2);
     const bool tval = T.data >= 0.0f;
     const float mh0 = -T.h0, mh1 = -T.h1, mh2 = -T.h2;
+    const bool thr_mid = thresh >= __FLT_MIN__ && thresh <= __FLT_MAX__;  // (else the sqrt form)
+    const double thr2 = thr_mid ? sq_mid(__int_as_float(__float_as_int(thresh) - 1), thresh) : 0.0;
+    const double big2 = sq_mid(1e6f, __int_as_float(__float_as_int(1e6f) + 1));
+    // the in-bound test of an update (image_utilities::inbound after transform *= exp) is taken
+    // with the next iteration's first test (before any other outcome of that iteration), or after
+    // the loop: no branch between the update and the next gather (the iteration computed on an
+    // out-of-bound transform is discarded, as the reference never computes it)
+    bool oob = false;
     for (int it = 0; it < max_iter; ++it) {
 #ifdef RSVIO_STAMPS
         if (lane == 0 && blockIdx.x < 4096) g_dbg[blockIdx.x * 32 + 15] += 1;
@@ -377,20 +394,22 @@ __device__ bool track_at_level(const LevelImg& im, const Template& T, float patx
         LK_ACC(18, t2, t3);
         const float i0 = inc[0], i1 = inc[1], i2 = inc[2];
         const bool fin = isfinite(i0) && isfinite(i1) && isfinite(i2);
-        const float nrm = sqrtf(i0 * i0 + i1 * i1 + i2 * i2);
+        const float nx = i0 * i0 + i1 * i1 + i2 * i2;
 #ifdef RSVIO_STAMPS
         if (lane == 0 && blockIdx.x < 4096 && !(fabsf(i2) < 0.0625f)) g_dbg[blockIdx.x * 32 + 21] += 1;
 #endif
+        const bool too_big = (double)nx > big2;  // nrm > 1e6 (nx = +inf included; NaN: false, as the sqrt)
+        const bool conv = thr_mid ? (double)nx < thr2 : sqrtf(nx) < thresh;  // nrm < thresh
         const Aff An = mul3(A, se2_exp(i0, i1, i2));
         const bool inb2 = inbound(im, An.m02, An.m12, 2);
         LK_CLK(t4);
         LK_ACC(19, t3, t4);
-        if (sum < __FLT_EPSILON__ || !(nres > NP / 2) || !fin || nrm > 1e6f) return false;
-        if (nrm < thresh) break;
+        if (oob || sum < __FLT_EPSILON__ || !(nres > NP / 2) || !fin || too_big) return false;
+        if (conv) break;
         A = An;
-        if (!inb2) return false;
+        oob = !inb2;
     }
-    return true;
+    return !oob;
 }
 
 // track_one_point (feature_tracker.rs:292-342): the L templates first (make_templates), then

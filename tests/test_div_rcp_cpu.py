@@ -32,3 +32,28 @@ def test_div_rcp_random_significands():
     n = 1_000_000
     _check(rng.uniform(1.0, 2.0, n), rng.uniform(1.0, 2.0, n))
     _check(rng.uniform(-1e3, 1e3, n), np.exp(rng.uniform(-20, 20, n)))
+
+
+def _f32_step(t, d):
+    return np.frombuffer((np.frombuffer(np.float32(t).tobytes(), np.int32) + d).tobytes(), np.float32)[0]
+
+
+def test_norm_threshold_without_sqrt():
+    """track_at_level's norm tests (feature_tracker.rs:376-384) without the square root: for f32 x
+    and a positive normal f32 t, RN(sqrt(x)) < t  <=>  x < m^2 in f64, m the midpoint of t and its
+    predecessor; RN(sqrt(x)) > 1e6  <=>  x > m'^2, m' the midpoint of 1e6 and its successor.
+    Every f32 x within 2^17 ulps of t^2, and random x over the whole positive range."""
+    rng = np.random.default_rng(9)
+    rand = np.frombuffer(rng.integers(0, 0x7F800000, 2_000_000, dtype=np.int32).tobytes(), np.float32)
+    for t in (np.float32(0.01), np.float32(1e-3), np.float32(0.5), np.float32(3.0), np.float32(4.7e-38)):
+        m = 0.5 * (float(_f32_step(t, -1)) + float(t))
+        c = np.frombuffer(np.float32(t * t).tobytes(), np.int32)[0]
+        xs = np.frombuffer(np.arange(c - 2 ** 17, c + 2 ** 17, dtype=np.int32).tobytes(), np.float32)
+        for x in (xs, rand):
+            assert np.array_equal(np.sqrt(x) < t, x.astype(np.float64) < m * m)
+    t = np.float32(1e6)
+    m = 0.5 * (float(t) + float(_f32_step(t, 1)))
+    c = np.frombuffer(np.float32(t * t).tobytes(), np.int32)[0]
+    xs = np.frombuffer(np.arange(c - 2 ** 17, c + 2 ** 17, dtype=np.int32).tobytes(), np.float32)
+    for x in (xs, rand):
+        assert np.array_equal(np.sqrt(x) > t, x.astype(np.float64) > m * m)
