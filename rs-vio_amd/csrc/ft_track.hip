@@ -16,6 +16,7 @@
 #include <stdexcept>
 
 #include "ft.hpp"
+#include "se3.hpp"
 #include "trig.hpp"
 
 namespace rsvio {
@@ -281,12 +282,13 @@ __device__ __forceinline__ void iso_apply(const Iso& a, float x, float y, float&
 
 // feature_tracking.rs:195-219, twist [theta, vx, vy]
 __device__ __forceinline__ Iso exp_se2(float theta, float v0, float v1) {
+    const double rth = rcp_f64((double)theta);  // beside sincosf (the quotients' divisor, se3.hpp div_rcp)
     float s, c;
     libm_trig::sincosf(theta, &s, &c);
     float diag, cross;
     if (fabsf(theta) > 1e-4f) {
-        diag = s / theta;
-        cross = (1.0f - c) / theta;
+        diag = div_rcp(s, rth);         // s / theta
+        cross = div_rcp(1.0f - c, rth);  // (1 - c) / theta
     } else {
         const float th2 = theta * theta;
         diag = 1.0f - (theta * theta) / 6.0f;
@@ -400,8 +402,8 @@ __device__ bool track_level(const float* __restrict__ im1, uint32_t w, uint32_t 
             const float z1[1] = {0.0f};
             float s1[1];
             chains<1>(x1, z1, s1, sh, lane);
-            const float mean = s1[0] / (float)NP;
-            r = v / mean - P.data;
+            const float mean = div_rcp(s1[0], 1.0 / NP);  // s1 / 52 (se3.hpp div_rcp)
+            r = div_rcp(v, rcp_f64((double)mean)) - P.data;  // v / mean
         }
         if (!act) r = 0.0f;
         // b = J^T r (gemv: first term is the bare product -> chains start at -0)

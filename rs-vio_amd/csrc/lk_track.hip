@@ -9,10 +9,9 @@
 // H^-1 J^T, its bilinear sample).  Everything the reference sums over the 52 points is summed
 // in the reference's order -- sequential add chains over lanes 0..51, staged through LDS and
 // read back by broadcast ds_read_b128, several independent chains interleaved -- so
-// the result is bit-identical to the scalar Rust/oracle arithmetic (no FMA contraction,
-// correctly rounded f32 divide/sqrt).  The only deviation: sin/cos of the SE(2) increment
-// are evaluated in f64 and rounded to f32 (glibc sinf differs from that on < 1e-4 of the
-// |theta| < 2^-6 inputs the tracker produces; DESIGN.md "Tracker parity").
+// the result is bit-identical to the scalar Rust/oracle arithmetic (no FMA contraction; the
+// quotients exact through an f64 reciprocal, se3.hpp div_rcp; the norm tests exact against
+// squared midpoints; sin/cos = glibc's sinf/cosf restated, trig.hpp).
 #include "lk_track.hpp"
 #include "se3.hpp"
 #include "trig.hpp"
@@ -135,14 +134,6 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
 #undef RSV_EL
     return C;
 }
-
-// The correctly rounded f32 quotient a / b as RN_f32(a * (1/b)) in f64, 1/b = rcp_f64 (se3.hpp:
-// ~2^-52 relative): the f64 product is within 2^-51 of a / b, and the quotient of two f32 values
-// is never a rounding midpoint nor within 2^-49 (relative) of one (|A 2^k - M B| >= 1 for the
-// 24-bit significands A, B and a 25-bit midpoint M), so rounding the product to f32 gives exactly
-// a / b -- with the reciprocal off the chain when b is known before a (theta before its sine, the
-// patch sum before the samples' products).
-__device__ __forceinline__ float div_rcp(float a, double rb) { return (float)((double)a * rb); }
 
 // image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos = glibc sinf/cosf (trig.hpp)
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {

@@ -154,6 +154,14 @@ __device__ __forceinline__ double rcp_f64(double d) {
     return fma(y, fma(e, e, e), y);
 }
 
+// The correctly rounded f32 quotient a / b as RN_f32(a * (1/b)) in f64, 1/b = rcp_f64 (~2^-52
+// relative): the f64 product is within 2^-51 of a / b, and the quotient of two f32 values is never
+// a rounding midpoint nor within 2^-49 (relative) of one (|A 2^k - M B| >= 1 for the 24-bit
+// significands A, B and a 25-bit midpoint M), so rounding the product to f32 gives exactly a / b
+// (tests/test_div_rcp_cpu.py) -- with the reciprocal off the chain when b is known before a (the
+// trackers: theta before its sine, a patch sum before the samples' products).
+__device__ __forceinline__ float div_rcp(float a, double rb) { return (float)((double)a * rb); }
+
 // 1/sqrt(d), f64: hardware estimate + two Newton steps (y <- y (3 - d y^2) / 2)
 __device__ __forceinline__ double rsqrt_f64(double d) {
     double y = __builtin_amdgcn_rsq(d);
