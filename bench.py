@@ -356,6 +356,18 @@ class _StageTimer:
         self.t["track"] += time.perf_counter() - t0
         return out
 
+    def submit(self, l, r):
+        t0 = time.perf_counter()
+        self.be.submit(l, r)
+        self.t["track"] += time.perf_counter() - t0
+
+    def collect(self):
+        """(Estimator.run) the wait for a frame submitted one frame earlier, plus its read-out"""
+        t0 = time.perf_counter()
+        out = self.be.collect()
+        self.t["track"] += time.perf_counter() - t0
+        return out
+
     def track_motion(self, *a):
         t0 = time.perf_counter()
         out = self.be.track_motion(*a)
@@ -372,8 +384,13 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
     resident in HBM): per frame the tracker (6 levels, grid 50, fused radtan unprojection), PnP +
     keyframe rule once the window is full, and a window-10 BA per keyframe; host logic in Python
     between the device calls.  Pipelined: a keyframe's BA runs on its own stream while the next
-    frame is tracked (Estimator(pipelined=True); outputs equal the sequential order's, tests/
-    test_estimator_*).  value = frames / wall time over the whole stream."""
+    frame is tracked (Estimator(pipelined=True)), and the tracker runs one frame ahead
+    (Estimator.run: frame t + 1 is submitted as soon as frame t's features are back, so frame t's
+    host logic, PnP and BA start overlap its tracking); outputs equal the sequential order's
+    (tests/test_estimator_*).  value = frames / wall time over the whole stream.  With the CPU
+    leg, the row is checked frame by frame against the oracle Estimator (keyframe flags, PnP and
+    BA status and iteration counts, pose within 1e-6): a divergent frame FAILS the row (value
+    null, "parity": "failed")."""
     import torch
 
     from rsvio import synthetic as S
@@ -388,7 +405,7 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         be = _StageTimer(DeviceBackend(W, H, cams, 6, 50, MAX_IT, THRESH, 10, 0.05, 0.05, device))
         est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=be, pipelined=True)
         t0 = time.perf_counter()
-        out = [est.process_frame(l, r) for l, r in frames]
+        out = list(est.run(frames))
         est.flush()
         el = time.perf_counter() - t0
         be.be.close()
@@ -400,7 +417,8 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
     err = max(float(np.linalg.norm(r.T_W_B[:3, 3] - T[:3, 3])) for r, T in zip(out, s.T_W_B))
     row = {"workload": f"config 4: Estimator::process_frame over {n_frames} rendered 752x480 stereo frames "
                        "(textured planes at 3-8 m, EuRoC radtan rig, 0.02 m/frame); tracker L=6 grid 50 + "
-                       "unprojection, PnP + keyframe rule, window-10 BA per keyframe (pipelined: the solve overlaps the next frame's tracking)",
+                       "unprojection, PnP + keyframe rule, window-10 BA per keyframe (pipelined: the solve overlaps the "
+                       "next frame's tracking; the tracker one frame ahead: frame t+1 tracks during frame t's PnP and BA start)",
            "value": round(n_frames / el, 3), "unit": "frames/s", "higher_is_better": True,
            "ms_per_frame": round(1e3 * el / n_frames, 4), "keyframes": n_kf, "ba_solves": be.n_solves,
            "ba_lm_iterations_mean": round(be.ba_iters / max(be.n_solves, 1), 2),
@@ -412,8 +430,9 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
                    "(each returns its results to the host, as the reference API does)"}
     if cpu:
         from oracle import oracle as O
-        from oracle.estimator import OracleBackend
+        from oracle.estimator import OracleBackend, outcome_difference
         host = [(l.cpu().numpy(), r.cpu().numpy()) for l, r in s.frames]
+        pnp_tail = []
 
         def oracle_leg(threads, budget_s, compare):
             """The same Estimator host logic over the oracle backend: `threads` = 1 sequential,
@@ -433,8 +452,10 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
                         rd = out[k]
                         d = float(np.abs(rd.T_W_B - ro.T_W_B).max())
                         maxd = max(maxd, d)
-                        if first is None and (rd.is_keyframe != ro.is_keyframe or d > 1e-6 or
-                                              (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)):
+                        diff = outcome_difference(rd, ro)
+                        if diff == "pnp_tail":
+                            pnp_tail.append(k)
+                        if first is None and (d > 1e-6 or diff not in (None, "pnp_tail")):
                             first = k
                     k += 1
             finally:
@@ -449,6 +470,15 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         row["gpu_max_position_error_m_same_frames"] = round(gerr_k, 5)
         row["first_divergent_frame"] = first
         row["max_pose_diff_vs_oracle"] = maxd
+        row["parity_checks"] = ("per frame: keyframe flag and BA status + LM iterations exactly; PnP status + LM "
+                                "iterations exactly except in the converged tail (both succeed, final costs equal "
+                                "to 1e-12: oracle/estimator.py outcome_difference); T_W_B within 1e-6")
+        row["pnp_converged_tail_frames"] = pnp_tail
+        row["parity"] = "ok" if first is None else "failed"
+        if first is not None:  # a number whose outputs differ from the reference path's is no result
+            row["value_unchecked"] = row["value"]
+            row["value"] = None
+            print(f"[bench] config-4 row FAILED parity at frame {first}", file=sys.stderr)
         single = {"value": round(k / cel, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                   "sample": f"the first {k} frames of the same stream through the same Estimator "
                             "host logic over the oracle (oracle/estimator.py), 1 thread",
@@ -1011,11 +1041,12 @@ def cpu_baseline(frames_budget_s: float, threads: int = 1):
     affn[:, 4:6] += np.array([1.7, -0.9], np.float32)
     prob = S.ba_problem()
     pyr_prev = [O.build_pyramid(frames[0][c], LEVELS) for c in range(2)]
-    n, t_track, t_ba = 0, 0.0, 0.0
+    n, t_track, t_ba, t_pyr = 0, 0.0, 0.0, 0.0
     t_start = time.perf_counter()
     while time.perf_counter() - t_start < frames_budget_s or n < 2:
         t0 = time.perf_counter()
         pc = [O.build_pyramid(frames[1][c], LEVELS, threads) for c in range(2)]
+        t_pyr += time.perf_counter() - t0
         O.track_points(pyr_prev[0], pc[0], W, H, LEVELS, aff0, MAX_IT, THRESH, threads)
         O.track_points(pyr_prev[1], pc[1], W, H, LEVELS, aff1, MAX_IT, THRESH, threads)
         O.track_points(pc[0], pc[1], W, H, LEVELS, affn, MAX_IT, THRESH, threads)
@@ -1034,8 +1065,13 @@ def cpu_baseline(frames_budget_s: float, threads: int = 1):
             "sample": f"{n} frames of config 2 (2 pyramids + 3x300 track_points) each followed by one config-3 "
                       f"BA solve ({r.iterations} LM iterations), oracle/ C++ restatement, "
                       + ("1 thread" if threads == 1 else
-                         f"{threads} threads (pyramid levels and features in parallel, threaded Schur BA)"),
-            "tracker_ms_per_frame": round(1e3 * t_track / n, 3), "ba_ms_per_solve": round(1e3 * t_ba / n, 3),
+                         f"{threads} threads of one persistent pool (oracle/pool.hpp: pyramid levels and grains of "
+                         "2 feature tracks claimed dynamically, as rayon's par_iter; threaded Schur BA)"),
+            "tracker_ms_per_frame": round(1e3 * t_track / n, 3),
+            "stage_ms_per_frame": {"pyramids": round(1e3 * t_pyr / n, 3),
+                                   "track_points_900": round(1e3 * (t_track - t_pyr) / n, 3),
+                                   "ba_solve": round(1e3 * t_ba / n, 3)},
+            "ba_ms_per_solve": round(1e3 * t_ba / n, 3),
             "ba_ms_per_iter": round(1e3 * t_ba / n / max(r.iterations, 1), 3)}
 
 
@@ -1240,7 +1276,9 @@ def main():
         cb = cpu_baseline(args.cpu_seconds, cores)
         cb1 = cpu_baseline(args.cpu_seconds / 2, 1)
         cb["single_thread"] = {k: cb1[k] for k in ("value", "cores", "sample", "tracker_ms_per_frame",
-                                                   "ba_ms_per_solve", "ba_ms_per_iter")}
+                                                   "stage_ms_per_frame", "ba_ms_per_solve", "ba_ms_per_iter")}
+        cb["stage_speedup_all_cores_vs_1"] = {k: round(cb1["stage_ms_per_frame"][k] / max(v, 1e-9), 2)
+                                              for k, v in cb["stage_ms_per_frame"].items()}
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 2)
         out["speedup_vs_cpu_single_thread"] = round(value / cb1["value"], 2)

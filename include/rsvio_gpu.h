@@ -91,6 +91,19 @@ int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left,
                                        const uint8_t* d_right, rsvio_feature* out_l,
                                        size_t cap_l, size_t* n_l, rsvio_feature* out_r,
                                        size_t cap_r, size_t* n_r);
+/* process_frame in two halves, for a caller that runs one frame ahead (the Estimator's look-ahead:
+ * estimator.rs:190 passes the tracker only the two images, so frame t+1 can be tracked while frame
+ * t's motion tracking and BA run).  submit enqueues the frame (pyramids, LK, FAST, packing and the
+ * read-back of its lists) and returns at once; collect waits for it and fills the lists exactly as
+ * process_frame does.  One frame in flight per handle: process_frame*, submit*, remove_ids and
+ * set_cameras refuse (RSVIO_ERR_INVALID_ARG) while one is, collect refuses when none is.  Host
+ * images (rsvio_tracker_submit) are borrowed until collect returns.  Consumers of the last
+ * collected frame (rsvio_tracker_undistorted, rsvio_track_motion_tracker) keep reading THAT frame
+ * after a later submit: frames alternate between two device output slots. */
+int rsvio_tracker_submit(rsvio_tracker* t, const uint8_t* left, const uint8_t* right, size_t stride);
+int rsvio_tracker_submit_device(rsvio_tracker* t, const uint8_t* d_left, const uint8_t* d_right);
+int rsvio_tracker_collect(rsvio_tracker* t, rsvio_feature* out_l, size_t cap_l, size_t* n_l,
+                          rsvio_feature* out_r, size_t cap_r, size_t* n_r);
 /* StereoPatchTracker::remove_id (:201-206) */
 int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n);
 /* HIP stream the tracker enqueues on (hipStream_t) */
@@ -418,9 +431,10 @@ int rsvio_track_motion(rsvio_pnp* p, const uint64_t* ids_l, const float* uv_l, s
                        const uint64_t* ids_r, const float* uv_r, size_t n_r,
                        const double* T_W_B_last_kf, const double* T_C_B2, const rsvio_lm_cfg* cfg,
                        const rsvio_keyframe_rule* rule, rsvio_motion_result* res);
-/* Same for the tracker's last frame, read in place on the device (ids, counts and the fused
+/* Same for the tracker's last COLLECTED frame, read in place on the device (ids and the fused
  * undistorted coordinates; needs rsvio_tracker_set_cameras): no host round trip between
- * tracking and motion tracking.  Runs on the tracker's stream. */
+ * tracking and motion tracking.  Runs on the pnp handle's stream, so it may run while the next
+ * frame (rsvio_tracker_submit*) is being tracked: that frame writes the other output slot. */
 int rsvio_track_motion_tracker(rsvio_pnp* p, rsvio_tracker* t, const double* T_W_B_last_kf,
                                const double* T_C_B2, const rsvio_lm_cfg* cfg,
                                const rsvio_keyframe_rule* rule, rsvio_motion_result* res);

@@ -9,6 +9,7 @@
 //     not on disk; its LM is restated as documented in DESIGN.md ("BA LM definition").
 // Accumulation order is sequential: landmarks ascending, observations of a landmark
 // sorted by (kf, cam).
+#include "pool.hpp"
 #include "rsvio_oracle.h"
 
 #include <algorithm>
@@ -188,20 +189,22 @@ struct System {
 };
 
 // Threads of the BA restatement (orc_set_ba_threads; 1 = the sequential reference order).  With
-// T > 1 the landmarks are split into T contiguous ranges whose sums (S, b, g_c, U, cost, the
-// step norms) are combined in range order -- the "threaded Schur variant" CPU leg of BASELINE.md;
-// deterministic for a given T, tolerance-equal to T = 1.
+// T > 1 the landmarks are split into R <= T contiguous ranges (at least kMinRange landmarks each)
+// whose sums (S, b, g_c, U, cost, the step norms) are combined in range order -- the "threaded
+// Schur variant" CPU leg of BASELINE.md; deterministic for a given (T, n), tolerance-equal to
+// T = 1.  The ranges run as tasks of the persistent pool (pool.hpp): an LM iteration's several
+// parallel passes pay no thread start.
 int g_ba_threads = 1;
+constexpr int kMinRange = 48;
 
 template <class F>
-void for_ranges(int n, int T, F&& f) {  // f(range index, begin, end) over T contiguous ranges
-    if (T <= 1 || n < 2 * T) {
+void for_ranges(int n, int T, F&& f) {  // f(range index, begin, end) over R <= T contiguous ranges
+    const int R = std::min(T, n / kMinRange);
+    if (R <= 1) {
         f(0, 0, n);
         return;
     }
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) pool.emplace_back([&, t] { f(t, (int)((long long)n * t / T), (int)((long long)n * (t + 1) / T)); });
-    for (auto& th : pool) th.join();
+    orc::Pool::get().run(R, R, [&](int t) { f(t, (int)((long long)n * t / R), (int)((long long)n * (t + 1) / R)); });
 }
 
 double eval_cost(const Problem& pr, const std::vector<Pose>& poses, const double* pW) {
@@ -319,7 +322,7 @@ System build(const Problem& pr, const std::vector<Pose>& poses, const double* pW
     sy.ok = true;
     std::vector<double> U((size_t)pr.n_free * 36, 0.0);
     const int T = g_ba_threads;
-    if (T <= 1 || pr.n_lm < 2 * T) {
+    if (std::min(T, pr.n_lm / kMinRange) <= 1) {
         build_range(pr, poses, pW, lambda, 0, pr.n_lm, sy, U, sy.lms);
     } else {
         std::vector<System> part(T);

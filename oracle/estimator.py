@@ -46,6 +46,13 @@ class OracleBackend:
         self.solver = OracleSolver(oracle)
         self.map = (np.zeros(0, np.uint64), np.zeros((0, 3), np.float32))
 
+    def submit(self, left, right):
+        self._submitted = (left, right)
+
+    def collect(self):
+        (left, right), self._submitted = self._submitted, None
+        return self.track(left, right)
+
     def track(self, left, right):
         out = []
         for feats, cam in zip(self.tracker.process_frame(left, right), self.cams):
@@ -63,8 +70,31 @@ class OracleBackend:
         (ids_l, uv_l), (ids_r, uv_r) = self.last
         r = self.o.track_motion(ids_l, uv_l, ids_r, uv_r, self.map[0], self.map[1], T_W_B_last_kf, T_C_B2,
                                 thr_t=self.thr[0], thr_r=self.thr[1])
-        return r.status, bool(r.is_keyframe), np.array(r.T_W_B[:]).reshape(4, 4)
+        return r.status, bool(r.is_keyframe), np.array(r.T_W_B[:]).reshape(4, 4), r.iterations, r.final_cost
 
     def close(self):
         pass
 
+
+
+PNP_TAIL_COST_RTOL = 1e-12
+
+
+def outcome_difference(rd, ro):
+    """How the device FrameResult rd differs from the oracle's ro in its integer outcomes: None
+    (keyframe flag, PnP status + LM iterations, BA status + LM iterations all equal), "pnp_tail"
+    (only the PnP's status / iteration count differ, both runs succeeded and their final costs
+    agree to PNP_TAIL_COST_RTOL -- the LM iterated in its converged tail, where the accept test
+    compares cost changes at rounding level, ~1e-15 relative, and the device's fixed-order tree
+    sums and the oracle's sequential sums round differently), or a description of a divergence."""
+    if rd.is_keyframe != ro.is_keyframe:
+        return f"keyframe flag {rd.is_keyframe} vs {ro.is_keyframe}"
+    if (rd.ba_status, rd.ba_iterations) != (ro.ba_status, ro.ba_iterations):
+        return f"BA (status, iterations) {(rd.ba_status, rd.ba_iterations)} vs {(ro.ba_status, ro.ba_iterations)}"
+    pd, po = (rd.pnp_status, rd.pnp_iterations), (ro.pnp_status, ro.pnp_iterations)
+    if pd == po:
+        return None
+    if (rd.pnp_status is not None and ro.pnp_status is not None and rd.pnp_status > 0 and ro.pnp_status > 0
+            and abs(rd.pnp_cost - ro.pnp_cost) <= PNP_TAIL_COST_RTOL * abs(ro.pnp_cost)):
+        return "pnp_tail"
+    return f"PnP (status, iterations) {pd} vs {po}, final cost {rd.pnp_cost} vs {ro.pnp_cost}"

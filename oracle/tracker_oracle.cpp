@@ -4,6 +4,7 @@
 // EthanD11/RS-VIO.  Every floating-point expression keeps the reference's
 // evaluation order (Rust never contracts a*b+c, nalgebra accumulates small
 // products sequentially in k); build with -ffp-contract=off.
+#include "pool.hpp"
 #include "rsvio_oracle.h"
 
 #include <algorithm>
@@ -633,20 +634,18 @@ void orc_build_pyramid(const uint8_t* img, int w, int h, int levels, uint8_t* ou
     }
 }
 
-// build_image_pyramid with rayon's par_iter over levels (feature_tracker.rs:213): one thread
-// per level (the all-cores CPU baseline); the same bytes as orc_build_pyramid
+// build_image_pyramid with rayon's par_iter over levels (feature_tracker.rs:213): the levels as
+// tasks of the persistent pool (pool.hpp; the all-cores CPU baseline); the same bytes as
+// orc_build_pyramid
 void orc_build_pyramid_mt(const uint8_t* img, int w, int h, int levels, uint8_t* out, int n_threads) {
     if (n_threads <= 1 || levels < 2) {
         orc_build_pyramid(img, w, h, levels, out);
         return;
     }
-    std::vector<std::thread> th;
-    for (int i = 0; i < levels; ++i)
-        th.emplace_back([=] {
-            int nw = (int)((uint32_t)w / (1u << i)), nh = (int)((uint32_t)h / (1u << i));
-            orc_resize_triangle(img, w, h, out + orc_pyramid_offset(w, h, i), nw, nh);
-        });
-    for (auto& t : th) t.join();
+    orc::Pool::get().run(levels, std::min(n_threads, levels), [=](int i) {
+        int nw = (int)((uint32_t)w / (1u << i)), nh = (int)((uint32_t)h / (1u << i));
+        orc_resize_triangle(img, w, h, out + orc_pyramid_offset(w, h, i), nw, nh);
+    });
 }
 
 int orc_pattern52_new(const uint8_t* img, int w, int h, float px, float py, float* out_data,
@@ -698,14 +697,11 @@ void orc_track_points(const uint8_t* pyr0, const uint8_t* pyr1, int w, int h, in
         work(0, n);
         return;
     }
-    // rayon par_iter analogue (feature_tracker.rs:260): static per-thread chunks
-    std::vector<std::thread> th;
-    int chunk = (n + n_threads - 1) / n_threads;
-    for (int t = 0; t < n_threads; ++t) {
-        int b = t * chunk, e = std::min(n, b + chunk);
-        if (b < e) th.emplace_back(work, b, e);
-    }
-    for (auto& x : th) x.join();
+    // rayon par_iter analogue (feature_tracker.rs:260): grains of 2 features claimed dynamically
+    // by the persistent pool's threads (the chains' lengths vary by 10x, so static chunks idle)
+    constexpr int kGrain = 2;
+    orc::Pool::get().run((n + kGrain - 1) / kGrain, n_threads,
+                         [&](int g) { work(g * kGrain, std::min(n, (g + 1) * kGrain)); });
 }
 
 int orc_fast9_scores(const uint8_t* img, int w, int h, int threshold, uint8_t* score_out) {

@@ -1433,6 +1433,23 @@ constexpr int kMfPanel = 8;  // panel width: 8 pivots of in-panel VALU work betw
 // row of every panel).  Rows past NP are never initialised: elimination is row-local (a row's
 // update uses its own multiplier and the pivot rows' values), so they cannot leak into the
 // result; the same holds for the upper halves of the diagonal tiles.
+constexpr int kP2PMax = 8;       // ranks
+constexpr int kP2PMsg = 8192;    // doubles per slot (>= 36 * 210 + 12 * 20 + 2)
+
+struct P2P {
+    double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
+    int nranks, rank;
+};
+
+__device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
+    return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
+}
+
+// P2P exchange buffer slot [parity][rank] of a peer's buffer, and the generation flags
+__device__ __forceinline__ double* p2p_slot(double* xbuf, int par, int r) {
+    return xbuf + (size_t)(par * kP2PMax + r) * kP2PMsg;
+}
+
 template <int NF>
 struct MfDims {
     static constexpr int NP = 6 * NF;
@@ -1520,6 +1537,116 @@ __device__ bool combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
             Wk.sys[G.n_pb * 36 + 12 * G.n_free] = c;  // the decision of iteration 0 reads the initial cost here
             *fail = sing;
         }
+    }
+    return false;
+}
+
+// combine_mapped for the landmark-sharded path over the P2P exchange (X1 folded into K5): this
+// rank's reduced system is summed from its partials as combine_mapped does (+ lambda on rank 0,
+// after the sum, as K4d), each entry pushed from its register into slot [parity][rank] of every
+// peer's exchange buffer together with the rank's initial cost and singular flag; after the
+// system-scope flags of every rank have arrived, each thread sums its entries over the slots in
+// RANK ORDER (identical bits on every rank, and the same bits as X1's exchange into sys followed
+// by K5's read of sys) and scatters them into M / gsh by the map.  Returns the state's done flag:
+// every rank takes the same decision, so either all exchange or none does.
+template <int NF>
+__device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
+                            const LmState* st, int* fail, const P2P& P, unsigned long long* xgen, int* err) {
+    constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
+    constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
+    __shared__ unsigned long long sgen;
+    const size_t L = sys_len(G);
+    const int ne = G.n_pb * 36 + 12 * G.n_free;
+    const int tid = threadIdx.x, nr = P.nranks, me = P.rank;
+    double pa[16];
+    int sing = 0;
+    if (tid < 64) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pa[k] = tid + 64 * k < G.n_wave ? Wk.partA[(tid + 64 * k) * kPartA] : 0.0;
+        sing = *Wk.singular;
+    }
+    if (tid == 0) sgen = *xgen + 1;
+    double v[kE][kGrp];
+    int dst[kE];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        dst[i] = e < ne ? Pr.dmap[e] : -1;
+#pragma unroll
+        for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
+    }
+    const int done = st->done;
+    const double lambda = st->lambda;
+#pragma unroll
+    for (int i = 0; i < kE; ++i)
+#pragma unroll
+        for (int x = 0; x < kGrp; ++x) __asm__ volatile("" ::"v"(v[i][x]));
+    if (done) return true;
+    __syncthreads();  // sgen
+    const unsigned long long gen = sgen;
+    const int par = (int)(gen & 1);
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= ne) break;
+        double a = v[i][0];
+#pragma unroll
+        for (int x = 1; x < kGrp; ++x) a += v[i][x];
+        if (me == 0 && dst[i] >= 0 && (dst[i] & kMfMapLambda)) a += lambda;
+        for (int r = 0; r < nr; ++r) p2p_slot(P.peer[r], par, me)[e] = a;
+    }
+    if (tid < 64) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+        c = wave_sum_det(c);
+        if (tid < nr) {  // lane r pushes the scalars to rank r
+            double* d = p2p_slot(P.peer[tid], par, me);
+            d[ne] = c;
+            d[ne + 1] = sing ? 1.0 : 0.0;
+        }
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nr)
+        __hip_atomic_store(p2p_flags(P.peer[tid]) + par * kP2PMax + me, gen, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < nr) {
+        const unsigned long long* f = p2p_flags(P.peer[me]) + par * kP2PMax + tid;
+        long long spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1ll << 25)) {  // a peer never arrived: report, do not hang
+                atomicExch(err, 1);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const double* mine = p2p_slot(P.peer[me], par, 0);
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= ne) break;
+        double a = 0.0;
+        for (int r = 0; r < nr; ++r)
+            a += __hip_atomic_load(mine + (size_t)r * kP2PMsg + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int d = dst[i];
+        if (d >= 0)
+            M[d & (kMfMapLambda - 1)] = a;
+        else if (d <= -2)
+            gsh[-2 - d] = a;
+    }
+    if (tid == 0) {
+        double c = 0.0, f = 0.0;
+        for (int r = 0; r < nr; ++r) {
+            c += __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            f += __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        Wk.sys[ne] = c;  // the decision of iteration 0 reads the (all-reduced) initial cost here
+        *fail = f != 0.0;
+        *xgen = gen;
     }
     return false;
 }
@@ -1640,7 +1767,8 @@ __device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int 
 }
 
 template <int NF>
-__device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine) {
+__device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine,
+                                       const P2P* P = nullptr, unsigned long long* xgen = nullptr, int* err = nullptr) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
     constexpr int NP = MfDims<NF>::NP, NPP = MfDims<NF>::NPP;
     __shared__ __attribute__((aligned(16))) double M[NPP * kMfLd];
@@ -1670,7 +1798,9 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
             for (int i = 0; i < 7; ++i) p7b[b][i] = i == 3 ? 1.0 : 0.0;
     }
     STAMP(0);
-    if (combine) {
+    if (combine == 2) {  // sharded over P2P: this rank's system exchanged in the prologue (X1 folded in)
+        if (combine_p2p<NF>(G, Pr, Wk, M, gsh, st, &fail, *P, xgen, err)) return;
+    } else if (combine) {
         if (combine_mapped<NF>(G, Pr, Wk, M, gsh, st, &fail)) return;
     } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
         if (st->done) return;
@@ -1739,6 +1869,14 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
 template <int NF>
 __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, Prob Pr, Work Wk, int combine) {
     camera_solve_mfma_body<NF>(G, Pr, Wk, combine);
+}
+
+// K5 of the landmark-sharded iteration over the P2P exchange: the exchange of the reduced system
+// (X1: combine + push + flags + rank-ordered sum) in the prologue, then the same factorisation
+template <int NF>
+__global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma_p2p(Geometry G, Prob Pr, Work Wk, P2P P,
+                                                                        unsigned long long* xgen, int* err) {
+    camera_solve_mfma_body<NF>(G, Pr, Wk, 2, &P, xgen, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2328,17 +2466,6 @@ __global__ __launch_bounds__(64) void bab_lm_decide(const WinDesc* __restrict__ 
 // round trip, identical bits on every rank.  Generations alternate two parities, so a rank
 // that runs ahead can never overwrite a slot its slower peer is still reading.
 // ---------------------------------------------------------------------------------------
-constexpr int kP2PMax = 8;       // ranks
-constexpr int kP2PMsg = 8192;    // doubles per slot (>= 36 * 210 + 12 * 20 + 2)
-
-struct P2P {
-    double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
-    int nranks, rank;
-};
-
-__device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
-    return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
-}
 
 // One exchange by a whole 256-thread block: this rank's message msg[0..n) (LDS or global) is
 // pushed into slot [parity][rank] of every peer's buffer, the flags are raised (system-scope
@@ -2605,6 +2732,10 @@ struct BundleAdjuster {
     hipEvent_t ev_desc = nullptr;
     bool desc_pending = false;
     bool desc_mode() const { return desc_on && coll == 0 && k5_variant == 2 && G.n_free <= 10 && G.n_wave > 0; }
+    // the P2P-sharded iteration with the reduced system's exchange in K5's prologue (4 launches);
+    // RSVIO_P2P_FOLD=0: the separate exchange kernel X1 (5 launches, A/B switch)
+    bool fold_on = true;
+    bool p2p_fold() const { return fold_on && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
     void fill_desc(WinDesc& d) const {
         d = WinDesc{};
@@ -2632,6 +2763,7 @@ struct BundleAdjuster {
         hdesc.G.chol = desc_chol;
         if (!h_desc1.p) h_desc1.alloc(1);
         *h_desc1.p = hdesc;
+        settled = false;
         RSVIO_HIP(hipMemcpyAsync(d_arena.p + lay.desc, h_desc1.p, sizeof(WinDesc), hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_desc, stream));
         desc_pending = true;
@@ -2725,6 +2857,7 @@ struct BundleAdjuster {
             sl.chunk = G.n_chunk;
             sl.dptr = dm ? static_cast<const void*>(dptr()) : nullptr;
         }
+        settled = false;  // (drop_slot above may have found the stream idle)
         RSVIO_HIP(hipGraphLaunch(sl.exec, stream));
         if (graph_update) RSVIO_HIP(hipEventRecord(sl.ev_launch, stream));
         return true;
@@ -2789,6 +2922,8 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreateWithFlags(&gv.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
+        const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0": X1 as its own launch
+        fold_on = !(fv && fv[0] == '0');
         const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
         desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
@@ -3020,6 +3155,7 @@ struct BundleAdjuster {
         if (d_arena.n < L.upload) {  // (grown for the whole arena below once its size is known)
             d_arena.alloc(2 * L.upload);
         }
+        settled = false;  // (the upload, grow_buffers' memset and ba_build_layout go on the stream)
         RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice, stream));
         mark();
         // waves: whole landmarks, <= 64 slots each (greedy, in landmark order); the Schur pair
@@ -3123,6 +3259,7 @@ struct BundleAdjuster {
     }
 
     void enqueue_reset(double lambda0) {
+        settled = false;
         const int n = std::max(std::max(7 * G.n_kf, 3 * G.n_lm), 1);
         hipLaunchKernelGGL(ba_reset, dim3((n + 255) / 256), dim3(256), 0, stream, G, work_at(0), lambda0);
         RSVIO_HIP(hipGetLastError());
@@ -3130,6 +3267,7 @@ struct BundleAdjuster {
 
     // K0 + K4: initial state and its linearisation (buffer 0); the LM state in copy 0
     void enqueue_start(double lambda0) {
+        settled = false;
         if (G.n_wave)  // K0 folded into K4
             hipLaunchKernelGGL(ba_linearize, dim3(G.n_wave), dim3(64), 0, stream, G, prob(), work_at(0), lambda0);
         else
@@ -3199,8 +3337,24 @@ struct BundleAdjuster {
     void enqueue_iteration(const rsvio_lm_cfg& cfg, int it) {
         const Prob pr = prob();
         const Work wk = work(it);
-        enqueue_linear_system(it, lm_args(cfg), false);
-        launch_camera_solve(pr, wk, sharded() ? 0 : 1);
+        if (p2p_fold()) {  // sharded over P2P, 4 launches: K4c, K5 with X1 folded in, K6, X2
+            hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
+                               lm_args(cfg), 1);
+            RSVIO_HIP(hipGetLastError());
+            switch (G.n_free) {
+#define RSVIO_CAMP(NF) \
+    case NF: hipLaunchKernelGGL(ba_camera_solve_mfma_p2p<NF>, dim3(1), dim3(kK5Threads), 0, stream, G, pr, wk, p2p, \
+                                d_xgen.p, d_p2p_err.p); break;
+                RSVIO_CAMP(1) RSVIO_CAMP(2) RSVIO_CAMP(3) RSVIO_CAMP(4) RSVIO_CAMP(5)
+                RSVIO_CAMP(6) RSVIO_CAMP(7) RSVIO_CAMP(8) RSVIO_CAMP(9) RSVIO_CAMP(10)
+#undef RSVIO_CAMP
+                default: throw std::logic_error("p2p_fold: more than 10 free keyframes");
+            }
+            RSVIO_HIP(hipGetLastError());
+        } else {
+            enqueue_linear_system(it, lm_args(cfg), false);
+            launch_camera_solve(pr, wk, sharded() ? 0 : 1);
+        }
         if (G.n_wave) hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
         RSVIO_HIP(hipGetLastError());
         if (coll == 2) {  // P2P: trial scalars + exchange in one launch (X2)
@@ -3263,6 +3417,7 @@ struct BundleAdjuster {
     } pend;
 
     void enqueue_chunk(int k) {
+        settled = false;
         for (int i = 0; i < k; ++i) enqueue_iteration(pend.cfg, pend.enq + i);
         pend.enq += k;
         enqueue_decide(pend.cfg, pend.enq);  // K7 also writes the state into h_state
@@ -3598,6 +3753,7 @@ struct BundleBatch {
     HostBuf<LmState> h_states;
     DevBuf<int> d_dmap;
     HostBuf<int> h_dmap;
+    std::vector<hipEvent_t> ev_win;  // per window: its stream's pending work (an upload) before the batch
     int last_iterations = 3;
 
     void init(BundleAdjuster* const* w, int n) {
@@ -3606,6 +3762,8 @@ struct BundleBatch {
             if (!w[i]) throw std::invalid_argument("null window handle");
             if (i && w[i]->P.device != w[0]->P.device) throw std::invalid_argument("windows on different devices");
             if (w[i]->sharded()) throw std::invalid_argument("a sharded window cannot join a batch");
+            for (int j = 0; j < i; ++j)  // two grid rows on one set of state buffers would race
+                if (w[j] == w[i]) throw std::invalid_argument("a window handle appears twice in the batch");
             win.push_back(w[i]);
         }
         device = w[0]->P.device;
@@ -3613,6 +3771,8 @@ struct BundleBatch {
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
+        ev_win.assign(n, nullptr);
+        for (int i = 0; i < n; ++i) RSVIO_HIP(hipEventCreateWithFlags(&ev_win[i], hipEventDisableTiming));
         d_desc.alloc(n);
         h_desc.alloc(n);
         h_states.alloc(n, hipHostMallocCoherent);
@@ -3621,6 +3781,8 @@ struct BundleBatch {
         if (stream) (void)hipStreamSynchronize(stream);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        for (hipEvent_t e : ev_win)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -3644,7 +3806,7 @@ struct BundleBatch {
         size_t ne_total = 0;
         for (int i = 0; i < B; ++i) {
             BundleAdjuster& w = *win[i];
-            w.require_idle("rsvio_ba_batch_run");
+            if (w.pend.active) throw CallOrderError("rsvio_ba_batch_run: a solve is in flight (call rsvio_ba_wait first)");
             w.state_export = false;  // the batch's decisions leave the state in device memory
             if (!w.has_problem) throw std::invalid_argument("batch window without a problem");
             const Geometry& G = w.G;
@@ -3690,6 +3852,15 @@ struct BundleBatch {
             }
         }
         if (!active) return;
+        // the batch's kernels read what each window's stream may still be writing (set_problem's
+        // upload and ba_build_layout are asynchronous): the batch stream waits on an event of each
+        // window's stream instead of synchronising the host
+        for (int i = 0; i < B; ++i) {
+            BundleAdjuster& w = *win[i];
+            if (w.settled) continue;
+            RSVIO_HIP(hipEventRecord(ev_win[i], w.stream));
+            RSVIO_HIP(hipStreamWaitEvent(stream, ev_win[i], 0));
+        }
         RSVIO_HIP(hipMemcpyAsync(d_dmap.p, h_dmap.p, sizeof(int) * std::max<size_t>(off, 1), hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipMemcpyAsync(d_desc.p, h_desc.p, sizeof(WinDesc) * B, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev0, stream));
@@ -3731,7 +3902,10 @@ struct BundleBatch {
             const LmState& st = h_states.p[i];
             *w.h_state.p = st;
             w.state_fresh = false;
+            // the window's stream ran nothing after the event the batch waited on, and the batch
+            // stream is synchronised: both are idle
             w.settled = true;
+            w.destroy_retired();
             w.last_iterations = st.iter;
             res[i].status = st.status;
             res[i].iterations = st.iter;

@@ -96,13 +96,15 @@ int guarded(F&& f) {
 #define RSVIO_DBG_READER(name)
 #endif
 
-// The tracker's device-resident output of the last frame (tracker.hip), for consumers on the
-// device (pnp.hip): features (AoS rsvio_feature), fused undistorted coordinates, counts.
+// The tracker's device-resident output of the last COLLECTED frame (tracker.hip), for consumers
+// on the device (pnp.hip): features (AoS rsvio_feature), fused undistorted coordinates, lengths.
+// Complete when the view is taken (the collect waited for it); a frame submitted since writes the
+// other output slot.
 struct TrackerView {
     hipStream_t stream;
     const rsvio_feature* out[2];
     const float2* undist[2];   // null unless cameras are attached
-    const int* counts;         // device (n_l, n_r)
+    int n[2];                  // list lengths (n_l, n_r)
     int device;
 };
 TrackerView tracker_view(rsvio_tracker* t);

@@ -777,15 +777,24 @@ int rsvio_track_motion_tracker(rsvio_pnp* h, rsvio_tracker* t, const double* T_W
             return (int)RSVIO_ERR_INVALID_ARG;
         }
         RSVIO_HIP(hipSetDevice(P.device));
-        // the map upload (set_map) is ordered before this launch: it synchronised its stream
+        if (v.n[0] + v.n[1] > rsvio::kPnpMaxFeatures) {
+            rsvio::set_last_error("track_motion: more than 4096 features in one frame");
+            return (int)RSVIO_ERR_CAPACITY;
+        }
+        // the map upload (set_map) is ordered before this launch: it synchronised its stream.  The
+        // view is the last collected frame's output slot, complete on the device (its collect
+        // waited for it), so the launch goes on the handle's own stream: it runs beside a next
+        // frame already submitted to the tracker's stream, which writes the other slot
         rsvio::PnpArgs A = rsvio::make_args(P, T_W_B_last_kf, T_C_B2, cfg, rule);
         A.ids[0] = reinterpret_cast<const uint8_t*>(v.out[0]);
         A.ids[1] = reinterpret_cast<const uint8_t*>(v.out[1]);
         A.id_stride = (int)sizeof(rsvio_feature);
         A.uv[0] = v.undist[0];
         A.uv[1] = v.undist[1];
-        A.dcount = v.counts;
-        return rsvio::run_pnp(P, A, v.stream, res);
+        A.dcount = nullptr;
+        A.n[0] = v.n[0];
+        A.n[1] = v.n[1];
+        return rsvio::run_pnp(P, A, P.active(), res);
     });
 }
 

@@ -155,11 +155,15 @@ __device__ __forceinline__ double rcp_f64(double d) {
 }
 
 // The correctly rounded f32 quotient a / b as RN_f32(a * (1/b)) in f64, 1/b = rcp_f64 (~2^-52
-// relative): the f64 product is within 2^-51 of a / b, and the quotient of two f32 values is never
-// a rounding midpoint nor within 2^-49 (relative) of one (|A 2^k - M B| >= 1 for the 24-bit
-// significands A, B and a 25-bit midpoint M), so rounding the product to f32 gives exactly a / b
-// (tests/test_div_rcp_cpu.py) -- with the reciprocal off the chain when b is known before a (the
-// trackers: theta before its sine, a patch sum before the samples' products).
+// relative): the f64 product is within 2^-51 of a / b, and a NORMAL f32 quotient of two f32 values
+// is never a rounding midpoint nor within 2^-49 (relative) of one (|A 2^k - M B| >= 1 for the
+// 24-bit significands A, B and a 25-bit midpoint M), so rounding the product to f32 gives exactly
+// a / b (tests/test_div_rcp_cpu.py) -- with the reciprocal off the chain when b is known before a
+// (the trackers: theta before its sine, a patch sum before the samples' products).
+// Domain: |a / b| >= FLT_MIN (or 0).  A subnormal quotient has a shorter midpoint and CAN be an
+// exact tie (e.g. (9 * 2^-149) / 6 = 1.5 * 2^-149), which RN(a * rcp(b)) may round the wrong way;
+// the trackers' quotients (sin(theta) / theta, (1 - cos theta) / theta, nv v / sum over a patch of
+// 8-bit intensities) never come near that range, so no guard sits on their chains.
 __device__ __forceinline__ float div_rcp(float a, double rb) { return (float)((double)a * rb); }
 
 // 1/sqrt(d), f64: hardware estimate + two Newton steps (y <- y (3 - d y^2) / 2)

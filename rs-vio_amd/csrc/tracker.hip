@@ -284,14 +284,24 @@ struct Tracker {
     DevBuf<int> counts, bins, overflow;
     DevBuf<int4> cell_pt;
     DevBuf<unsigned long long> last_id;
+    // packed output lists, TWO frame slots (2 x 2 cams x cap): frame t writes slot t & 1, so a
+    // consumer of the last collected frame (track_motion_tracker, remove_ids, undistorted) reads
+    // a slot that the next frame -- submitted before that consumer runs, in the Estimator's
+    // one-frame look-ahead -- does not write
     DevBuf<rsvio_feature> out;
     HostBuf<int> h_counts;
     CamPair cams{};                 // T12 unprojection fused into append_pack_kernel when on
-    DevBuf<float2> undist;          // 2 x cap
+    DevBuf<float2> undist;          // 2 slots x 2 x cap
     DevBuf<float2> tmp_und;         // cap (remove_ids compaction scratch)
     HostBuf<float2> h_undist;       // last process_frame's undistorted coordinates
     HostBuf<rsvio_feature> h_out;   // pinned staging of both packed feature lists (2 x cap)
     size_t last_n[2] = {0, 0};
+    int wslot = 0;                  // the output slot the next submitted frame writes
+    int rslot = 0;                  // the output slot of the last collected frame
+    int coll_n[2] = {0, 0};         // its device list lengths (<= cap)
+    bool inflight = false;          // a frame was submitted and not yet collected
+    size_t bnd[2] = {0, 0};         // the list bounds the submit's copies covered
+    hipEvent_t ev_done = nullptr;   // after the submitted frame's read-back copies
 
     uint8_t* pyr(int slot, int cam) { return d_pyr.p + (size_t)(2 * slot + cam) * pyr_bytes; }
 
@@ -324,8 +334,9 @@ struct Tracker {
         overflow.alloc(1);
         cell_pt.alloc(n_cells);
         last_id.alloc(1);
-        out.alloc((size_t)2 * cap);
+        out.alloc((size_t)4 * cap);
         h_counts.alloc(4);
+        RSVIO_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
         h_out.alloc((size_t)2 * cap);
         RSVIO_HIP(hipMemsetAsync(counts.p, 0, sizeof(int) * 2, stream));
         RSVIO_HIP(hipMemsetAsync(last_id.p, 0, sizeof(unsigned long long), stream));
@@ -333,12 +344,16 @@ struct Tracker {
         RSVIO_HIP(hipStreamSynchronize(stream));
     }
     ~Tracker() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
     float* maff(int c) { return map_aff.p + (size_t)c * cap * 6; }
     float* taff(int c) { return tmp_aff.p + (size_t)c * cap * 6; }
     uint64_t* mid(int c) { return ids.p + (size_t)c * cap; }
+    rsvio_feature* outp(int slot, int c) { return out.p + (size_t)(2 * slot + c) * cap; }
+    float2* undp(int slot, int c) { return cams.on ? undist.p + (size_t)(2 * slot + c) * cap : nullptr; }
 
     // Enqueue one frame; images already in device memory.
     void enqueue_frame(const uint8_t* d_left, const uint8_t* d_right) {
@@ -373,8 +388,8 @@ struct Tracker {
         hipLaunchKernelGGL(append_pack_kernel, dim3(1), dim3(1024), 0, stream, G, bins.p, host_count[0],
                            host_count[1], has_prev ? 1 : 0, taff(0), taff(1), valid.p, valid.p + cap, ids_tmp.p,
                            cell_pt.p, n_cells, new_aff.p, new_aff1.p, new_valid.p, maff(0), maff(1), mid(0), mid(1),
-                           counts.p, last_id.p, cap, out.p, out.p + cap, overflow.p, cams, undist.p,
-                           undist.p + (cams.on ? cap : 0));
+                           counts.p, last_id.p, cap, outp(wslot, 0), outp(wslot, 1), overflow.p, cams,
+                           undp(wslot, 0), undp(wslot, 1));
         RSVIO_HIP(hipGetLastError());
         cur = nxt;
         has_prev = true;
@@ -384,31 +399,52 @@ struct Tracker {
     // the lists are copied up to a host-known bound into pinned staging -- a camera's list is its
     // previous survivors plus at most one new point per grid cell (feature_tracker.rs:143-170) --
     // and a second copy covers any excess (never expected).
-    void copy_lists(size_t l0, size_t l1, size_t r0, size_t r1) {
-        if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_out.p + l0, out.p + l0, (l1 - l0) * sizeof(rsvio_feature),
+    void copy_lists(int slot, size_t l0, size_t l1, size_t r0, size_t r1) {
+        if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_out.p + l0, outp(slot, 0) + l0, (l1 - l0) * sizeof(rsvio_feature),
                                               hipMemcpyDeviceToHost, stream));
-        if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_out.p + cap + r0, out.p + cap + r0, (r1 - r0) * sizeof(rsvio_feature),
+        if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_out.p + cap + r0, outp(slot, 1) + r0, (r1 - r0) * sizeof(rsvio_feature),
                                               hipMemcpyDeviceToHost, stream));
         if (cams.on) {
-            if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + l0, undist.p + l0, (l1 - l0) * sizeof(float2),
+            if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + l0, undp(slot, 0) + l0, (l1 - l0) * sizeof(float2),
                                                   hipMemcpyDeviceToHost, stream));
-            if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap + r0, undist.p + cap + r0,
+            if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap + r0, undp(slot, 1) + r0,
                                                   (r1 - r0) * sizeof(float2), hipMemcpyDeviceToHost, stream));
         }
     }
 
-    int fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
-        const size_t bl = std::min((size_t)cap, (size_t)host_count[0] + (size_t)n_cells);
-        const size_t br = std::min((size_t)cap, (size_t)host_count[1] + (size_t)n_cells);
+    // submit: the frame's kernels, then the read-back of counts, overflow flag and both lists
+    // (+ undistorted coordinates) up to a host-known bound, all on the stream; returns at once.
+    void submit(const uint8_t* d_left, const uint8_t* d_right) {
+        enqueue_frame(d_left, d_right);
+        bnd[0] = std::min((size_t)cap, (size_t)host_count[0] + (size_t)n_cells);
+        bnd[1] = std::min((size_t)cap, (size_t)host_count[1] + (size_t)n_cells);
         RSVIO_HIP(hipMemcpyAsync(h_counts.p, counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipMemcpyAsync(h_counts.p + 2, overflow.p, sizeof(int), hipMemcpyDeviceToHost, stream));
-        copy_lists(0, bl, 0, br);
-        RSVIO_HIP(hipStreamSynchronize(stream));
+        copy_lists(wslot, 0, bnd[0], 0, bnd[1]);
+        RSVIO_HIP(hipEventRecord(ev_done, stream));
+        inflight = true;
+    }
+
+    void require_collected(const char* what) {
+        if (inflight) throw CallOrderError(std::string(what) + ": a frame is in flight (collect it first)");
+    }
+
+    // collect: wait for the submitted frame's read-back, then the host lists
+    int fetch(rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r, size_t cap_r, size_t* n_r) {
+        if (!inflight) throw CallOrderError("no frame in flight (submit one first)");
+        inflight = false;
+        const int slot = wslot;
+        wslot ^= 1;
+        rslot = slot;
+        RSVIO_HIP(hipEventSynchronize(ev_done));
+        const size_t bl = bnd[0], br = bnd[1];
         host_count[0] = h_counts.p[0];
         host_count[1] = h_counts.p[1];
         const size_t ml = std::min((size_t)host_count[0], (size_t)cap), mr = std::min((size_t)host_count[1], (size_t)cap);
+        coll_n[0] = (int)ml;
+        coll_n[1] = (int)mr;
         if (ml > bl || mr > br) {
-            copy_lists(bl, std::max(ml, bl), br, std::max(mr, br));
+            copy_lists(slot, bl, std::max(ml, bl), br, std::max(mr, br));
             RSVIO_HIP(hipStreamSynchronize(stream));
         }
         const size_t nl = std::min(ml, cap_l), nr = std::min(mr, cap_r);
@@ -450,11 +486,13 @@ TrackerView tracker_view(rsvio_tracker* h) {
     Tracker& T = h->t;
     TrackerView v{};
     v.stream = T.stream;
-    v.out[0] = T.out.p;
-    v.out[1] = T.out.p + T.cap;
-    v.undist[0] = T.cams.on ? T.undist.p : nullptr;
-    v.undist[1] = T.cams.on ? T.undist.p + T.cap : nullptr;
-    v.counts = T.counts.p;
+    // the last COLLECTED frame's slot and lengths: a frame submitted since writes the other slot
+    v.out[0] = T.outp(T.rslot, 0);
+    v.out[1] = T.outp(T.rslot, 1);
+    v.undist[0] = T.undp(T.rslot, 0);
+    v.undist[1] = T.undp(T.rslot, 1);
+    v.n[0] = T.coll_n[0];
+    v.n[1] = T.coll_n[1];
     v.device = T.P.device;
     return v;
 }
@@ -535,9 +573,10 @@ int rsvio_tracker_process_frame(rsvio_tracker* t, const uint8_t* left, const uin
         const size_t w = (size_t)T.P.width, h = (size_t)T.P.height;
         if (stride == 0) stride = w;
         if (stride < w) throw std::invalid_argument("stride < width");
+        T.require_collected("rsvio_tracker_process_frame");
         RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p, w, left, stride, w, h, hipMemcpyHostToDevice, T.stream));
         RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p + w * h, w, right, stride, w, h, hipMemcpyHostToDevice, T.stream));
-        T.enqueue_frame(T.d_img.p, T.d_img.p + w * h);
+        T.submit(T.d_img.p, T.d_img.p + w * h);
         return T.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
     });
 }
@@ -547,9 +586,40 @@ int rsvio_tracker_process_frame_device(rsvio_tracker* t, const uint8_t* d_left, 
                                        size_t cap_r, size_t* n_r) {
     if (!t || !d_left || !d_right || !n_l || !n_r) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
-        t->t.enqueue_frame(d_left, d_right);
+        t->t.require_collected("rsvio_tracker_process_frame_device");
+        t->t.submit(d_left, d_right);
         return t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r);
     });
+}
+
+int rsvio_tracker_submit_device(rsvio_tracker* t, const uint8_t* d_left, const uint8_t* d_right) {
+    if (!t || !d_left || !d_right) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        t->t.require_collected("rsvio_tracker_submit_device");
+        t->t.submit(d_left, d_right);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_submit(rsvio_tracker* t, const uint8_t* left, const uint8_t* right, size_t stride) {
+    if (!t || !left || !right) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        auto& T = t->t;
+        const size_t w = (size_t)T.P.width, h = (size_t)T.P.height;
+        if (stride == 0) stride = w;
+        if (stride < w) throw std::invalid_argument("stride < width");
+        T.require_collected("rsvio_tracker_submit");
+        RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p, w, left, stride, w, h, hipMemcpyHostToDevice, T.stream));
+        RSVIO_HIP(hipMemcpy2DAsync(T.d_img.p + w * h, w, right, stride, w, h, hipMemcpyHostToDevice, T.stream));
+        T.submit(T.d_img.p, T.d_img.p + w * h);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_tracker_collect(rsvio_tracker* t, rsvio_feature* out_l, size_t cap_l, size_t* n_l, rsvio_feature* out_r,
+                          size_t cap_r, size_t* n_r) {
+    if (!t || !n_l || !n_r || (cap_l && !out_l) || (cap_r && !out_r)) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] { return t->t.fetch(out_l, cap_l, n_l, out_r, cap_r, n_r); });
 }
 
 int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const rsvio_camera* right) {
@@ -560,6 +630,7 @@ int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const 
     }
     return guarded([&] {
         auto& T = t->t;
+        T.require_collected("rsvio_tracker_set_cameras");
         RSVIO_HIP(hipStreamSynchronize(T.stream));
         if (!left) {
             T.cams.on = 0;
@@ -567,7 +638,7 @@ int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const 
             return (int)RSVIO_OK;
         }
         if (!T.undist.p) {
-            T.undist.alloc((size_t)2 * T.cap);
+            T.undist.alloc((size_t)4 * T.cap);
             T.h_undist.alloc((size_t)2 * T.cap);
             T.tmp_und.alloc((size_t)T.cap);
         }
@@ -596,22 +667,24 @@ int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n) {
     if (n == 0) return RSVIO_OK;
     return guarded([&] {
         auto& T = t->t;
+        T.require_collected("rsvio_tracker_remove_ids");
         if (T.rm_ids.n < n) T.rm_ids.alloc(n);
         RSVIO_HIP(hipMemcpyAsync(T.rm_ids.p, ids, n * sizeof(uint64_t), hipMemcpyHostToDevice, T.stream));
         hipLaunchKernelGGL(rsvio::remove_ids_kernel, dim3(1), dim3(1024), 0, T.stream, T.rm_ids.p, (int)n, T.maff(0),
-                           T.maff(1), T.mid(0), T.mid(1), T.tmp_aff.p, T.ids_tmp.p, T.counts.p, T.out.p,
-                           T.out.p + T.cap, T.cams.on ? T.undist.p : nullptr,
-                           T.cams.on ? T.undist.p + T.cap : nullptr, T.tmp_und.p);
+                           T.maff(1), T.mid(0), T.mid(1), T.tmp_aff.p, T.ids_tmp.p, T.counts.p, T.outp(T.rslot, 0),
+                           T.outp(T.rslot, 1), T.undp(T.rslot, 0), T.undp(T.rslot, 1), T.tmp_und.p);
         RSVIO_HIP(hipGetLastError());
         RSVIO_HIP(hipMemcpyAsync(T.h_counts.p, T.counts.p, sizeof(int) * 2, hipMemcpyDeviceToHost, T.stream));
         RSVIO_HIP(hipStreamSynchronize(T.stream));
         T.host_count[0] = T.h_counts.p[0];
         T.host_count[1] = T.h_counts.p[1];
+        T.coll_n[0] = std::min(T.host_count[0], T.cap);
+        T.coll_n[1] = std::min(T.host_count[1], T.cap);
         if (T.cams.on) {  // undistorted() stays aligned with the compacted feature lists
             const size_t nl = std::min(T.last_n[0], (size_t)T.host_count[0]);
             const size_t nr = std::min(T.last_n[1], (size_t)T.host_count[1]);
-            if (nl) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p, T.undist.p, nl * sizeof(float2), hipMemcpyDeviceToHost, T.stream));
-            if (nr) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p + T.cap, T.undist.p + T.cap, nr * sizeof(float2),
+            if (nl) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p, T.undp(T.rslot, 0), nl * sizeof(float2), hipMemcpyDeviceToHost, T.stream));
+            if (nr) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p + T.cap, T.undp(T.rslot, 1), nr * sizeof(float2),
                                              hipMemcpyDeviceToHost, T.stream));
             RSVIO_HIP(hipStreamSynchronize(T.stream));
             T.last_n[0] = nl;

@@ -99,6 +99,10 @@ SIG = {
                                               C.c_size_t, C.POINTER(C.c_size_t)]),
     "rsvio_tracker_process_frame_device": (C.c_int, [P, P, P, P, C.c_size_t, C.POINTER(C.c_size_t), P,
                                                      C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rsvio_tracker_submit": (C.c_int, [P, P, P, C.c_size_t]),
+    "rsvio_tracker_submit_device": (C.c_int, [P, P, P]),
+    "rsvio_tracker_collect": (C.c_int, [P, P, C.c_size_t, C.POINTER(C.c_size_t), P, C.c_size_t,
+                                        C.POINTER(C.c_size_t)]),
     "rsvio_tracker_remove_ids": (C.c_int, [P, P, C.c_size_t]),
     "rsvio_tracker_stream": (P, [P]),
     "rsvio_sincosf": (C.c_int, [P, C.c_size_t, P, P]),

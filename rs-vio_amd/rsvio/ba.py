@@ -118,13 +118,21 @@ class BundleAdjuster:
 
     def set_problem_from(self, prob):
         """set_problem with the fields of a problem object.  Its marshalled arguments are kept on
-        the object for as long as its fields are the same array objects (in-place edits are seen,
-        the pointers stay valid): a Rust caller hands its slices over as they are, while ctypes
-        pointer extraction costs ~2 us per array, a fifth of the C call."""
+        the object for as long as its fields are the same array objects AND marshalling used them
+        as they are (the C types, contiguous): in-place edits are then seen and the pointers stay
+        valid -- a Rust caller hands its slices over as they are, while ctypes pointer extraction
+        costs ~2 us per array, a fifth of the C call.  A field that had to be converted (another
+        dtype, non-contiguous) is a copy, so such a problem is re-marshalled on every call."""
         src = tuple(getattr(prob, f) for f in self._FIELDS)
         m = prob.__dict__.get("_rsvio_marshal")
         if m is None or any(a is not b for a, b in zip(m[0], src)):
-            m = (src, self._marshal(*src))
+            keep, args = self._marshal(*src)
+            # a reshape of the source is a view: in-place edits of the source reach it
+            if not all(k is s or (k.base is not None and (k.base is s or k.base is getattr(s, "base", None)))
+                       for k, s in zip(keep, src)):
+                self._set(keep, args)
+                return
+            m = (src, (keep, args))
             object.__setattr__(prob, "_rsvio_marshal", m)
         self._set(*m[1])
 

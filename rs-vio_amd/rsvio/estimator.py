@@ -13,6 +13,11 @@ Per frame (estimator.rs:190-248):
 The host logic is the reference's, in canonical order (ids in detection scan
 order, features by id).  The heavy work is device work behind the C ABI; `Backend` is the seam
 the parity tests use to run the same host logic over the CPU restatement.
+
+Estimator.run(frames) runs the tracker ONE FRAME AHEAD: step 1 of frame t + 1 only needs its two
+images (estimator.rs:190 hands the tracker nothing from the window), so it is submitted to the
+device as soon as frame t's features are back, and frame t's steps 2-3 (host logic, PnP, the BA
+upload and start) run while frame t + 1 tracks.  Results equal process_frame's frame by frame.
 """
 from __future__ import annotations
 
@@ -32,6 +37,9 @@ class FrameResult:
     n_right: int
     pnp_status: int | None       # None: window not full yet (no motion tracking)
     ba_status: int | None        # None: no optimisation this frame
+    pnp_iterations: int | None = None   # LM iterations of the motion tracking
+    pnp_cost: float | None = None       # its final cost
+    ba_iterations: int | None = None    # LM iterations of the window's solve (the retry's, after a fallback)
 
 
 class DeviceBackend:
@@ -48,22 +56,31 @@ class DeviceBackend:
         self.motion = MotionTracker(device, translation_threshold, rotation_threshold)
         self.solver = BundleAdjuster(max_keyframes=max(window, 2), device=device)
 
-    def track(self, left, right):
-        """Host u8 arrays, or device-resident u8 tensors (data_ptr; no H2D copy)."""
+    def submit(self, left, right):
+        """Enqueue a frame's tracking: host u8 arrays, or device-resident u8 tensors (data_ptr; no
+        H2D copy)."""
         if hasattr(left, "data_ptr"):
-            nl, nr = self.tracker.process_frame_device(left.data_ptr(), right.data_ptr())
-            fl, fr = self.tracker._out_l[:nl], self.tracker._out_r[:nr]
+            self.tracker.submit_device(left.data_ptr(), right.data_ptr())
         else:
-            fl, fr = self.tracker.process_frame(left, right)
+            self.tracker.submit(left, right)
+
+    def collect(self):
+        """The submitted frame's features: ((ids, undistorted uv) left, (ids, uv) right)."""
+        nl, nr = self.tracker.collect_device()
+        fl, fr = self.tracker._out_l[:nl], self.tracker._out_r[:nr]
         ul, ur = self.tracker.undistorted()
         return (fl["id"].astype(np.int64), ul), (fr["id"].astype(np.int64), ur)
+
+    def track(self, left, right):
+        self.submit(left, right)
+        return self.collect()
 
     def set_map(self, ids, p_W):
         self.motion.set_map(np.asarray(ids, np.uint64), np.asarray(p_W, np.float32))
 
     def track_motion(self, T_W_B_last_kf, T_C_B2):
         r = self.motion.track_motion_tracker(self.tracker, T_W_B_last_kf, T_C_B2)
-        return r.status, r.is_keyframe, r.T_W_B
+        return r.status, r.is_keyframe, r.T_W_B, r.iterations, r.final_cost
 
     def close(self):
         for o in (self.tracker, self.motion, self.solver):
@@ -101,6 +118,7 @@ class Estimator:
             r = self.window.last_result
             out, frame = self._pending_frame
             out.ba_status = None if r is None else int(r.status)
+            out.ba_iterations = None if r is None else int(r.iterations)
             out.T_W_B = frame.T_W_B.copy()  # the solve refined this keyframe's pose too
             self._pending_frame = None
 
@@ -114,22 +132,52 @@ class Estimator:
         return self._tcb
 
     def process_frame(self, left: np.ndarray, right: np.ndarray) -> FrameResult:
+        return self._process_tracked(self.backend.track(left, right))
+
+    def run(self, frames):
+        """process_frame over an iterable of (left, right) image pairs, yielding one FrameResult
+        per frame, with the tracker one frame ahead (module docstring): frame t + 1 is submitted
+        right after frame t's features are collected, before frame t's motion tracking and BA.
+        In pipelined mode a keyframe's FrameResult gets its BA outcome when the solve is next
+        waited for (at the latest by flush()); frames left unconsumed are collected on exit."""
+        it = iter(frames)
+        nxt = next(it, None)
+        if nxt is None:
+            return
+        self.backend.submit(*nxt)
+        in_flight = True
+        try:
+            while in_flight:
+                feats = self.backend.collect()
+                in_flight = False
+                nxt = next(it, None)
+                if nxt is not None:
+                    self.backend.submit(*nxt)
+                    in_flight = True
+                yield self._process_tracked(feats)
+        finally:
+            if in_flight:  # the consumer stopped early: the tracker holds no frame in flight after
+                self.backend.collect()
+
+    def _process_tracked(self, feats) -> FrameResult:
+        """Steps 2-3 of process_frame (estimator.rs:195-248) for a frame whose features are in."""
         self.frame_id += 1
-        (ids_l, uv_l), (ids_r, uv_r) = self.backend.track(left, right)
+        (ids_l, uv_l), (ids_r, uv_r) = feats
         frame = Frame(frame_id=self.frame_id, T_W_B=np.eye(4), T_B_Cl=self.T_B_Cl, T_B_Cr=self.T_B_Cr,
                       is_keyframe=True, left_features=(ids_l, uv_l), right_features=(ids_r, uv_r))
-        pnp_status = None
+        pnp_status = pnp_iters = pnp_cost = None
         self.flush()
         if self.window.is_full():
             if self.window.map_version != self._map_key:  # map_points changes only in optimize
                 self.backend.set_map(self.window.map_ids, self.window.map_pw)  # ascending ids, f32
                 self._map_key = self.window.map_version
-            status, is_kf, T_W_B = self.backend.track_motion(self.window.get_keyframe_poses()[-1], self._T_C_B2())
+            status, is_kf, T_W_B, pnp_iters, pnp_cost = self.backend.track_motion(
+                self.window.get_keyframe_poses()[-1], self._T_C_B2())
             pnp_status = status
             if status > 0:
                 frame.T_W_B = T_W_B
                 frame.is_keyframe = bool(is_kf)
-        ba_status = None
+        ba_status = ba_iters = None
         pending = False
         if frame.is_keyframe:
             self.window.add_frame(frame)
@@ -140,8 +188,10 @@ class Estimator:
                     self.window.optimize()
                     r = self.window.last_result
                     ba_status = None if r is None else int(r.status)
+                    ba_iters = None if r is None else int(r.iterations)
         out = FrameResult(self.frame_id, frame.is_keyframe, frame.T_W_B.copy(), len(ids_l), len(ids_r),
-                          pnp_status, ba_status)
+                          pnp_status, ba_status, pnp_iterations=pnp_iters, pnp_cost=pnp_cost,
+                          ba_iterations=ba_iters)
         if pending:
             self._pending_frame = (out, frame)
         return out

@@ -117,6 +117,36 @@ class StereoPatchTracker:
         check(rc)
         return nl.value, nr.value
 
+    def submit(self, left: np.ndarray, right: np.ndarray):
+        """First half of process_frame (rsvio_tracker_submit): enqueue the frame and return at
+        once; the images are borrowed until collect()."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        if left.shape != (self.height, self.width) or right.shape != left.shape:
+            raise ValueError(f"expected {self.height}x{self.width} images")
+        check(_lib.load().rsvio_tracker_submit(self._h, ptr(left), ptr(right), self.width))
+        self._borrowed = (left, right)
+
+    def submit_device(self, d_left: int, d_right: int):
+        """rsvio_tracker_submit_device: device images (tightly packed), enqueued; collect() later."""
+        check(_lib.load().rsvio_tracker_submit_device(self._h, d_left, d_right))
+
+    def collect_device(self):
+        """Second half (rsvio_tracker_collect): wait for the submitted frame; (n_left, n_right),
+        the lists in self._out_l / self._out_r."""
+        nl, nr = C.c_size_t(0), C.c_size_t(0)
+        rc = _lib.load().rsvio_tracker_collect(self._h, ptr(self._out_l), self.cap, C.byref(nl), ptr(self._out_r),
+                                               self.cap, C.byref(nr))
+        self._n = (nl.value, nr.value)
+        self._borrowed = None
+        check(rc)
+        return nl.value, nr.value
+
+    def collect(self):
+        """collect_device() returning (left_features, right_features) like process_frame."""
+        nl, nr = self.collect_device()
+        return self._out_l[:nl].copy(), self._out_r[:nr].copy()
+
     def get_track_points(self):
         """[{id: (x, y)} for cam0, cam1] like feature_tracker.rs:188-200."""
         l, r = self._out_l[:self._n[0]], self._out_r[:self._n[1]]

@@ -505,10 +505,11 @@ def test_async_wrong_call_order_refused(gpu, cfg3):
     a.close()
 
 
-def _p2p_worker(rank, world, port, out_dir, n_lm=2000):
+def _p2p_worker(rank, world, port, out_dir, n_lm=2000, env=None):
     import os
 
     import torch.distributed as dist
+    os.environ.update(env or {})
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -557,9 +558,9 @@ def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
 
 def test_sharded_p2p_weak_scaling_size_matches_oracle(gpu, oracle, tmp_path):
     """The weak-scaling configuration of the bench at N = 2: 2,000 landmarks per rank (4,000 in
-    all, 48,000 observations), the fused P2P path (K4c, combine+exchange, K5, K6,
-    trial+exchange: 5 launches per LM iteration), against the oracle's single 4,000-landmark
-    solve within the config-3 tolerances."""
+    all, 48,000 observations), the fused P2P path (K4c, K5 with the reduced system's exchange in
+    its prologue, K6, trial+exchange: 4 launches per LM iteration), against the oracle's single
+    4,000-landmark solve within the config-3 tolerances."""
     import socket
 
     import torch.multiprocessing as mp
@@ -659,3 +660,83 @@ def test_batched_windows_match_single_and_oracle(gpu, oracle):
     batch.close()
     for w in wins:
         w.close()
+
+
+def test_batch_runs_right_after_a_large_upload(gpu, oracle):
+    """set_problem is asynchronous (H2D of the arena, ba_build_layout and a memset on
+    the window's stream), so the batch stream must be ordered after it.  The largest window
+    (config 5's shape, 20 keyframes would exceed the batched K5; 10 x 5,000 here) is uploaded
+    LAST and the batch started at once, for several rounds of fresh problems: every window must
+    equal the oracle's solve of ITS problem (a batch that read a half-written arena would not)."""
+    from rsvio import synthetic as S
+    from rsvio.ba import BundleAdjuster, BundleBatch
+    shapes = [(4, 80, 3), (6, 200, 4), (10, 5000, 6)]
+    wins = [BundleAdjuster(max_keyframes=21, max_landmarks=5000, max_observations=80000) for _ in shapes]
+    batch = BundleBatch(wins)
+    for rnd in range(3):
+        probs = [S.ba_problem(n_kf=k, n_lm=m, kf_per_lm=p, seed=700 + 10 * rnd + i, init_seed=800 + 10 * rnd + i)
+                 for i, (k, m, p) in enumerate(shapes)]
+        for w, pr in zip(wins, probs):   # the large window goes up last
+            w.set_problem_from(pr)
+        res = batch.run()
+        for i, (w, pr, r) in enumerate(zip(wins, probs, res)):
+            pose, pw = w.state()
+            po, pwo, ro = oracle.ba_solve(pr)
+            assert (r.status, r.iterations) == (ro.status, ro.iterations), (rnd, i)
+            assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6, (rnd, i)
+    batch.close()
+    for w in wins:
+        w.close()
+
+
+def test_batch_refuses_a_handle_twice(gpu, cfg3):
+    """two grid rows on one handle's state buffers would race -- refused."""
+    from rsvio import RsvioError
+    from rsvio.ba import BundleBatch
+    a = _adjuster(gpu, cfg3)
+    with pytest.raises(RsvioError) as e:
+        BundleBatch([a, a])
+    assert e.value.code == -1
+    a.close()
+
+
+def _run_p2p(world, n_lm, tmp_path, env=None):
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_p2p_worker, args=(world, port, str(tmp_path), n_lm, env), nprocs=world, join=True,
+                       start_method="spawn")
+    return [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+
+
+def test_sharded_p2p_four_ranks_match_oracle(gpu, oracle, tmp_path):
+    """Four ranks (four processes on one GPU, IPC-mapped exchange buffers): the 4-rank slot layout,
+    generation parity and rank-ordered sums N = 8 uses.  2,000 landmarks per rank = the oracle's
+    single 8,000-landmark, 96,000-observation solve; every rank ends with bitwise the same poses and
+    LM outcome, and the gathered solution matches the oracle within the config-3 tolerances."""
+    from rsvio import synthetic as S
+    rs = _run_p2p(4, 8000, tmp_path)
+    for r in rs[1:]:
+        assert np.array_equal(rs[0]["pose"], r["pose"]) and np.array_equal(rs[0]["res"], r["res"])
+    full = S.ba_problem(n_lm=8000)
+    po, pwo, ro = oracle.ba_solve(full)
+    assert int(rs[0]["res"][0]) == ro.status and int(rs[0]["res"][1]) == ro.iterations
+    assert abs(rs[0]["res"][2] - ro.final_cost) <= 1e-8 * ro.initial_cost
+    assert np.abs(rs[0]["pose"] - po).max() < 1e-7
+    assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
+
+
+def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path):
+    """The 4-launch iteration (X1's exchange folded into K5's prologue) against the 5-launch one
+    (RSVIO_P2P_FOLD=0: X1 as its own kernel, K5 reading the exchanged system): the same sums in the
+    same order, so the 2-rank solves are bit-identical."""
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    fold = _run_p2p(2, 4000, tmp_path / "a")
+    sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": "0"})
+    for a, b in zip(fold, sep):
+        for k in ("pose", "pw", "res"):
+            assert np.array_equal(a[k], b[k]), k

@@ -169,10 +169,74 @@ def test_estimator_pipelined_equals_sequential(oracle, scene_stream):
     pip.flush()
     assert deferred > 0
     for x, y in zip(a, b):
-        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right) == \
-               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right)
+        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right, x.pnp_iterations, x.ba_iterations) == \
+               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right, y.pnp_iterations, y.ba_iterations)
         assert np.array_equal(x.T_W_B, y.T_W_B)
     for Ta, Tb in zip(seq.trajectory(), pip.trajectory()):
         assert np.array_equal(Ta, Tb)
     ma, mb = seq.window.map_points, pip.window.map_points
     assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
+
+
+class _OrderSpy:
+    """Records the order of the backend calls the Estimator makes."""
+
+    def __init__(self, be):
+        self.be, self.solver, self.log = be, be.solver, []
+
+    def submit(self, l, r):
+        self.log.append("submit")
+        return self.be.submit(l, r)
+
+    def collect(self):
+        self.log.append("collect")
+        return self.be.collect()
+
+    def track_motion(self, *a):
+        self.log.append("pnp")
+        return self.be.track_motion(*a)
+
+    def __getattr__(self, k):
+        return getattr(self.be, k)
+
+
+def test_estimator_lookahead_equals_sequential(oracle, scene_stream):
+    """Estimator.run: the tracker one frame ahead (frame t + 1 submitted right after frame t's
+    features are collected, before frame t's PnP and BA), pipelined BA on top: every frame result
+    -- statuses and LM iteration counts included -- the trajectory and the map equal the
+    sequential process_frame order's exactly, and the call order is the look-ahead's."""
+    from oracle.estimator import OracleBackend
+    from rsvio.camera import Camera
+    from rsvio.estimator import Estimator
+    s, win = scene_stream
+    cams = [Camera.opencv5(*p) for p in s.intrinsics]
+    h, w = s.frames[0][0].shape
+    seq = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=OracleBackend(oracle, w, h, cams))
+    a = [seq.process_frame(l, r) for l, r in s.frames]
+    be = OracleBackend(oracle, w, h, cams)
+    be.solver = _DeferredSolver(be.solver)
+    spy = _OrderSpy(be)
+    la = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=spy, pipelined=True)
+    b = list(la.run(s.frames))
+    la.flush()
+    assert len(b) == len(a)
+    for x, y in zip(a, b):
+        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right, x.pnp_iterations, x.ba_iterations) == \
+               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right, y.pnp_iterations, y.ba_iterations)
+        assert np.array_equal(x.T_W_B, y.T_W_B)
+    for Ta, Tb in zip(seq.trajectory(), la.trajectory()):
+        assert np.array_equal(Ta, Tb)
+    ma, mb = seq.window.map_points, la.window.map_points
+    assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
+    # the look-ahead: submit(0), then per frame t: collect(t), submit(t + 1), [pnp(t)]
+    log = [e for e in spy.log]
+    assert log[:3] == ["submit", "collect", "submit"]
+    first_pnp = log.index("pnp")
+    assert log[first_pnp - 2:first_pnp] == ["collect", "submit"]
+    assert log.count("submit") == log.count("collect") == len(s.frames)
+    # an early stop leaves no frame in flight
+    la2 = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=OracleBackend(oracle, w, h, cams))
+    g = la2.run(s.frames)
+    next(g)
+    g.close()
+    assert la2.backend._submitted is None

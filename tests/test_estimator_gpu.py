@@ -3,13 +3,20 @@ with fused unprojection, PnP + keyframe rule, BA -- against the same host logic 
 backend (oracle/estimator.py), frame by frame on the rendered stream.
 
 Parity: features (ids, f32 undistorted coordinates) bit-exact every frame (both sides use glibc
-sinf/cosf semantics, as the reference's f32::sin/cos); keyframe flags equal; PnP and BA outcomes equal in class
-(ran / success / failure); poses within 1e-6 m / rad -- BA and PnP agree to 1e-7 per solve
-(test_ba_gpu, test_motion_gpu) and map points are narrowed to f32 between solves, so
-differences may carry over frames.  The termination REASON of a converged LM (cost tolerance 1
-vs parameter tolerance 2) is a threshold test on values the GPU reduces in a different fixed
-order, so it may flip on a frame whose last step sits at the threshold: such flips are counted
-and must stay rare (<= 1 in 20 frames), and the poses still agree to the tolerance.
+sinf/cosf semantics, as the reference's f32::sin/cos); keyframe flags equal; BA status and LM
+iteration count EXACTLY equal on every solve; poses within 1e-6 m / rad -- BA and PnP agree to 1e-7
+per solve (test_ba_gpu, test_motion_gpu) and map points are narrowed to f32 between solves, so
+differences may carry over frames.
+
+PnP status and iteration count are exactly equal too, except on the frames listed in PNP_TAIL: there
+the PnP LM reaches the same minimum (final costs equal to ~1e-14 relative, the pose within 1e-9)
+but keeps iterating in its converged tail, where the accept test compares cost changes at rounding
+level (~1e-15 relative) and the GPU's fixed-order tree sums round differently from the oracle's
+sequential ones (oracle.estimator.outcome_difference).  Everything is deterministic, so the lists
+are pinned EXACTLY -- the (status, iterations) of both sides on each listed frame, and no other
+frame may differ: a kernel change that moves any termination fails here loudly.  Observed with
+tools/c4_outcomes.py (profiles/r04_c4_outcomes.txt); the bench's 500-frame stream has the same two
+frames as its first 200 (26, 101) and no other.
 """
 import numpy as np
 import pytest
@@ -17,6 +24,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-6
+
+# stream -> {frame: (device PnP (status, iterations), oracle PnP (status, iterations))}
+PNP_TAIL = {
+    "scene24": {10: ((1, 4), (1, 3)), 12: ((1, 3), (1, 4)), 21: ((1, 3), (1, 4))},
+    "scene72": {16: ((1, 3), (1, 4)), 29: ((1, 3), (2, 8)), 37: ((1, 3), (1, 5)), 59: ((1, 4), (1, 3))},
+    "dev200": {26: ((1, 3), (1, 4)), 101: ((1, 3), (1, 5))},
+}
 
 
 class _Spy:
@@ -31,11 +45,36 @@ class _Spy:
         self.feats = self.be.track(l, r)
         return self.feats
 
+    def submit(self, l, r):
+        self.be.submit(l, r)
+
+    def collect(self):
+        self.feats = self.be.collect()
+        return self.feats
+
     def __getattr__(self, k):
         return getattr(self.be, k)
 
 
-def _compare_with_oracle(oracle, s, win):
+def _outcome(r):
+    return r.pnp_status, r.pnp_iterations, r.pnp_cost, r.ba_status, r.ba_iterations
+
+
+def _check_outcome(k, rd, ro, tail):
+    from oracle.estimator import outcome_difference
+    d = outcome_difference(rd, ro)
+    if k in tail:
+        assert d == "pnp_tail", f"frame {k}: {d}"
+        assert ((rd.pnp_status, rd.pnp_iterations), (ro.pnp_status, ro.pnp_iterations)) == tail[k], f"frame {k}"
+    else:
+        assert d is None, f"frame {k}: {d}"
+    assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
+
+
+def _compare_with_oracle(oracle, s, win, tail, lookahead=False):
+    """lookahead: the device Estimator runs Estimator.run (tracker one frame ahead, pipelined BA);
+    its FrameResults are checked after the stream (a keyframe's BA outcome lands one frame late).
+    tail: the stream's PNP_TAIL entry."""
     from oracle.estimator import OracleBackend
     from rsvio.camera import Camera
     from rsvio.estimator import DeviceBackend, Estimator
@@ -43,23 +82,25 @@ def _compare_with_oracle(oracle, s, win):
     cams = [Camera.opencv5(*p) for p in s.intrinsics]
     dev = _Spy(DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0))
     orc = _Spy(OracleBackend(oracle, w, h, cams))
-    ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev)
+    ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=dev, pipelined=lookahead)
     eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=orc)
-    n_kf = flips = 0
-    for k, (l, r) in enumerate(s.frames):
-        rd = ed.process_frame(l, r)
+    dev_frames = ed.run(s.frames) if lookahead else (ed.process_frame(l, r) for l, r in s.frames)
+    outs = []
+    for k, ((l, r), rd) in enumerate(zip(s.frames, dev_frames)):
         ro = eo.process_frame(l, r)
         for (ids_d, uv_d), (ids_o, uv_o) in zip(dev.feats, orc.feats):
             assert np.array_equal(ids_d, ids_o), f"frame {k}"
             assert np.array_equal(np.asarray(uv_d, np.float32).view(np.uint32),
                                   np.asarray(uv_o, np.float32).view(np.uint32)), f"frame {k}"
-        assert rd.is_keyframe == ro.is_keyframe, f"frame {k}"
-        for a, b in ((rd.pnp_status, ro.pnp_status), (rd.ba_status, ro.ba_status)):
-            assert (a is None) == (b is None) and (a is None or (a > 0) == (b > 0)), f"frame {k}: {a} vs {b}"
-        flips += (rd.pnp_status, rd.ba_status) != (ro.pnp_status, ro.ba_status)
-        assert np.abs(rd.T_W_B - ro.T_W_B).max() <= POSE_TOL, f"frame {k}"
+        outs.append((rd, ro))
+        if not lookahead:  # (look-ahead: a keyframe's BA outcome lands one frame late)
+            _check_outcome(k, rd, ro, tail)
+    ed.flush()
+    assert len(outs) == len(s.frames)
+    n_kf = 0
+    for k, (rd, ro) in enumerate(outs):
+        _check_outcome(k, rd, ro, tail)
         n_kf += rd.is_keyframe
-    assert flips <= max(1, len(s.frames) // 20), flips
     for Td, To in zip(ed.trajectory(), eo.trajectory()):
         assert np.abs(Td - To).max() <= POSE_TOL
     assert win < n_kf < len(s.frames)
@@ -72,7 +113,7 @@ def _compare_with_oracle(oracle, s, win):
 
 def test_estimator_matches_oracle_pipeline(gpu, oracle, scene_stream):
     s, win = scene_stream
-    _compare_with_oracle(oracle, s, win)
+    _compare_with_oracle(oracle, s, win, PNP_TAIL["scene24"])
 
 
 def test_estimator_matches_oracle_window10(gpu, oracle, scene_stream_long):
@@ -82,16 +123,17 @@ def test_estimator_matches_oracle_window10(gpu, oracle, scene_stream_long):
     BA at every keyframe (21 solves), frame by frame against the oracle backend."""
     s, win = scene_stream_long
     assert win == 10 and len(s.frames) >= 60
-    n_kf, _ = _compare_with_oracle(oracle, s, win)
+    n_kf, _ = _compare_with_oracle(oracle, s, win, PNP_TAIL["scene72"])
     assert n_kf >= win + 15
 
 
 def test_estimator_matches_oracle_200_frames(gpu, oracle):
     """The config-4 stream at the reference window over 200 frames (the bench's stream, rendered
     on the device so the test stays within its time budget, then handed to both backends as
-    host images): every frame's ids and undistorted bits, keyframe flags, PnP / BA outcome and
-    pose against the oracle backend, as above.  tools/config4_parity.py runs the same comparison
-    over all 500 frames (profiles/r03a_config4_parity_500.json)."""
+    host images), the device Estimator in the bench's mode (Estimator.run: tracker one frame
+    ahead, pipelined BA): every frame's ids and undistorted bits, keyframe flags, PnP / BA status
+    and iteration counts and pose against the oracle backend, as above.  tools/config4_parity.py
+    runs the same comparison over all 500 frames."""
     import dataclasses
 
     import torch
@@ -100,32 +142,37 @@ def test_estimator_matches_oracle_200_frames(gpu, oracle):
     s = S.euroc_scene_stream_device(200, torch.device("cuda", 0))
     frames = [(l.cpu().numpy(), r.cpu().numpy()) for l, r in s.frames]
     s = dataclasses.replace(s, frames=frames)
-    n_kf, _ = _compare_with_oracle(oracle, s, 10)
+    n_kf, _ = _compare_with_oracle(oracle, s, 10, PNP_TAIL["dev200"], lookahead=True)
     assert n_kf >= 50
 
 
 def test_estimator_pipelined_matches_sequential(gpu, scene_stream):
     """Pipelined mode on the device (the BA solve on its stream overlaps the next frame's
-    tracking): frame results, trajectory and map bit-identical to the sequential order."""
+    tracking), and Estimator.run on top of it (the tracker one frame ahead: frame t + 1 tracks
+    while frame t's PnP reads its own output slot and its BA starts): frame results, trajectory
+    and map bit-identical to the sequential order."""
     from rsvio.camera import Camera
     from rsvio.estimator import DeviceBackend, Estimator
     s, win = scene_stream
     h, w = s.frames[0][0].shape
     cams = [Camera.opencv5(*p) for p in s.intrinsics]
     res, ests = [], []
-    for pipelined in (False, True):
+    for mode in ("sequential", "pipelined", "lookahead"):
         be = DeviceBackend(w, h, cams, 6, 50, 20, 0.01, win, 0.05, 0.05, 0)
-        est = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=be, pipelined=pipelined)
-        res.append([est.process_frame(l, r) for l, r in s.frames])
+        est = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=win, backend=be, pipelined=mode != "sequential")
+        if mode == "lookahead":
+            res.append(list(est.run(s.frames)))
+        else:
+            res.append([est.process_frame(l, r) for l, r in s.frames])
         est.flush()
         ests.append(est)
-    for x, y in zip(*res):
-        assert (x.is_keyframe, x.pnp_status, x.ba_status, x.n_left, x.n_right) == \
-               (y.is_keyframe, y.pnp_status, y.ba_status, y.n_left, y.n_right)
-        assert np.array_equal(x.T_W_B, y.T_W_B)
-    for Ta, Tb in zip(ests[0].trajectory(), ests[1].trajectory()):
-        assert np.array_equal(Ta, Tb)
-    ma, mb = ests[0].window.map_points, ests[1].window.map_points
-    assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
+    for other, e in zip(res[1:], ests[1:]):
+        for x, y in zip(res[0], other):
+            assert (x.is_keyframe, x.n_left, x.n_right) + _outcome(x) == (y.is_keyframe, y.n_left, y.n_right) + _outcome(y)
+            assert np.array_equal(x.T_W_B, y.T_W_B)
+        for Ta, Tb in zip(ests[0].trajectory(), e.trajectory()):
+            assert np.array_equal(Ta, Tb)
+        ma, mb = ests[0].window.map_points, e.window.map_points
+        assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
     for e in ests:
         e.close()

@@ -128,3 +128,72 @@ def test_track_motion_from_the_tracker(gpu, oracle, stereo_frames):
     finally:
         mt.close()
         trk.close()
+
+
+def test_track_motion_reads_the_collected_frame_while_the_next_tracks(gpu, oracle, stereo_frames):
+    """The Estimator's look-ahead (rsvio_tracker_submit / _collect): with frame t + 1 submitted
+    (in flight or done on the tracker's stream), rsvio_track_motion_tracker still reads frame t's
+    output slot -- the same result as before the submit -- and after frame t + 1 is collected it
+    reads frame t + 1's; both equal the oracle on the lists read back.  One frame in flight per
+    handle: a second submit, a process_frame, remove_ids or set_cameras while one is, and a collect
+    without one, are refused."""
+    from rsvio import RsvioError
+    from rsvio import synthetic as S
+    from rsvio.camera import EUROC
+    from rsvio.motion import MotionTracker
+    trk = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50)
+    trk.set_cameras(*EUROC)
+    mt = MotionTracker()
+    T_last = np.eye(4)
+    T_C_B2 = np.stack([np.linalg.inv(S.T_B_CL).reshape(16), np.linalg.inv(S.T_B_CR).reshape(16)])
+
+    def frame_map(fl, ul):
+        ids = fl["id"].astype(np.uint64)
+        rays = np.concatenate([ul.astype(np.float64), np.ones((len(ul), 1))], 1) * 4.0
+        p_W = (S.T_B_CL[:3, :3] @ rays.T).T + S.T_B_CL[:3, 3]
+        return ids, p_W.astype(np.float32)
+
+    try:
+        trk.submit(*stereo_frames[0])
+        with pytest.raises(RsvioError):
+            trk.submit(*stereo_frames[1])
+        with pytest.raises(RsvioError):
+            trk.process_frame(*stereo_frames[1])
+        trk.collect()
+        with pytest.raises(RsvioError):
+            trk.collect()
+        trk.submit(*stereo_frames[1])
+        fl, fr = trk.collect()
+        ul, ur = trk.undistorted()
+        ids, p_W = frame_map(fl, ul)
+        mt.set_map(ids, p_W)
+        r_before = mt.track_motion_tracker(trk, T_last, T_C_B2)
+        o = oracle.track_motion(ids, ul, fr["id"].astype(np.uint64), ur, ids, p_W, T_last, T_C_B2)
+        _check(r_before, o)
+        trk.submit(*stereo_frames[2])                      # frame t + 1 in flight
+        for call in (lambda: trk.remove_id(fl["id"][:1]), lambda: trk.set_cameras(*EUROC)):
+            with pytest.raises(RsvioError):
+                call()
+        r_during = mt.track_motion_tracker(trk, T_last, T_C_B2)
+        assert np.array_equal(r_during.T_W_B, r_before.T_W_B)
+        assert (r_during.status, r_during.iterations, r_during.n_observations) == \
+               (r_before.status, r_before.iterations, r_before.n_observations)
+        assert np.array_equal(trk.undistorted()[0], ul)  # undistorted() is the collected frame's too
+        fl2, fr2 = trk.collect()
+        ul2, ur2 = trk.undistorted()
+        r_after = mt.track_motion_tracker(trk, T_last, T_C_B2)
+        o2 = oracle.track_motion(fl2["id"].astype(np.uint64), ul2, fr2["id"].astype(np.uint64), ur2, ids, p_W,
+                                 T_last, T_C_B2)
+        _check(r_after, o2)
+        # the look-ahead's lists equal process_frame's on a fresh tracker
+        ref = gpu.StereoPatchTracker(752, 480, levels=3, grid_size=50)
+        ref.set_cameras(*EUROC)
+        for f in stereo_frames[:2]:
+            ref.process_frame(*f)
+        gl, gr = ref.process_frame(*stereo_frames[2])
+        assert np.array_equal(gl, fl2) and np.array_equal(gr, fr2)
+        assert all(np.array_equal(a, b) for a, b in zip(ref.undistorted(), (ul2, ur2)))
+        ref.close()
+    finally:
+        mt.close()
+        trk.close()
