@@ -419,6 +419,27 @@ void rsvio_pnp_destroy(rsvio_pnp* p);
  * iterative Rotation3::from_matrix_eps(m, f64::EPSILON, 0, identity) then from_rotation_matrix,
  * for n row-major 3x3 matrices -> n quaternions (w, i, j, k).  Host only (no device needed). */
 int rsvio_quat_from_matrix(const double* R, size_t n, double* q);
+/* ---- the Estimator's per-keyframe host logic (host only, no device needed) ---- */
+
+/* SlidingWindow::optimize's problem assembly (sliding_window.rs:174-300) for a window of n_kf
+ * keyframes: T_W_B (n_kf row-major 4x4), T_B_C2 (the FRONT keyframe's T_B_Cl, T_B_Cr; :180-181),
+ * per keyframe k and camera c (list 2k + c, the 2 n_kf lists back to back in ids / uv, n_feat[i]
+ * entries each) the features' ids and undistorted coordinates (frame.rs:107-134, f32), the map (ids strictly ascending, p_W as f32; :466-475).  Out: pose7
+ * (T_B_W as [t; w, i, j, k], :214-226), kf_fixed (KF_0), T_C_B2 (T_Cl_B, T_Cr_B), the landmarks
+ * -- features seen at least once in each camera across the window (:183-209, :238-240), indexed
+ * by first appearance -- with their ids and initial values (map point, else depth 2.0 along the
+ * first observation's ray, :241-262), and one observation per factor in window order (keyframe,
+ * left then right, feature order).  RSVIO_ERR_CAPACITY when cap_lm / cap_obs are too small. */
+int rsvio_window_problem(int32_t n_kf, const double* T_W_B, const double* T_B_C2, const uint64_t* ids,
+                         const float* uv, const int32_t* n_feat, const uint64_t* map_ids,
+                         const float* map_pw, int32_t n_map, double* pose7, uint8_t* kf_fixed, double* T_C_B2,
+                         int32_t cap_lm, uint64_t* lm_ids, double* p_init, int32_t* n_lm, int32_t cap_obs,
+                         int32_t* obs_lm, int32_t* obs_kf, uint8_t* obs_cam, double* obs_uv, int32_t* n_obs);
+/* process_optimization_result (sliding_window.rs:418-486): keyframe T_W_B = inverse(SE3(pose7))
+ * (n_kf row-major 4x4) and the map = the optimised landmarks as f32, by ascending id. */
+int rsvio_window_apply(int32_t n_kf, const double* pose7, int32_t n_lm, const uint64_t* lm_ids, const double* p_W,
+                       double* T_W_B, uint64_t* map_ids, float* map_pw);
+
 /* Launch rsvio_track_motion on a caller-owned stream (hipStream_t; NULL: the handle's own). */
 int rsvio_pnp_set_stream(rsvio_pnp* p, void* stream);
 /* SlidingWindow::map_points after optimize (sliding_window.rs:466-475): feature ids strictly

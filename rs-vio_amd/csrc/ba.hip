@@ -2409,32 +2409,63 @@ struct WinDesc {
     int skip;
 };
 
+// The descriptor's fields a block needs before its first data load -- the skip flag, its grid
+// bound and the problem pointers -- are read at entry, unconditionally, so their scalar loads
+// go out together (one round trip to the descriptor); an early exit tested first (a
+// short-circuit `skip || n_wave` test) chained two more dependent round trips before any data
+// load could issue.  (The state views stay references into the descriptor: a local copy of Work
+// is indexed by the state's cur at run time, which puts it in scratch memory.)
+// Forces pointer fields of the descriptor into SGPRs at this point (their scalar loads are
+// issued with the ones before, one wait for all); the body's later reads of the same fields are
+// the same loads (no store in between), so its first data loads issue right after the exit test.
+__device__ __forceinline__ void desc_touch1(const void* p) { __asm__ volatile("" ::"s"(p)); }
+template <class... T>
+__device__ __forceinline__ void desc_touch(const T*... p) {
+    (desc_touch1(p), ...);
+}
+
 __global__ __launch_bounds__(64) void bab_linearize(const WinDesc* __restrict__ D, double lambda0) {
     const WinDesc& d = D[blockIdx.y];
-    if (d.skip || (int)blockIdx.x >= d.G.n_wave) return;
-    linearize_body(d.G, d.Pr, d.W[2], blockIdx.x, 1, lambda0);
+    const int skip = d.skip, bound = d.G.n_wave;
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[2];
+    desc_touch(Pr.slot_hdr, Pr.slot_uv, Wk.pose_init, Wk.pw_init, Wk.st);
+    if (skip | ((int)blockIdx.x >= bound)) return;
+    linearize_body(d.G, Pr, Wk, blockIdx.x, 1, lambda0);
 }
 
 __global__ __launch_bounds__(kSchurThreads) void bab_schur_chunks(const WinDesc* __restrict__ D, int wi, LmArgs la) {
     const WinDesc& d = D[blockIdx.y];
-    if (d.skip || (int)blockIdx.x >= d.G.n_chunk) return;
-    schur_chunks_body(d.G, d.Pr, d.W[wi], la, 0, blockIdx.x);
+    const int skip = d.skip, bound = d.G.n_chunk;
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[wi];
+    desc_touch(Pr.pairs, Wk.partD, Wk.pose[0], Wk.pose[1], Wk.st_prev, Wk.st);
+    if (skip | ((int)blockIdx.x >= bound)) return;
+    schur_chunks_body(d.G, Pr, Wk, la, 0, blockIdx.x);
 }
 
 template <int NF>
 __global__ __launch_bounds__(kK5Threads) void bab_camera_solve(const WinDesc* __restrict__ D, int wi) {
     const WinDesc& d = D[blockIdx.x];
-    if (d.skip) return;
-    camera_solve_mfma_body<NF>(d.G, d.Pr, d.W[wi], 1);
+    const int skip = d.skip;
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[wi];
+    if (skip) return;
+    camera_solve_mfma_body<NF>(d.G, Pr, Wk, 1);
 }
 
 __global__ __launch_bounds__(64) void bab_backsub_relinearize(const WinDesc* __restrict__ D, int wi) {
     const WinDesc& d = D[blockIdx.y];
-    if (d.skip || (int)blockIdx.x >= d.G.n_wave) return;
+    const int skip = d.skip, bound = d.G.n_wave;
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[wi];
+    desc_touch(Pr.slot_hdr, Pr.slot_uv, Wk.st, Wk.raws[0], Wk.raws[1], Wk.rawl[0], Wk.rawl[1], Wk.pw[0], Wk.pw[1],
+               Wk.pose[0], Wk.pose[1], Wk.dc);
+    if (skip | ((int)blockIdx.x >= bound)) return;
     __shared__ double sh[10][64];
     __shared__ double shp[3][64];
     __shared__ double shs[4][64];
-    k6_body<false>(d.G, d.Pr, d.W[wi], blockIdx.x, threadIdx.x, sh, shp, shs);
+    k6_body<false>(d.G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs);
 }
 
 // Single-window front end of K7 (the handle's graph in descriptor mode, BundleAdjuster::start_graph):
@@ -2443,7 +2474,9 @@ __global__ __launch_bounds__(64) void bab_backsub_relinearize(const WinDesc* __r
 __global__ __launch_bounds__(kK7Threads) void bad_lm_decide(const WinDesc* __restrict__ D, int wi, LmArgs la,
                                                             LmState* host, unsigned long long* htick, double* hout) {
     const WinDesc& d = D[0];
-    lm_decide_body(d.G, d.Pr, d.W[wi], 0, la, host, htick, hout);
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[wi];
+    lm_decide_body(d.G, Pr, Wk, 0, la, host, htick, hout);
 }
 
 // K7 per window: the pending decision in place and into the pinned host copy host[window]

@@ -164,14 +164,20 @@ __device__ __forceinline__ void chains(const float (&v)[N], const float (&init)[
     const int c = lane < N ? lane : 0;
     float acc = sh[c * kLd + 64];
     const float4* row = reinterpret_cast<const float4*>(sh + c * kLd);
+    float4 xs[NP / 4];
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) xs[q] = row[q];
 #pragma unroll
     for (int q = 0; q < NP / 4; ++q) {
-        const float4 x = row[q];
+        const float4 x = xs[q];
         acc = acc + x.x;
         acc = acc + x.y;
         acc = acc + x.z;
         acc = acc + x.w;
     }
+    // every row read issued before the first add (one LDS latency per chain, as lk_track.hip)
+    __builtin_amdgcn_sched_group_barrier(0x100, NP / 4 + 1, 0);  // DS reads (+ the start value)
+    __builtin_amdgcn_sched_group_barrier(0x002, NP, 0);          // the chain's VALU adds
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), i));

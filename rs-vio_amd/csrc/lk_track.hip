@@ -61,10 +61,13 @@ __device__ __forceinline__ void lane_chains(const float (&v)[N], float (&out)[N]
     for (int i = 0; i < N; ++i) sh[i * kChainLd + lane] = v[i];
     __builtin_amdgcn_wave_barrier();
     const float4* row = reinterpret_cast<const float4*>(sh + (lane < N ? lane : 0) * kChainLd);
+    float4 xs[NP / 4];
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) xs[q] = row[q];
     float acc = 0.0f;
 #pragma unroll
     for (int q = 0; q < NP / 4; ++q) {
-        const float4 x = row[q];
+        const float4 x = xs[q];
         if (!FROM_ZERO && q == 0)
             acc = x.x;
         else
@@ -73,6 +76,11 @@ __device__ __forceinline__ void lane_chains(const float (&v)[N], float (&out)[N]
         acc = acc + x.z;
         acc = acc + x.w;
     }
+    // all 13 row reads issued before the first add, consumed in order as they land (the chain
+    // then waits on LDS latency once, not once per row: the scheduler otherwise interleaves
+    // reads and adds two rows deep when registers are tight)
+    __builtin_amdgcn_sched_group_barrier(0x100, NP / 4, 0);  // DS reads
+    __builtin_amdgcn_sched_group_barrier(0x002, NP, 0);      // the chain's VALU adds
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), i));
@@ -137,18 +145,19 @@ __device__ __forceinline__ Aff mul3(const Aff& A, const Aff& B) {
 
 // image_utilities.rs:82-106, twist [vx, vy, theta]; sin/cos = glibc sinf/cosf (trig.hpp)
 __device__ __forceinline__ Aff se2_exp(float a0, float a1, float theta) {
-    const double rth = rcp_f64((double)theta);  // beside sincosf (the quotients' divisor)
+    double rth = rcp_f64((double)theta);  // beside sincosf (the quotients' divisor)
+    // pinned here: the compiler otherwise sinks the reciprocal into the branch that uses it,
+    // after sincosf, and its ~7 dependent f64 ops land on the chain instead of beside it
+    __asm__ volatile("" : "+v"(rth));
     float s, c;
     libm_trig::sincosf(theta, &s, &c);
-    float sin_by, omc_by;
-    if (fabsf(theta) < __FLT_EPSILON__) {
-        float th2 = theta * theta;
-        sin_by = 1.0f - (1.0f / 6.0f) * th2;
-        omc_by = 0.5f * theta - (1.0f / 24.0f) * theta * th2;
-    } else {
-        sin_by = div_rcp(s, rth);          // s / theta
-        omc_by = div_rcp(1.0f - c, rth);   // (1 - c) / theta
-    }
+    // both forms, then a select (no branch between sincosf and the update)
+    const float th2 = theta * theta;
+    const float sin_small = 1.0f - (1.0f / 6.0f) * th2;
+    const float omc_small = 0.5f * theta - (1.0f / 24.0f) * theta * th2;
+    const bool small = fabsf(theta) < __FLT_EPSILON__;
+    const float sin_by = small ? sin_small : div_rcp(s, rth);         // s / theta
+    const float omc_by = small ? omc_small : div_rcp(1.0f - c, rth);  // (1 - c) / theta
     Aff E;
     E.m00 = c; E.m01 = -s; E.m10 = s; E.m11 = c;
     E.m02 = sin_by * a0 - omc_by * a1;

@@ -99,6 +99,9 @@ SIG = {
                                               C.c_size_t, C.POINTER(C.c_size_t)]),
     "rsvio_tracker_process_frame_device": (C.c_int, [P, P, P, P, C.c_size_t, C.POINTER(C.c_size_t), P,
                                                      C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rsvio_window_problem": (C.c_int, [C.c_int32, P, P, P, P, P, P, P, C.c_int32, P, P, P, C.c_int32, P, P,
+                                       C.POINTER(C.c_int32), C.c_int32, P, P, P, P, C.POINTER(C.c_int32)]),
+    "rsvio_window_apply": (C.c_int, [C.c_int32, P, C.c_int32, P, P, P, P, P]),
     "rsvio_tracker_submit": (C.c_int, [P, P, P, C.c_size_t]),
     "rsvio_tracker_submit_device": (C.c_int, [P, P, P]),
     "rsvio_tracker_collect": (C.c_int, [P, P, C.c_size_t, C.POINTER(C.c_size_t), P, C.c_size_t,
@@ -210,9 +213,10 @@ def ptr(a) -> int | None:
     """Host pointer of a C-contiguous numpy array (or None)."""
     if a is None:
         return None
-    if not a.flags["C_CONTIGUOUS"]:
+    ai = a.__array_interface__  # (half the cost of a.ctypes.data; strides None = C-contiguous)
+    if ai["strides"] is not None and not a.flags["C_CONTIGUOUS"]:
         raise ValueError("array must be C-contiguous")
-    return a.ctypes.data
+    return ai["data"][0]
 
 
 def require_device(device: int = 0) -> str:

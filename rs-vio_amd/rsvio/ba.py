@@ -218,16 +218,18 @@ class Frame:
     right_features: list = field(default_factory=list)
 
 
-def _feature_arrays(feats):
-    """(ids int64, uv f64 n x 2) from a frame's features: (ids, uv) arrays or (id, (x, y)) pairs;
-    coordinates pass through f32 like Feature::undistorted_coord (frame.rs:118-119)."""
+def _feature_lists(feats):
+    """(ids u64, uv f32 n x 2) C-contiguous from a frame's features: (ids, uv) arrays or
+    (id, (x, y)) pairs (Feature::undistorted_coord is f32, frame.rs:118-119)."""
     if isinstance(feats, tuple) and len(feats) == 2 and isinstance(feats[0], np.ndarray):
         ids, uv = feats
+        if ids.dtype == np.int64 and uv.dtype == np.float32 and uv.ndim == 2:  # the Estimator's lists
+            return ids.view(np.uint64), uv
     else:
         ids = [fid for fid, _ in feats]
         uv = [xy for _, xy in feats]
-    return (np.asarray(ids, np.int64).reshape(-1),
-            np.asarray(uv, np.float64).reshape(-1, 2).astype(np.float32).astype(np.float64))
+    ids = np.ascontiguousarray(np.asarray(ids, np.int64).reshape(-1)).view(np.uint64)
+    return ids, np.ascontiguousarray(np.asarray(uv, np.float32).reshape(-1, 2))
 
 
 def quat_from_matrix(R) -> np.ndarray:
@@ -335,55 +337,31 @@ class SlidingWindow:
         """sliding_window.rs:174-300 in canonical order (frames, left then right, feature order):
         landmarks = ids seen at least once left and once right in the window, indexed by first
         appearance; initial point from map_points (f32) or the depth-2.0 ray of its first
-        observation (sliding_window.rs:248-272).  Vectorised over the window's observations."""
+        observation (sliding_window.rs:248-272).  Assembled by the library's host code
+        (rsvio_window_problem, csrc/window.hip) in one call."""
         kfs = list(self.keyframes)
-        # stacked inversions (numpy inverts each matrix exactly as a single call would)
-        T_Cl_B, T_Cr_B = np.linalg.inv(np.stack([kfs[0].T_B_Cl, kfs[0].T_B_Cr]))
-        ids, uv, kf, cam = [], [], [], []
-        for i, f in enumerate(kfs):
-            for c, feats in enumerate((f.left_features, f.right_features)):
-                fi, fu = _feature_arrays(feats)
-                ids.append(fi)
-                uv.append(fu)
-                kf.append(np.full(len(fi), i, np.int32))
-                cam.append(np.full(len(fi), c, np.uint8))
-        ids, uv = np.concatenate(ids), np.concatenate(uv)
-        kf, cam = np.concatenate(kf), np.concatenate(cam)
-        keep = np.isin(ids, ids[cam == 0]) & np.isin(ids, ids[cam == 1])
-        ids, uv, kf, cam = ids[keep], uv[keep], kf[keep], cam[keep]
-        uniq, first, inv = np.unique(ids, return_index=True, return_inverse=True)
-        order = np.argsort(first, kind="stable")          # landmarks by first appearance
-        rank = np.empty(len(uniq), np.int64)
-        rank[order] = np.arange(len(uniq))
-        obs_lm = rank[inv].astype(np.int32)
-        lm_ids = uniq[order]
-        p_init = np.zeros((len(lm_ids), 3))
-        in_map = np.zeros(len(lm_ids), bool)
-        if len(self.map_ids):
-            mid, mpw = self.map_ids, self.map_pw.astype(np.float64)  # ascending ids
-            pos = np.clip(np.searchsorted(mid, lm_ids), 0, len(mid) - 1)
-            in_map = mid[pos] == lm_ids
-            p_init[in_map] = mpw[pos[in_map]]
-        fo = first[order]                                  # first observation of each landmark
-        T_B_C = np.linalg.inv(np.stack([T_Cl_B, T_Cr_B]))
-        T_W_B = np.stack([f.T_W_B for f in kfs])
-        new = np.nonzero(~in_map)[0]
-        if len(new):
-            # p_W = T_W_B (T_B_C (u, v, 2.0)) of the first observation, batched (same per-row bits
-            # as the 3x3 @ 3 products of a per-landmark loop)
-            o = fo[new]
-            Tbc, Twb = T_B_C[cam[o]], T_W_B[kf[o]]
-            p_C = np.stack([uv[o, 0], uv[o, 1], np.full(len(o), 2.0)], 1)
-            p_B = np.matmul(Tbc[:, :3, :3], p_C[:, :, None])[:, :, 0] + Tbc[:, :3, 3]
-            p_init[new] = np.matmul(Twb[:, :3, :3], p_B[:, :, None])[:, :, 0] + Twb[:, :3, 3]
-        pose7 = np.zeros((len(kfs), 7))
-        T_B_W = np.linalg.inv(T_W_B)  # try_inverse (:218)
-        pose7[:, :3] = T_B_W[:, :3, 3]
-        pose7[:, 3:] = quat_from_matrix(T_B_W[:, :3, :3])  # UnitQuaternion::from_matrix (:221)
-        kf_fixed = np.zeros(len(kfs), np.uint8)
-        kf_fixed[0] = 1
-        T_C_B2 = np.stack([T_Cl_B.reshape(16), T_Cr_B.reshape(16)])
-        return (pose7, kf_fixed, p_init, obs_lm, kf.astype(np.int32), cam, uv, T_C_B2, lm_ids)
+        n = len(kfs)
+        lists = [_feature_lists(feats) for f in kfs for feats in (f.left_features, f.right_features)]
+        ids_a = np.concatenate([i for i, _ in lists])
+        uv_a = np.concatenate([u for _, u in lists])
+        n_feat = np.array([len(i) for i, _ in lists], np.int32)
+        tot = len(ids_a)
+        T_W_B = np.ascontiguousarray(np.stack([f.T_W_B for f in kfs]), np.float64)
+        T_B_C2 = np.ascontiguousarray(np.stack([kfs[0].T_B_Cl, kfs[0].T_B_Cr]), np.float64)
+        map_ids = self.map_ids.view(np.uint64) if self.map_ids.dtype == np.int64 else self.map_ids
+        pose7, fixed, tcb = np.empty((n, 7)), np.empty(n, np.uint8), np.empty((2, 16))
+        lm_ids, p_init = np.empty(max(tot, 1), np.uint64), np.empty((max(tot, 1), 3))
+        obs_lm, obs_kf = np.empty(max(tot, 1), np.int32), np.empty(max(tot, 1), np.int32)
+        obs_cam, obs_uv = np.empty(max(tot, 1), np.uint8), np.empty((max(tot, 1), 2))
+        n_lm, n_obs = C.c_int32(0), C.c_int32(0)
+        check(_lib.load().rsvio_window_problem(
+            n, ptr(T_W_B), ptr(T_B_C2), ptr(ids_a) if tot else None, ptr(uv_a) if tot else None, ptr(n_feat), ptr(map_ids) if len(map_ids) else None,
+            ptr(self.map_pw) if len(map_ids) else None, len(map_ids), ptr(pose7), ptr(fixed), ptr(tcb),
+            max(tot, 1), ptr(lm_ids), ptr(p_init), C.byref(n_lm), max(tot, 1), ptr(obs_lm), ptr(obs_kf),
+            ptr(obs_cam), ptr(obs_uv), C.byref(n_obs)))
+        L, O = n_lm.value, n_obs.value
+        return (pose7, fixed, p_init[:L], obs_lm[:O], obs_kf[:O], obs_cam[:O], obs_uv[:O], tcb,
+                lm_ids[:L].view(np.int64))
 
     def optimize(self, cfg=None) -> bool:
         """Returns Ok(true)/Ok(false) as a bool; raises RuntimeError for a non-full window (:137-149)."""
@@ -405,14 +383,21 @@ class SlidingWindow:
         return self._apply(ids, pose, pw, res)
 
     def _apply(self, ids, pose, pw, res) -> bool:
-        """process_optimization_result (sliding_window.rs:418-486)."""
+        """process_optimization_result (sliding_window.rs:418-486), by the library's host code
+        (rsvio_window_apply): map points as f32 by ascending id, T_W_B = inverse(SE3(pose7))."""
         self.last_result = res
         if res.status <= 0:
             return False  # revert: nothing was modified
-        srt = np.argsort(ids, kind="stable")  # (ids are distinct)
-        self.map_ids, self.map_pw = np.asarray(ids, np.int64)[srt], pw.astype(np.float32)[srt]
+        n, m = len(self.keyframes), len(ids)
+        pose = np.ascontiguousarray(pose, np.float64)
+        pw = np.ascontiguousarray(pw, np.float64).reshape(-1, 3)
+        ids = np.ascontiguousarray(ids, np.int64)
+        T_W_B = np.empty((n, 4, 4))
+        map_ids, map_pw = np.empty(m, np.int64), np.empty((m, 3), np.float32)
+        check(_lib.load().rsvio_window_apply(n, ptr(pose), m, ptr(ids) if m else None, ptr(pw) if m else None,
+                                             ptr(T_W_B), ptr(map_ids) if m else None, ptr(map_pw) if m else None))
+        self.map_ids, self.map_pw = map_ids, map_pw
         self.map_version += 1
-        T_W_B = np.linalg.inv(np.stack([se3_matrix(pose[i]) for i in range(len(self.keyframes))]))
         for f, T in zip(self.keyframes, T_W_B):
             f.T_W_B = T
         return True
