@@ -172,7 +172,7 @@ class Estimator:
                 self.backend.set_map(self.window.map_ids, self.window.map_pw)  # ascending ids, f32
                 self._map_key = self.window.map_version
             status, is_kf, T_W_B, pnp_iters, pnp_cost = self.backend.track_motion(
-                self.window.get_keyframe_poses()[-1], self._T_C_B2())
+                self.window.keyframes[-1].T_W_B, self._T_C_B2())  # keyframes.back() (sliding_window.rs:506)
             pnp_status = status
             if status > 0:
                 frame.T_W_B = T_W_B

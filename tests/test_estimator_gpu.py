@@ -15,8 +15,8 @@ level (~1e-15 relative) and the GPU's fixed-order tree sums round differently fr
 sequential ones (oracle.estimator.outcome_difference).  Everything is deterministic, so the lists
 are pinned EXACTLY -- the (status, iterations) of both sides on each listed frame, and no other
 frame may differ: a kernel change that moves any termination fails here loudly.  Observed with
-tools/c4_outcomes.py (profiles/r04_c4_outcomes.txt); the bench's 500-frame stream has the same two
-frames as its first 200 (26, 101) and no other.
+tools/c4_outcomes.py (profiles/r04g_c4_outcomes.txt); the bench's config-4 row lists its own
+stream's frames (pnp_converged_tail_frames) and fails on any other divergence.
 """
 import numpy as np
 import pytest
@@ -27,9 +27,10 @@ POSE_TOL = 1e-6
 
 # stream -> {frame: (device PnP (status, iterations), oracle PnP (status, iterations))}
 PNP_TAIL = {
-    "scene24": {10: ((1, 4), (1, 3)), 12: ((1, 3), (1, 4)), 21: ((1, 3), (1, 4))},
-    "scene72": {16: ((1, 3), (1, 4)), 29: ((1, 3), (2, 8)), 37: ((1, 3), (1, 5)), 59: ((1, 4), (1, 3))},
-    "dev200": {26: ((1, 3), (1, 4)), 101: ((1, 3), (1, 5))},
+    "scene24": {10: ((1, 4), (1, 3))},
+    "scene72": {11: ((1, 4), (1, 7)), 16: ((1, 3), (1, 4)), 29: ((1, 3), (2, 8)), 37: ((1, 3), (1, 7)),
+                65: ((1, 3), (1, 4))},
+    "dev200": {120: ((1, 4), (1, 3))},
 }
 
 

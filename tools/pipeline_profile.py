@@ -27,8 +27,8 @@ def run(frames, prof=None):
     t0 = time.perf_counter()
     if prof:
         prof.enable()
-    for l, r in frames:
-        est.process_frame(l, r)
+    for _ in est.run(frames):  # the bench's mode: tracker one frame ahead, pipelined BA
+        pass
     est.flush()
     if prof:
         prof.disable()
