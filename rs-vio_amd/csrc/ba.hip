@@ -226,6 +226,43 @@ struct Work {
 __device__ __forceinline__ size_t sys_len(const Geometry& G) { return (size_t)G.n_pb * 36 + 12 * G.n_free + 2; }
 
 // ---------------------------------------------------------------------------------------
+// Landmark sharding over the P2P one-shot exchange
+// ---------------------------------------------------------------------------------------
+constexpr int kP2PMax = 8;       // ranks
+constexpr int kP2PMsg = 8192;    // doubles per slot (>= 36 * 210 + 12 * 20 + 2)
+
+struct P2P {
+    double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
+    int nranks, rank;
+    int* xnw;                    // (local) every rank's wave count, as K5's exchange carried it
+};
+
+// The trial-scalar exchange folded into K6 and the next decision (RSVIO_P2P_FOLD=2): after the
+// system's message slots and their flags, each buffer holds per parity, per source rank and per
+// wave that rank's K6 wave partial (4 doubles) and its generation flag.
+constexpr int kP2PWaves = 16384;  // waves per rank (a larger shard takes the X2 path)
+constexpr size_t kP2PTval = (size_t)2 * kP2PMax * kP2PMsg + 2 * kP2PMax;  // doubles before the trial values
+constexpr size_t kP2PTflag = kP2PTval + (size_t)2 * kP2PMax * kP2PWaves * 4;
+constexpr size_t kP2PBytes = sizeof(double) * (kP2PTflag + (size_t)2 * kP2PMax * kP2PWaves);
+
+__device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
+    return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
+}
+
+// P2P exchange buffer slot [parity][rank] of a peer's buffer, and the generation flags
+__device__ __forceinline__ double* p2p_slot(double* xbuf, int par, int r) {
+    return xbuf + (size_t)(par * kP2PMax + r) * kP2PMsg;
+}
+// trial exchange: wave w of source rank r, parity par (value quad and its flag)
+__device__ __forceinline__ double* p2p_tval(double* xbuf, int par, int r, int w) {
+    return xbuf + kP2PTval + (((size_t)par * kP2PMax + r) * kP2PWaves + w) * 4;
+}
+__device__ __forceinline__ unsigned long long* p2p_tflag(double* xbuf, int par, int r, int w) {
+    return reinterpret_cast<unsigned long long*>(xbuf + kP2PTflag) + ((size_t)par * kP2PMax + r) * kP2PWaves + w;
+}
+
+
+// ---------------------------------------------------------------------------------------
 __global__ void ba_reset(Geometry G, Work Wk, double lambda0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 7 * G.n_kf) {
@@ -686,6 +723,68 @@ __device__ void trial_scalars_wave(const Geometry& G, const Prob& Pr, const Work
     for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
 }
 
+// trial_scalars_wave over ALL ranks of the P2P-sharded solve, from the wave partials every rank's
+// K6 pushed into this rank's exchange buffer (RSVIO_P2P_FOLD=2): per source rank r, in rank order,
+// exactly the per-lane strided sums and the fixed-pairing wave reduction rank r's X2 would have
+// computed (+ |x|^2 of the free poses on rank 0, from this rank's identical pose buffers), then
+// the rank-ordered sum from 0.0 the exchange would have formed -- the same bits as the X2 path.
+// Each lane waits (bounded) for the generation flags of the slots it reads.
+__device__ void trial_scalars_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, const LmState& s, const P2P& P,
+                                  unsigned long long gen, int* err, double out[4]) {
+    const int lane = threadIdx.x & 63, par = (int)(gen & 1);
+    double* own = P.peer[P.rank];
+    const int el = 7 * G.n_kf - 1;
+    double p0[3], p1[3];
+    int fi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int e = min(lane + 64 * k, el);
+        fi[k] = Pr.free_idx[e / 7];
+        p0[k] = Wk.pose[0][e];
+        p1[k] = Wk.pose[1][e];
+    }
+    double sq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (lane + 64 * k <= el && fi[k] >= 0) {
+            sq[0] += p0[k] * p0[k];
+            sq[1] += p1[k] * p1[k];
+        }
+    for (int j = 0; j < 4; ++j) out[j] = 0.0;
+    bool late = false;
+    for (int r = 0; r < P.nranks; ++r) {
+        const int nw = P.xnw[r];
+        double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
+        for (int w = lane; w < max(nw, 512); w += 64) {  // (>= 8 steps: the wave sum's order)
+            double4 v = make_double4(0.0, 0.0, 0.0, 0.0);
+            if (w < nw) {
+                const unsigned long long* f = p2p_tflag(own, par, r, w);
+                long long spins = 0;
+                while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1ll << 25)) {
+                        late = true;
+                        break;
+                    }
+                }
+                const double* q = p2p_tval(own, par, r, w);
+                v.x = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                v.y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                v.z = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                v.w = __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            acc[0] += v.x;
+            acc[1] += v.y;
+            acc[2] += v.z;
+            acc[3] += v.w;
+        }
+        if (r == 0) acc[3] += sq[s.cur];
+#pragma unroll
+        for (int k = 0; k < kPartD; ++k) out[k] += wave_sum_det(acc[k]);
+    }
+    if (late) atomicExch(err, 1);
+}
+
 // The build's LM decision for one iteration: cost = cost at the current
 // state, tv = trial cost, |dp|^2, g_p.dp, |x|^2.  Flips the state buffers on acceptance.
 __device__ void lm_update(LmState& s, double cost, const double tv[4], int max_iter, double cost_tol,
@@ -756,12 +855,18 @@ struct LmArgs {
 // sharded combine + all-reduce, wrote it in iteration 0).  Every caller runs the same
 // operations on the same data, so every workgroup that decides gets identical bits.
 __device__ LmState lm_decide(const Geometry& G, const Prob& Pr, const Work& Wk, const LmState* src, int pre_reduced,
-                             const LmArgs& la) {
+                             const LmArgs& la, const P2P* PP = nullptr, const unsigned long long* xgen = nullptr,
+                             int* err = nullptr) {
     LmState s = *src;
     // the trial scalars are gathered whether or not a decision is pending, so their loads are
-    // in flight together with the state's (one round trip)
+    // in flight together with the state's (one round trip) -- except from the P2P exchange
+    // (pre_reduced 2), which waits for flags only a pending decision has
     double tv[4];
-    if (pre_reduced) {
+    if (pre_reduced == 2) {
+        const unsigned long long gen = *xgen;  // K5 of the iteration that produced the trial
+        for (int k = 0; k < 4; ++k) tv[k] = 0.0;
+        if (s.pending && !s.done && s.solve_ok) trial_scalars_p2p(G, Pr, Wk, s, *PP, gen, err, tv);
+    } else if (pre_reduced) {
         for (int k = 0; k < 4; ++k) tv[k] = Wk.trial4[k];
     } else {
         trial_scalars_wave(G, Pr, Wk, s, 1, tv);
@@ -889,7 +994,8 @@ __device__ __forceinline__ void schur_chunk_pairs(const Geometry& G, const Work&
 }
 
 __device__ void schur_chunks_body(const Geometry& G, const Prob& Pr, const Work& Wk, const LmArgs& la,
-                                  int pre_reduced, int c) {
+                                  int pre_reduced, int c, const P2P* PP = nullptr,
+                                  const unsigned long long* xgen = nullptr, int* err = nullptr) {
     __shared__ double red[kSchurThreads / 64][kBlockF];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pb = c / kGrp, x = c % kGrp;
@@ -905,7 +1011,7 @@ __device__ void schur_chunks_body(const Geometry& G, const Prob& Pr, const Work&
     __shared__ LmState sd;
     STAMP(27);
     if (wave == 0) {
-        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la);
+        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la, PP, xgen, err);
         STAMP(28);
         if (lane == 0) {
             sd = d;
@@ -945,6 +1051,13 @@ __device__ void schur_chunks_body(const Geometry& G, const Prob& Pr, const Work&
 __global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Prob Pr, Work Wk, LmArgs la,
                                                                   int pre_reduced) {
     schur_chunks_body(G, Pr, Wk, la, pre_reduced, blockIdx.x);
+}
+
+// K4c of the P2P-sharded iteration with the trial-scalar exchange folded in (RSVIO_P2P_FOLD=2):
+// the pending decision from every rank's K6 wave partials in this rank's exchange buffer
+__global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks_p2p(Geometry G, Prob Pr, Work Wk, LmArgs la, P2P P,
+                                                                      const unsigned long long* xgen, int* err) {
+    schur_chunks_body(G, Pr, Wk, la, 2, blockIdx.x, &P, xgen, err);
 }
 
 // The reduced system of this rank into dst (sys layout): S, b, g_c summed over the kGrp partial
@@ -1433,23 +1546,6 @@ constexpr int kMfPanel = 8;  // panel width: 8 pivots of in-panel VALU work betw
 // row of every panel).  Rows past NP are never initialised: elimination is row-local (a row's
 // update uses its own multiplier and the pivot rows' values), so they cannot leak into the
 // result; the same holds for the upper halves of the diagonal tiles.
-constexpr int kP2PMax = 8;       // ranks
-constexpr int kP2PMsg = 8192;    // doubles per slot (>= 36 * 210 + 12 * 20 + 2)
-
-struct P2P {
-    double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
-    int nranks, rank;
-};
-
-__device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
-    return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
-}
-
-// P2P exchange buffer slot [parity][rank] of a peer's buffer, and the generation flags
-__device__ __forceinline__ double* p2p_slot(double* xbuf, int par, int r) {
-    return xbuf + (size_t)(par * kP2PMax + r) * kP2PMsg;
-}
-
 template <int NF>
 struct MfDims {
     static constexpr int NP = 6 * NF;
@@ -1605,6 +1701,7 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
             double* d = p2p_slot(P.peer[tid], par, me);
             d[ne] = c;
             d[ne + 1] = sing ? 1.0 : 0.0;
+            d[ne + 2] = (double)G.n_wave;  // (per rank, not summed: the folded trial exchange's bound)
         }
     }
     __threadfence_system();
@@ -1648,6 +1745,9 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
         *fail = f != 0.0;
         *xgen = gen;
     }
+    if (tid < nr && P.xnw)
+        P.xnw[tid] = (int)__hip_atomic_load(mine + (size_t)tid * kP2PMsg + ne + 2, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
     return false;
 }
 
@@ -2171,7 +2271,8 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
 // is taken by the next iteration's K4c blocks (or K7 at the end of a chunk), after the boundary.
 template <bool FUSED>
 __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w, int lane, double (*sh)[64],
-                        double (*shp)[64], double (*shs)[64]) {
+                        double (*shp)[64], double (*shs)[64], const P2P* PP = nullptr,
+                        unsigned long long gen = 0) {
     // sh: W_s^T dc_f per slot, then the linearisation scratch; shp: trial point at the
     // landmark's first lane; shs: per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int s = 64 * w + lane;
@@ -2303,6 +2404,14 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w
         if (lane == 0)
 #pragma unroll
             for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
+        if (PP && lane < PP->nranks) {  // folded trial exchange: lane r pushes this wave's partial to rank r
+            const int par = (int)(gen & 1);
+            double* q = p2p_tval(PP->peer[lane], par, PP->rank, w);
+            q[0] = v[0]; q[1] = v[1]; q[2] = v[2]; q[3] = v[3];
+            __threadfence_system();
+            __hip_atomic_store(p2p_tflag(PP->peer[lane], par, PP->rank, w), gen, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     STAMP(21);
     RTSTAMP(8);
@@ -2315,6 +2424,19 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize(Geometry G, Prob Pr
     RTSTAMP(6);
     k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs);
     RTSTAMP(9);
+}
+
+// K6 of the P2P-sharded iteration with the trial-scalar exchange folded in (RSVIO_P2P_FOLD=2):
+// every wave also pushes its partial to every rank, tagged with this iteration's generation (the
+// one K5's exchange just used); the next decision (K4c or K7) sums them there
+__global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p(Geometry G, Prob Pr, Work Wk, P2P P,
+                                                                 const unsigned long long* xgen) {
+    __shared__ double sh[10][64];
+    __shared__ double shp[3][64];
+    __shared__ double shs[4][64];
+    unsigned long long gen = *xgen;
+    __asm__ volatile("" : "+s"(gen));  // loaded with the kernel's first loads, not at its end
+    k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs, &P, gen);
 }
 
 // K6r (sharded): this rank's trial scalars (|x|^2 of the poses on the owner rank) -> trial4,
@@ -2349,11 +2471,12 @@ constexpr int kK7Threads = 256;
 constexpr int kK7Blocks = RSVIO_K7_BLOCKS;
 __device__ __forceinline__ void lm_decide_body(const Geometry& G, const Prob& Pr, const Work& Wk, int pre_reduced,
                                                const LmArgs& la, LmState* host, unsigned long long* htick,
-                                               double* hout) {
+                                               double* hout, const P2P* PP = nullptr,
+                                               const unsigned long long* xgen = nullptr, int* err = nullptr) {
     STAMP(8);
     __shared__ LmState sd;
     if (threadIdx.x < 64) {  // the decision by wave 0 of every block
-        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la);
+        const LmState d = lm_decide(G, Pr, Wk, Wk.st_prev, pre_reduced, la, PP, xgen, err);
         if (threadIdx.x == 0) {
             sd = d;
             if (blockIdx.x == 0) {
@@ -2392,6 +2515,13 @@ __device__ __forceinline__ void lm_decide_body(const Geometry& G, const Prob& Pr
 __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, Work Wk, int pre_reduced, LmArgs la,
                                                            LmState* host, unsigned long long* htick, double* hout) {
     lm_decide_body(G, Pr, Wk, pre_reduced, la, host, htick, hout);
+}
+
+// K7 of the P2P-sharded solve with the folded trial exchange (RSVIO_P2P_FOLD=2)
+__global__ __launch_bounds__(kK7Threads) void ba_lm_decide_p2p(Geometry G, Prob Pr, Work Wk, LmArgs la, LmState* host,
+                                                               unsigned long long* htick, double* hout, P2P P,
+                                                               const unsigned long long* xgen, int* err) {
+    lm_decide_body(G, Pr, Wk, 2, la, host, htick, hout, &P, xgen, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2765,10 +2895,12 @@ struct BundleAdjuster {
     hipEvent_t ev_desc = nullptr;
     bool desc_pending = false;
     bool desc_mode() const { return desc_on && coll == 0 && k5_variant == 2 && G.n_free <= 10 && G.n_wave > 0; }
-    // the P2P-sharded iteration with the reduced system's exchange in K5's prologue (4 launches);
-    // RSVIO_P2P_FOLD=0: the separate exchange kernel X1 (5 launches, A/B switch)
-    bool fold_on = true;
-    bool p2p_fold() const { return fold_on && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
+    // the P2P-sharded iteration: RSVIO_P2P_FOLD=2 (default) 3 launches -- the reduced system's
+    // exchange in K5's prologue, the trial scalars pushed by K6's waves and summed by the next
+    // decision; 1: 4 launches (the trial scalars by X2); 0: 5 launches (X1 as its own kernel)
+    int fold_lvl = 2;
+    bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
+    bool p2p_fold2() const { return fold_lvl >= 2 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
     void fill_desc(WinDesc& d) const {
         d = WinDesc{};
@@ -2941,6 +3073,7 @@ struct BundleAdjuster {
     bool p2p_opened[kP2PMax] = {};
     DevBuf<int> d_p2p_err;
     DevBuf<unsigned long long> d_xgen;  // P2P exchange generation (advanced on the device)
+    DevBuf<int> d_xnw;                  // every rank's wave count (K5's exchange carries it)
 
     void init(const rsvio_ba_params& p) {
         P = p;
@@ -2955,8 +3088,8 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreateWithFlags(&gv.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
-        const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0": X1 as its own launch
-        fold_on = !(fv && fv[0] == '0');
+        const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0" / "1" / "2" (A/B switch)
+        if (fv && fv[0] >= '0' && fv[0] <= '2') fold_lvl = fv[0] - '0';
         const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
         desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
@@ -3222,6 +3355,8 @@ struct BundleAdjuster {
         int stride = 1;
         for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
         n_pad = (size_t)64 * n_wave;
+        if (coll == 2 && fold_lvl >= 2 && n_wave > kP2PWaves)  // (every rank must take the same path)
+            throw std::invalid_argument("shard exceeds the folded P2P trial exchange (16384 waves): RSVIO_P2P_FOLD=1");
         mark();
         // device-built part of the arena
         L.hdr = off;   off += al(sizeof(int4) * 2 * std::max<size_t>(n_pad, 1));
@@ -3370,9 +3505,13 @@ struct BundleAdjuster {
     void enqueue_iteration(const rsvio_lm_cfg& cfg, int it) {
         const Prob pr = prob();
         const Work wk = work(it);
-        if (p2p_fold()) {  // sharded over P2P, 4 launches: K4c, K5 with X1 folded in, K6, X2
-            hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
-                               lm_args(cfg), 1);
+        if (p2p_fold()) {  // sharded over P2P: K4c, K5 with X1 folded in, K6[, X2]
+            if (p2p_fold2())
+                hipLaunchKernelGGL(ba_schur_chunks_p2p, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
+                                   lm_args(cfg), p2p, d_xgen.p, d_p2p_err.p);
+            else
+                hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
+                                   lm_args(cfg), 1);
             RSVIO_HIP(hipGetLastError());
             switch (G.n_free) {
 #define RSVIO_CAMP(NF) \
@@ -3387,6 +3526,13 @@ struct BundleAdjuster {
         } else {
             enqueue_linear_system(it, lm_args(cfg), false);
             launch_camera_solve(pr, wk, sharded() ? 0 : 1);
+        }
+        if (p2p_fold2()) {  // K6 pushes its wave partials; the next decision sums them (no X2)
+            if (G.n_wave)
+                hipLaunchKernelGGL(ba_backsub_relinearize_p2p, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, p2p,
+                                   d_xgen.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
         }
         if (G.n_wave) hipLaunchKernelGGL(ba_backsub_relinearize, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk);
         RSVIO_HIP(hipGetLastError());
@@ -3403,6 +3549,13 @@ struct BundleAdjuster {
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
         // reads state copy it & 1 (the last iteration's pending trial), writes copy (it + 1) & 1
+        if (p2p_fold2()) {
+            hipLaunchKernelGGL(ba_lm_decide_p2p, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, G,
+                               prob(), work(it), lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr, p2p,
+                               d_xgen.p, d_p2p_err.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
         hipLaunchKernelGGL(ba_lm_decide, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, G, prob(),
                            work(it), sharded() ? 1 : 0, lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr);
         RSVIO_HIP(hipGetLastError());
@@ -3574,13 +3727,15 @@ struct BundleAdjuster {
     void p2p_export(int nr, hipIpcMemHandle_t* h) {
         if (nr < 1 || nr > kP2PMax) throw std::invalid_argument("P2P: 1..8 ranks");
         if (!xbuf) {
-            const size_t bytes = sizeof(double) * 2 * kP2PMax * kP2PMsg + sizeof(unsigned long long) * 2 * kP2PMax;
+            const size_t bytes = kP2PBytes;
             RSVIO_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&xbuf), bytes, hipDeviceMallocUncached));
             RSVIO_HIP(hipMemset(xbuf, 0, bytes));
             d_p2p_err.alloc(1);
             RSVIO_HIP(hipMemset(d_p2p_err.p, 0, sizeof(int)));
             d_xgen.alloc(1);
             RSVIO_HIP(hipMemset(d_xgen.p, 0, sizeof(unsigned long long)));
+            d_xnw.alloc(kP2PMax);
+            RSVIO_HIP(hipMemset(d_xnw.p, 0, sizeof(int) * kP2PMax));
         }
         RSVIO_HIP(hipIpcGetMemHandle(h, xbuf));
     }
@@ -3600,6 +3755,7 @@ struct BundleAdjuster {
         P2P P{};
         P.nranks = nr;
         P.rank = rk;
+        P.xnw = d_xnw.p;
         for (int r = 0; r < nr; ++r) {
             if (r == rk) {
                 P.peer[r] = xbuf;

@@ -55,6 +55,14 @@ class DeviceBackend:
         self.tracker.set_cameras(cameras[0], cameras[1])
         self.motion = MotionTracker(device, translation_threshold, rotation_threshold)
         self.solver = BundleAdjuster(max_keyframes=max(window, 2), device=device)
+        # motion tracking and the BA share one stream: PnP of frame t runs after BA(t - 1) was
+        # waited for and before BA(t) starts, so the stream is idle when it launches, and the
+        # process needs one stream fewer beside the tracker's (HIP maps streams onto 4 hardware
+        # queues per process; PnP queued on the tracker's queue waited behind frame t + 1)
+        from ._lib import CuStream
+        self._ba_stream = CuStream(device)
+        self.solver.set_stream(self._ba_stream.ptr)
+        self.motion.set_stream(self._ba_stream.ptr)
 
     def submit(self, left, right):
         """Enqueue a frame's tracking: host u8 arrays, or device-resident u8 tensors (data_ptr; no
@@ -83,7 +91,7 @@ class DeviceBackend:
         return r.status, r.is_keyframe, r.T_W_B, r.iterations, r.final_cost
 
     def close(self):
-        for o in (self.tracker, self.motion, self.solver):
+        for o in (self.tracker, self.motion, self.solver, self._ba_stream):
             o.close()
 
 

@@ -558,8 +558,9 @@ def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
 
 def test_sharded_p2p_weak_scaling_size_matches_oracle(gpu, oracle, tmp_path):
     """The weak-scaling configuration of the bench at N = 2: 2,000 landmarks per rank (4,000 in
-    all, 48,000 observations), the fused P2P path (K4c, K5 with the reduced system's exchange in
-    its prologue, K6, trial+exchange: 4 launches per LM iteration), against the oracle's single
+    all, 48,000 observations), the fused P2P path (K4c summing every rank's pushed trial
+    partials for the decision, K5 with the reduced system's exchange in its prologue, K6 pushing its
+    wave partials to every rank: 3 launches per LM iteration), against the oracle's single
     4,000-landmark solve within the config-3 tolerances."""
     import socket
 
@@ -729,14 +730,16 @@ def test_sharded_p2p_four_ranks_match_oracle(gpu, oracle, tmp_path):
     assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
 
 
-def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path):
-    """The 4-launch iteration (X1's exchange folded into K5's prologue) against the 5-launch one
-    (RSVIO_P2P_FOLD=0: X1 as its own kernel, K5 reading the exchanged system): the same sums in the
-    same order, so the 2-rank solves are bit-identical."""
+@pytest.mark.parametrize("level", ["1", "0"])
+def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level):
+    """The default 3-launch iteration (RSVIO_P2P_FOLD=2: the reduced system's exchange in K5's
+    prologue, the trial scalars pushed by K6's waves and summed by the next decision) against the
+    4-launch one (1: the trial scalars through X2) and the 5-launch one (0: X1 and X2 as kernels of
+    their own): the same sums in the same order, so the 2-rank solves are bit-identical."""
     (tmp_path / "a").mkdir()
     (tmp_path / "b").mkdir()
     fold = _run_p2p(2, 4000, tmp_path / "a")
-    sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": "0"})
+    sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": level})
     for a, b in zip(fold, sep):
         for k in ("pose", "pw", "res"):
             assert np.array_equal(a[k], b[k]), k
