@@ -1105,6 +1105,11 @@ def main():
     args = ap.parse_args()
     if args.same_device:
         args.collective = "p2p"
+        # ranks sharing one GPU: the 3-launch iteration's K4c (hundreds of workgroups waiting for
+        # every rank's K6 partials) can fill the shared CUs and starve the other rank's K6, so
+        # the rehearsal takes the 4-launch iteration (one single-workgroup exchange kernel X2);
+        # one rank per GPU -- the real layout -- runs the 3-launch one
+        os.environ.setdefault("RSVIO_P2P_FOLD", "1")
 
     world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:

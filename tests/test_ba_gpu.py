@@ -509,6 +509,10 @@ def _p2p_worker(rank, world, port, out_dir, n_lm=2000, env=None):
     import os
 
     import torch.distributed as dist
+    # ranks share this one GPU: the 4-launch iteration unless a test asks for another (the
+    # 3-launch one's K4c waits in hundreds of workgroups for every rank's K6, which on a shared
+    # device can starve a peer's K6 -- one rank per GPU never shares)
+    os.environ["RSVIO_P2P_FOLD"] = "1"
     os.environ.update(env or {})
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -558,9 +562,9 @@ def test_sharded_p2p_two_ranks_match_oracle(gpu, oracle, cfg3, tmp_path):
 
 def test_sharded_p2p_weak_scaling_size_matches_oracle(gpu, oracle, tmp_path):
     """The weak-scaling configuration of the bench at N = 2: 2,000 landmarks per rank (4,000 in
-    all, 48,000 observations), the fused P2P path (K4c summing every rank's pushed trial
-    partials for the decision, K5 with the reduced system's exchange in its prologue, K6 pushing its
-    wave partials to every rank: 3 launches per LM iteration), against the oracle's single
+    all, 48,000 observations), the fused P2P path (K4c, K5 with the reduced system's exchange in
+    its prologue, K6, X2 with the trial scalars' exchange: 4 launches per LM iteration -- the
+    3-launch one is checked bit for bit against it below), against the oracle's single
     4,000-landmark solve within the config-3 tolerances."""
     import socket
 
@@ -738,7 +742,7 @@ def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level):
     their own): the same sums in the same order, so the 2-rank solves are bit-identical."""
     (tmp_path / "a").mkdir()
     (tmp_path / "b").mkdir()
-    fold = _run_p2p(2, 4000, tmp_path / "a")
+    fold = _run_p2p(2, 4000, tmp_path / "a", env={"RSVIO_P2P_FOLD": "2"})
     sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": level})
     for a, b in zip(fold, sep):
         for k in ("pose", "pw", "res"):

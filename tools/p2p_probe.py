@@ -1,0 +1,51 @@
+"""GPU box (one GPU): the landmark-sharded BA alone, N ranks as N processes sharing cuda:0 (the
+P2P exchange over IPC-mapped buffers), each rank re-solving its 2,000-landmark shard of a
+config-3-per-rank window R times; prints per rank the device ms per LM iteration (the solve's
+device stamps) -- run it under rocprofv3 --kernel-trace --stats for the per-kernel split of the
+sharded iteration (K4c, K5, K6[, X1][, X2]) at each RSVIO_P2P_FOLD level.
+  python tools/p2p_probe.py [ranks] [repeats]"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "rs-vio_amd")]
+
+
+def worker(rank, world, port, reps):
+    import numpy as np
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rsvio import synthetic as S
+        from rsvio.ba import BundleAdjuster
+        shard = S.ba_problem(n_lm=2000 * world).shard(rank, world)
+        ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
+        handles = [None] * world
+        dist.all_gather_object(handles, ba.p2p_export(world))
+        ba.attach_p2p(world, rank, handles)
+        ba.set_problem_from(shard)
+        ms = []
+        for k in range(reps + 3):
+            r = ba.run()
+            if k >= 3:
+                ms.append(r.solve_ms / max(r.iterations, 1))
+        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '2')} status {r.status} it {r.iterations} "
+              f"ms/iter median {float(np.median(ms)):.4f} min {min(ms):.4f}", flush=True)
+        ba.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    import torch.multiprocessing as mp
+    world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(worker, args=(world, port, reps), nprocs=world, join=True, start_method="spawn")
