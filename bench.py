@@ -952,6 +952,13 @@ class BAWorkload:
         if world > 1:
             self.collective = self._attach(world, rank, collective, rccl_ok)
             log(f"[bench] rank {rank}: BA exchange = {self.collective}")
+        self.p2p_us = None
+        if self.collective == "p2p":
+            # the exchange's own latency (max over ranks): the 4 trial scalars and a reduced
+            # system of W=10 (1,600 doubles, 12.5 KB), 200 back-to-back exchanges each
+            self.p2p_us = {f"{n}_doubles": round(reduce_scalar(self.ba.p2p_latency_us(200, n), world, "max"), 2)
+                           for n in (4, 1600)}
+            log(f"[bench] rank {rank}: P2P exchange latency {self.p2p_us} us")
         if stream_ptr:
             self.ba.set_stream(stream_ptr)
         self.ba.set_problem_from(self.prob)
@@ -1105,11 +1112,10 @@ def main():
     args = ap.parse_args()
     if args.same_device:
         args.collective = "p2p"
-        # ranks sharing one GPU: the 3-launch iteration's K4c (hundreds of workgroups waiting for
-        # every rank's K6 partials) can fill the shared CUs and starve the other rank's K6, so
-        # the rehearsal takes the 4-launch iteration (one single-workgroup exchange kernel X2);
-        # one rank per GPU -- the real layout -- runs the 3-launch one
-        os.environ.setdefault("RSVIO_P2P_FOLD", "1")
+        # ranks sharing one GPU: never the 3-launch A/B iteration (RSVIO_P2P_FOLD=2), whose K4c
+        # (hundreds of workgroups waiting for every rank's K6 partials) can fill the shared CUs
+        # and starve the other rank's K6; the default 4-launch one
+        os.environ["RSVIO_P2P_FOLD"] = "1"
 
     world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:
@@ -1267,6 +1273,9 @@ def main():
                         "achieved_tflops": round(flops / (ba_ms_iter * 1e-3) / 1e12, 4),
                         "peak_tflops": FP64_PEAK_TFLOPS},
     }
+    if world > 1:
+        out["ba_exchange"] = {"collective": ba.collective, "p2p_latency_us": ba.p2p_us,
+                              "fold": os.environ.get("RSVIO_P2P_FOLD", "1") if ba.collective == "p2p" else None}
     if rank == 0 and not args.no_rows:
         out["rows"] = measure_rows(local, cpu=(world == 1 and not args.no_cpu))
     if rank == 0 and not args.no_rows and args.batch_streams > 0:

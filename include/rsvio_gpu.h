@@ -386,6 +386,10 @@ int rsvio_ba_attach_comm(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8
 int rsvio_ba_p2p_export(rsvio_ba* ba, int32_t nranks, uint8_t* handle_out, size_t cap);
 int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_t* handles);
 int rsvio_ba_detach_p2p(rsvio_ba* ba);
+/* Diagnostics (no reference counterpart): average device microseconds of one P2P exchange of n
+ * doubles (1 <= n <= 8192) over reps back-to-back exchanges after one warm-up; collective --
+ * every attached rank makes the same call.  Reported by bench.py at N > 1. */
+int rsvio_ba_p2p_latency(rsvio_ba* ba, int32_t reps, int32_t n, double* us_out);
 
 /* ===== B8: motion tracking (PnP) + keyframe rule (SlidingWindow::track_motion) ===== */
 

@@ -243,7 +243,15 @@ struct P2P {
 constexpr int kP2PWaves = 16384;  // waves per rank (a larger shard takes the X2 path)
 constexpr size_t kP2PTval = (size_t)2 * kP2PMax * kP2PMsg + 2 * kP2PMax;  // doubles before the trial values
 constexpr size_t kP2PTflag = kP2PTval + (size_t)2 * kP2PMax * kP2PWaves * 4;
-constexpr size_t kP2PBytes = sizeof(double) * (kP2PTflag + (size_t)2 * kP2PMax * kP2PWaves);
+// Small messages (n <= kP2PLLMax doubles: the trial scalars, the attach self-test) take the
+// flag-in-word protocol: every double travels as two 8-byte words {32 data bits, 32-bit
+// generation}, each an atomic store, so a reader knows a word has arrived when it carries the
+// exchange's generation -- no fence and no separate flag between the data and its readiness
+// (the flag protocol's writer waits for its data writes to be acknowledged before it may raise
+// the flag: one more xGMI round trip per exchange).  Per parity and source rank, 2 kP2PLLMax words.
+constexpr int kP2PLLMax = 16;
+constexpr size_t kP2PLL = kP2PTflag + (size_t)2 * kP2PMax * kP2PWaves;  // (in doubles / words)
+constexpr size_t kP2PBytes = sizeof(double) * (kP2PLL + (size_t)2 * kP2PMax * 2 * kP2PLLMax);
 
 __device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
     return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
@@ -259,6 +267,15 @@ __device__ __forceinline__ double* p2p_tval(double* xbuf, int par, int r, int w)
 }
 __device__ __forceinline__ unsigned long long* p2p_tflag(double* xbuf, int par, int r, int w) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PTflag) + ((size_t)par * kP2PMax + r) * kP2PWaves + w;
+}
+// flag-in-word slot [parity][source rank] (2 kP2PLLMax words)
+__device__ __forceinline__ unsigned long long* p2p_ll(double* xbuf, int par, int r) {
+    return reinterpret_cast<unsigned long long*>(xbuf + kP2PLL) + ((size_t)par * kP2PMax + r) * 2 * kP2PLLMax;
+}
+__device__ __forceinline__ void ll_put(unsigned long long* w, double v, unsigned g) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)g << 32;
+    __hip_atomic_store(w, (b & 0xffffffffull) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(w + 1, (b >> 32) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 
@@ -2577,9 +2594,13 @@ __global__ __launch_bounds__(kSchurThreads) void bab_schur_chunks(const WinDesc*
 template <int NF>
 __global__ __launch_bounds__(kK5Threads) void bab_camera_solve(const WinDesc* __restrict__ D, int wi) {
     const WinDesc& d = D[blockIdx.x];
-    const int skip = d.skip;
+    const int skip = d.skip, nkf = d.G.n_kf, nf = d.G.n_free, npb = d.G.n_pb, nw = d.G.n_wave;
     const Prob Pr = d.Pr;
     const Work& Wk = d.W[wi];
+    // the descriptor fields of the combine's first loads in one scalar round trip with the skip
+    // flag (the body read them on demand: a second round trip before the partial systems)
+    desc_touch(Pr.free_idx, Pr.dmap, Wk.pose[0], Wk.pose[1], Wk.cpart, Wk.partA, Wk.singular, Wk.st);
+    __asm__ volatile("" ::"s"(nkf), "s"(nf), "s"(npb), "s"(nw));
     if (skip) return;
     camera_solve_mfma_body<NF>(d.G, Pr, Wk, 1);
 }
@@ -2636,13 +2657,50 @@ __global__ __launch_bounds__(64) void bab_lm_decide(const WinDesc* __restrict__ 
 // host checks), and out[i] = the slots summed in rank order -- identical bits on every rank.
 // The generation lives in device memory (xgen, advanced by each exchange): every rank runs the
 // same exchange sequence, so the counters agree, and a captured graph replays correctly.
-__device__ void p2p_exchange(const double* msg, int n, const P2P& P, unsigned long long* xgen, int* err, double* out) {
+// gen_pre: this exchange's generation when the caller loaded the counter at its start (its
+// round trip then overlaps the caller's own loads); 0: loaded here.
+__device__ void p2p_exchange(const double* msg, int n, const P2P& P, unsigned long long* xgen, int* err, double* out,
+                             unsigned long long gen_pre = 0) {
     __shared__ unsigned long long sgen;
     const int tid = threadIdx.x, nr = P.nranks, me = P.rank;
-    if (tid == 0) sgen = *xgen + 1;
-    __syncthreads();
-    const unsigned long long gen = sgen;
+    if (!gen_pre) {
+        if (tid == 0) sgen = *xgen + 1;
+        __syncthreads();
+    }
+    const unsigned long long gen = gen_pre ? gen_pre : sgen;
     const int par = (int)(gen & 1);
+    if (n <= kP2PLLMax) {  // flag-in-word: thread (r, i) of the first nr * n pushes / polls one double
+        const unsigned g32 = (unsigned)gen;
+        const int r = tid / kP2PLLMax, i = tid % kP2PLLMax;
+        if (r < nr && i < n) ll_put(p2p_ll(P.peer[r], par, me) + 2 * i, msg[i], g32);
+        __shared__ double got[kP2PMax][kP2PLLMax];
+        if (r < nr && i < n) {
+            const unsigned long long* w = p2p_ll(P.peer[me], par, r) + 2 * i;
+            long long spins = 0;
+            for (;;) {
+                const unsigned long long a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned long long b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((unsigned)(a >> 32) == g32 && (unsigned)(b >> 32) == g32) {
+                    got[r][i] = __longlong_as_double((long long)((a & 0xffffffffull) | (b << 32)));
+                    break;
+                }
+                if (++spins > (1ll << 25)) {  // a peer never arrived: report, do not hang
+                    atomicExch(err, 1);
+                    got[r][i] = 0.0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        if (tid < n) {
+            double v = 0.0;
+            for (int q = 0; q < nr; ++q) v += got[q][tid];  // rank order: identical bits on every rank
+            out[tid] = v;
+        }
+        if (tid == 0) *xgen = gen;
+        return;
+    }
     for (int r = 0; r < nr; ++r) {
         double* dst = P.peer[r] + (size_t)(par * kP2PMax + me) * kP2PMsg;
         for (int i = tid; i < n; i += 256) dst[i] = msg[i];
@@ -2699,6 +2757,7 @@ __global__ __launch_bounds__(256) void ba_p2p_sys(Geometry G, Prob Pr, Work Wk, 
 __global__ __launch_bounds__(256) void ba_p2p_trial(Geometry G, Prob Pr, Work Wk, P2P P, unsigned long long* xgen,
                                                     int* err) {
     __shared__ double msg[4];
+    const unsigned long long gen = *xgen + 1;  // (with the state's load: one round trip for both)
     const LmState s = *Wk.st;
     if (s.done) return;
     if (threadIdx.x < 64) {
@@ -2708,7 +2767,7 @@ __global__ __launch_bounds__(256) void ba_p2p_trial(Geometry G, Prob Pr, Work Wk
             for (int k = 0; k < 4; ++k) msg[k] = v[k];
     }
     __syncthreads();
-    p2p_exchange(msg, 4, P, xgen, err, Wk.trial4);
+    p2p_exchange(msg, 4, P, xgen, err, Wk.trial4, gen);
 }
 
 }  // namespace
@@ -2895,10 +2954,12 @@ struct BundleAdjuster {
     hipEvent_t ev_desc = nullptr;
     bool desc_pending = false;
     bool desc_mode() const { return desc_on && coll == 0 && k5_variant == 2 && G.n_free <= 10 && G.n_wave > 0; }
-    // the P2P-sharded iteration: RSVIO_P2P_FOLD=2 (default) 3 launches -- the reduced system's
-    // exchange in K5's prologue, the trial scalars pushed by K6's waves and summed by the next
-    // decision; 1: 4 launches (the trial scalars by X2); 0: 5 launches (X1 as its own kernel)
-    int fold_lvl = 2;
+    // the P2P-sharded iteration: RSVIO_P2P_FOLD=1 (default) 4 launches -- the reduced system's
+    // exchange in K5's prologue, the trial scalars by X2; 2: 3 launches (the trial scalars pushed
+    // by K6's waves and summed by the next decision: measured 10.6 us per iteration slower on one
+    // rank, every K4c block's decision then polling every wave's partial of every rank,
+    // profiles/r04k_p2p_fold_kstats.txt); 0: 5 launches (X1 as its own kernel)
+    int fold_lvl = 1;
     bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
     bool p2p_fold2() const { return fold_lvl >= 2 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
@@ -3095,6 +3156,8 @@ struct BundleAdjuster {
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
         graph_update = !(gu && gu[0] == '0');
         h_state.alloc(1, hipHostMallocCoherent);  // read on the decision's ticket (wait_tick)
+        // (coarse-grained host memory, the stores gathered in L2 and written back whole by K7's
+        // system-scope release, measured the same: profiles/r04k_ab_multi.txt)
         h_out.alloc((size_t)7 * P.max_keyframes + (size_t)3 * P.max_landmarks, hipHostMallocCoherent);
         d_tick.alloc(2);
         RSVIO_HIP(hipMemset(d_tick.p, 0, 2 * sizeof(unsigned long long)));
@@ -3785,6 +3848,33 @@ struct BundleAdjuster {
         drop_graph();  // the iteration's launch sequence changes with the collective
     }
 
+    // measured exchange latency: one warm-up exchange (absorbs the ranks' start skew), then reps
+    // back-to-back exchanges of n doubles timed with events on this handle's stream; every rank
+    // must make the same call.  Average device microseconds per exchange.
+    double p2p_latency(int reps, int n) {
+        require_idle("rsvio_ba_p2p_latency");
+        if (coll != 2) throw CallOrderError("P2P latency: the P2P exchange is not attached");
+        if (reps < 1 || n < 1 || n > kP2PMsg) throw std::invalid_argument("P2P latency: bad reps or size");
+        DevBuf<double> t(n);
+        RSVIO_HIP(hipMemsetAsync(t.p, 0, (size_t)n * sizeof(double), stream));
+        hipEvent_t a, b;
+        RSVIO_HIP(hipEventCreate(&a));
+        RSVIO_HIP(hipEventCreate(&b));
+        for (int k = 0; k <= reps; ++k) {
+            if (k == 1) RSVIO_HIP(hipEventRecord(a, stream));
+            hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, n, p2p, d_xgen.p, d_p2p_err.p);
+        }
+        RSVIO_HIP(hipGetLastError());
+        RSVIO_HIP(hipEventRecord(b, stream));
+        RSVIO_HIP(hipEventSynchronize(b));
+        float ms = 0.f;
+        RSVIO_HIP(hipEventElapsedTime(&ms, a, b));
+        RSVIO_HIP(hipEventDestroy(a));
+        RSVIO_HIP(hipEventDestroy(b));
+        p2p_check();
+        return 1e3 * (double)ms / reps;
+    }
+
     void p2p_detach() {
         require_idle("rsvio_ba_detach_p2p");
         if (coll == 2) coll = comm ? 1 : 0;
@@ -4310,6 +4400,14 @@ int rsvio_ba_attach_p2p(rsvio_ba* ba, int32_t nranks, int32_t rank, const uint8_
             rsvio::set_last_error(std::string("P2P attach failed: ") + e.what());
             return (int)RSVIO_ERR_RCCL;
         }
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_p2p_latency(rsvio_ba* ba, int32_t reps, int32_t n, double* us_out) {
+    if (!ba || !us_out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        *us_out = ba->b.p2p_latency(reps, n);
         return (int)RSVIO_OK;
     });
 }

@@ -85,6 +85,13 @@ class BundleAdjuster:
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         check(_lib.load().rsvio_ba_attach_p2p(self._h, nranks, rank, buf))
 
+    def p2p_latency_us(self, reps: int = 200, n: int = 4) -> float:
+        """Average device microseconds of one P2P exchange of n doubles (collective: every
+        attached rank calls it with the same arguments)."""
+        us = C.c_double(0.0)
+        check(_lib.load().rsvio_ba_p2p_latency(self._h, reps, n, C.byref(us)))
+        return us.value
+
     def detach_p2p(self) -> None:
         check(_lib.load().rsvio_ba_detach_p2p(self._h))
 

@@ -27,13 +27,15 @@ def worker(rank, world, port, reps):
         handles = [None] * world
         dist.all_gather_object(handles, ba.p2p_export(world))
         ba.attach_p2p(world, rank, handles)
+        lat = {n: ba.p2p_latency_us(200, n) for n in (4, 1600)}
+        print(f"rank {rank}: exchange latency us {lat}", flush=True)
         ba.set_problem_from(shard)
         ms = []
         for k in range(reps + 3):
             r = ba.run()
             if k >= 3:
                 ms.append(r.solve_ms / max(r.iterations, 1))
-        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '2')} status {r.status} it {r.iterations} "
+        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '1')} status {r.status} it {r.iterations} "
               f"ms/iter median {float(np.median(ms)):.4f} min {min(ms):.4f}", flush=True)
         ba.close()
         dist.barrier()

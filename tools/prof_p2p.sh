@@ -6,7 +6,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-x}
-for cfg in "1 2" "2 2" "2 1" "2 0"; do
+# CFGS: "ranks fold" pairs (default: the single-rank fold-2 reference, then 2 ranks at each level)
+CFGS=${CFGS:-"1:2 2:2 2:1 2:0"}
+for cfg in $CFGS; do
+  cfg=${cfg/:/ }
   set -- $cfg
   R=$1; F=$2
   D=gpurun_out/p2pprof_${TAG}_r${R}_f${F}
