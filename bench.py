@@ -550,7 +550,8 @@ def measure_ft_row(device: int, cpu: bool, reps: int = 60):
            "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 6), "algorithmic_bytes_per_frame": byts,
                         "note": "whole frame (pyramid + LK + Shi-Tomasi); latency-bound: serial LK chains "
-                                "and fast_blur's sequential running sums (profiles/r01_ft_kernel_stats.csv)"}}
+                                "(ft_lk_kernel 254 us of 0.56 ms per frame) and fast_blur's sequential running "
+                                "sums (ft_boxblur_half 6 x 23 us) -- profiles/r04m_ft_kstats.txt"}}
     if cpu:
         from oracle import oracle as O
         ref = O.FeatureTracker(W, H)
