@@ -1339,7 +1339,9 @@ __device__ void k5_finish(const Geometry& G, const Work& Wk, double* A, double x
         Wk.dc[lane] = x;
         A[lane] = x;
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    // the LDS copy visible to the wave (lgkmcnt only: waiting for the dc store's acknowledgement
+    // as well, s_waitcnt 0, put a memory round trip before the trial poses)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     STAMP(4);
     if (lane < G.n_kf) {  // trial poses from the prefetched current poses
@@ -1946,10 +1948,10 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     }
     __syncthreads();
     STAMP(1);
-    if (tid == 0) {
-        fail |= *Wk.singular;
-        *Wk.singular = 0;
-    }
+    // the singular flag of this iteration's K4c is already in fail (combine_mapped / combine_p2p
+    // load it with the partial systems; the sys path's K4d / X1 carried it and cleared it): only
+    // its reset for the next iteration here (re-reading it cost a round trip on the chain)
+    if (tid == 0) *Wk.singular = 0;
     const double gcl_v = (wave == 0 && lane < n) ? gsh[lane] : 0.0;
     __syncthreads();
     STAMP(2);
@@ -2261,7 +2263,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
             dcs[i] = x[q];
         }
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the LDS copy (not the dc store's acknowledgement)
     __builtin_amdgcn_wave_barrier();
     if (lane < G.n_kf) {
         double* qd = Wk.pose[1 - st->cur] + 7 * lane;
@@ -2570,6 +2572,7 @@ template <class... T>
 __device__ __forceinline__ void desc_touch(const T*... p) {
     (desc_touch1(p), ...);
 }
+
 
 __global__ __launch_bounds__(64) void bab_linearize(const WinDesc* __restrict__ D, double lambda0) {
     const WinDesc& d = D[blockIdx.y];
