@@ -12,10 +12,14 @@ HEAD="bench.py --steps 20 --warmup 5 --no-cpu --no-rows --pipeline-frames 0"
 for rep in $(seq 1 $REPS); do
   for spec in "$@"; do
     name=${spec%%=*}; envs=${spec#*=}
-    E=""
-    [ "$envs" != "-" ] && E=$(echo "$envs" | tr ',' ' ')
+    E=""; A=""
+    case "$envs" in
+      -) ;;
+      args:*) A=$(echo "${envs#args:}" | tr ',' ' ') ;;   # bench.py arguments, e.g. args:--order,lookahead
+      *) E=$(echo "$envs" | tr ',' ' ') ;;
+    esac
     out=gpurun_out/abm_${TAG}_${name}_${rep}
-    env $E timeout -k 10 240 python $HEAD > $out.json 2> $out.err || { tail -20 $out.err; exit 1; }
+    env $E timeout -k 10 240 python $HEAD $A > $out.json 2> $out.err || { tail -20 $out.err; exit 1; }
     python3 - $out.json $name <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
