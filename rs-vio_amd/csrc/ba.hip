@@ -235,6 +235,7 @@ struct P2P {
     double* peer[kP2PMax];       // exchange buffer of each rank (own one included)
     int nranks, rank;
     int* xnw;                    // (local) every rank's wave count, as K5's exchange carried it
+    int ll;                      // K5's system exchange flag-in-word (RSVIO_P2P_LL=1, A/B) instead of data + flags
 };
 
 // The trial-scalar exchange folded into K6 and the next decision (RSVIO_P2P_FOLD=2): after the
@@ -251,7 +252,9 @@ constexpr size_t kP2PTflag = kP2PTval + (size_t)2 * kP2PMax * kP2PWaves * 4;
 // the flag: one more xGMI round trip per exchange).  Per parity and source rank, 2 kP2PLLMax words.
 constexpr int kP2PLLMax = 16;
 constexpr size_t kP2PLL = kP2PTflag + (size_t)2 * kP2PMax * kP2PWaves;  // (in doubles / words)
-constexpr size_t kP2PBytes = sizeof(double) * (kP2PLL + (size_t)2 * kP2PMax * 2 * kP2PLLMax);
+// K5's system exchange in flag-in-word form (A/B): per parity and source rank 2 kP2PMsg words
+constexpr size_t kP2PLLSys = kP2PLL + (size_t)2 * kP2PMax * 2 * kP2PLLMax;
+constexpr size_t kP2PBytes = sizeof(double) * (kP2PLLSys + (size_t)2 * kP2PMax * 2 * kP2PMsg);
 
 __device__ __forceinline__ unsigned long long* p2p_flags(double* xbuf) {
     return reinterpret_cast<unsigned long long*>(xbuf + (size_t)2 * kP2PMax * kP2PMsg);
@@ -268,9 +271,28 @@ __device__ __forceinline__ double* p2p_tval(double* xbuf, int par, int r, int w)
 __device__ __forceinline__ unsigned long long* p2p_tflag(double* xbuf, int par, int r, int w) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PTflag) + ((size_t)par * kP2PMax + r) * kP2PWaves + w;
 }
+// One value of every rank's slot, summed in rank order (identical bits on every rank): the
+// nranks loads are issued together (a clamped index past nranks, its value not added), so the
+// sum costs one round trip to the exchange buffer, not one per rank -- a runtime rank loop of
+// load + add put a full wait on every load (nranks round trips per value; at 4 ranks that was
+// the largest part of K5's exchange).
+__device__ __forceinline__ void p2p_rank_sum(const double* mine, int nr, int e, double& acc) {
+    double v[kP2PMax];
+#pragma unroll
+    for (int r = 0; r < kP2PMax; ++r)
+        v[r] = __hip_atomic_load(mine + (size_t)min(r, nr - 1) * kP2PMsg + e, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int r = 0; r < kP2PMax; ++r)
+        if (r < nr) acc += v[r];
+}
+
 // flag-in-word slot [parity][source rank] (2 kP2PLLMax words)
 __device__ __forceinline__ unsigned long long* p2p_ll(double* xbuf, int par, int r) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PLL) + ((size_t)par * kP2PMax + r) * 2 * kP2PLLMax;
+}
+__device__ __forceinline__ unsigned long long* p2p_llsys(double* xbuf, int par, int r) {
+    return reinterpret_cast<unsigned long long*>(xbuf + kP2PLLSys) + ((size_t)par * kP2PMax + r) * 2 * kP2PMsg;
 }
 __device__ __forceinline__ void ll_put(unsigned long long* w, double v, unsigned g) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)g << 32;
@@ -1656,6 +1678,135 @@ __device__ bool combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
     return false;
 }
 
+// combine_p2p's exchange in flag-in-word form (RSVIO_P2P_LL=1, A/B): every entry (and the three
+// scalars: initial cost, singular flag, wave count) goes to every rank as two tagged 8-byte words
+// -- no fence, no flags -- and the reader polls the words themselves, every rank's words of its
+// entries in flight together (ranks in two groups of 4), re-reading until all carry this
+// exchange's tag.  Same sums in the same rank order as the flag protocol: the same bits.
+template <int NF>
+__device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, double* gsh, int* fail, const P2P& P,
+                               unsigned long long* xgen, int* err,
+                               const double (&v)[((NF * (NF + 1) / 2) * 36 + 12 * NF + kK5Threads - 1) / kK5Threads][kGrp],
+                               const int (&dst)[((NF * (NF + 1) / 2) * 36 + 12 * NF + kK5Threads - 1) / kK5Threads],
+                               const double (&pa)[16], int sing, double lambda, unsigned long long gen) {
+    constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
+    constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
+    const int ne = G.n_pb * 36 + 12 * G.n_free;
+    const int tid = threadIdx.x, nr = P.nranks, me = P.rank, par = (int)(gen & 1);
+    const unsigned g32 = (unsigned)gen;
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= ne) break;
+        double a = v[i][0];
+#pragma unroll
+        for (int x = 1; x < kGrp; ++x) a += v[i][x];
+        if (me == 0 && dst[i] >= 0 && (dst[i] & kMfMapLambda)) a += lambda;
+        for (int r = 0; r < nr; ++r) ll_put(p2p_llsys(P.peer[r], par, me) + 2 * (size_t)e, a, g32);
+    }
+    if (tid < 64) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+        c = wave_sum_det(c);
+        if (tid < nr) {  // lane r pushes the scalars to rank r
+            unsigned long long* d = p2p_llsys(P.peer[tid], par, me) + 2 * (size_t)ne;
+            ll_put(d, c, g32);
+            ll_put(d + 2, sing ? 1.0 : 0.0, g32);
+            ll_put(d + 4, (double)G.n_wave, g32);
+        }
+    }
+    // entries: every rank's two words of this thread's entries, ranks in groups of 4
+    const unsigned long long* mine = p2p_llsys(P.peer[me], par, 0);
+    double acc[kE];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) acc[i] = 0.0;
+    bool late = false;
+#pragma unroll
+    for (int r0 = 0; r0 < kP2PMax; r0 += 4) {
+        if (r0 >= nr) break;
+        unsigned long long w[kE][4][2];
+        long long spins = 0;
+        for (;;) {
+#pragma unroll
+            for (int i = 0; i < kE; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned long long* a =
+                        mine + (size_t)min(r0 + q, nr - 1) * 2 * kP2PMsg + 2 * (size_t)min(tid + T * i, ne - 1);
+                    w[i][q][0] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    w[i][q][1] = __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < kE; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    ok &= (unsigned)(w[i][q][0] >> 32) == g32 && (unsigned)(w[i][q][1] >> 32) == g32;
+            if (ok) break;
+            if (++spins > (1ll << 25)) {
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int i = 0; i < kE; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (r0 + q < nr)
+                    acc[i] += __longlong_as_double((long long)((w[i][q][0] & 0xffffffffull) | (w[i][q][1] << 32)));
+    }
+    if (late) atomicExch(err, 1);
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= ne) break;
+        const int d = dst[i];
+        if (d >= 0)
+            M[d & (kMfMapLambda - 1)] = acc[i];
+        else if (d <= -2)
+            gsh[-2 - d] = acc[i];
+    }
+    // scalars: lane r of wave 0 reads rank r's three; the sums in rank order by lane 0
+    __shared__ double sc[kP2PMax][3];
+    if (tid < nr) {
+        const unsigned long long* a = mine + (size_t)tid * 2 * kP2PMsg + 2 * (size_t)ne;
+        unsigned long long ws[6];
+        long long spins = 0;
+        for (;;) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) ws[k] = __hip_atomic_load(a + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) ok &= (unsigned)(ws[k] >> 32) == g32;
+            if (ok) break;
+            if (++spins > (1ll << 25)) {
+                atomicExch(err, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            sc[tid][k] = __longlong_as_double((long long)((ws[2 * k] & 0xffffffffull) | (ws[2 * k + 1] << 32)));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double c = 0.0, f = 0.0;
+        for (int r = 0; r < nr; ++r) {
+            c += sc[r][0];
+            f += sc[r][1];
+        }
+        Wk.sys[ne] = c;  // the decision of iteration 0 reads the (all-reduced) initial cost here
+        *fail = f != 0.0;
+        *xgen = gen;
+    }
+    if (tid < nr && P.xnw) P.xnw[tid] = (int)sc[tid][2];
+    return false;
+}
+
 // combine_mapped for the landmark-sharded path over the P2P exchange (X1 folded into K5): this
 // rank's reduced system is summed from its partials as combine_mapped does (+ lambda on rank 0,
 // after the sum, as K4d), each entry pushed from its register into slot [parity][rank] of every
@@ -1700,6 +1851,7 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     __syncthreads();  // sgen
     const unsigned long long gen = sgen;
     const int par = (int)(gen & 1);
+    if (P.ll) return combine_p2p_ll<NF>(G, Wk, M, gsh, fail, P, xgen, err, v, dst, pa, sing, lambda, gen);
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
@@ -1741,13 +1893,31 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     }
     __syncthreads();
     const double* mine = p2p_slot(P.peer[me], par, 0);
+    // every value of this thread from every rank in flight together (clamped indices; only real
+    // entries of real ranks are added), then the rank-ordered sums
+    double sums[kE];
+    {
+        double v[kE][kP2PMax];
+#pragma unroll
+        for (int i = 0; i < kE; ++i)
+#pragma unroll
+            for (int r = 0; r < kP2PMax; ++r)
+                v[i][r] = __hip_atomic_load(mine + (size_t)min(r, nr - 1) * kP2PMsg + min(tid + T * i, ne - 1),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int i = 0; i < kE; ++i) {
+            double a = 0.0;
+#pragma unroll
+            for (int r = 0; r < kP2PMax; ++r)
+                if (r < nr) a += v[i][r];
+            sums[i] = a;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
         if (e >= ne) break;
-        double a = 0.0;
-        for (int r = 0; r < nr; ++r)
-            a += __hip_atomic_load(mine + (size_t)r * kP2PMsg + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const double a = sums[i];
         const int d = dst[i];
         if (d >= 0)
             M[d & (kMfMapLambda - 1)] = a;
@@ -1756,10 +1926,8 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     }
     if (tid == 0) {
         double c = 0.0, f = 0.0;
-        for (int r = 0; r < nr; ++r) {
-            c += __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            f += __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        p2p_rank_sum(mine, nr, ne, c);
+        p2p_rank_sum(mine, nr, ne + 1, f);
         Wk.sys[ne] = c;  // the decision of iteration 0 reads the (all-reduced) initial cost here
         *fail = f != 0.0;
         *xgen = gen;
@@ -2726,11 +2894,22 @@ __device__ void p2p_exchange(const double* msg, int n, const P2P& P, unsigned lo
     }
     __syncthreads();
     const double* mine = P.peer[me] + (size_t)(par * kP2PMax) * kP2PMsg;
-    for (int i = tid; i < n; i += 256) {
-        double v = 0.0;
-        for (int r = 0; r < nr; ++r)
-            v += __hip_atomic_load(mine + (size_t)r * kP2PMsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        out[i] = v;
+    for (int i0 = tid; i0 < n; i0 += 4 * 256) {  // 4 values x every rank in flight per round
+        double v[4][kP2PMax];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < kP2PMax; ++r)
+                v[q][r] = __hip_atomic_load(mine + (size_t)min(r, nr - 1) * kP2PMsg + min(i0 + 256 * q, n - 1),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double a = 0.0;
+#pragma unroll
+            for (int r = 0; r < kP2PMax; ++r)
+                if (r < nr) a += v[q][r];
+            if (i0 + 256 * q < n) out[i0 + 256 * q] = a;
+        }
     }
     if (tid == 0) *xgen = gen;
 }
@@ -3822,6 +4001,8 @@ struct BundleAdjuster {
         P.nranks = nr;
         P.rank = rk;
         P.xnw = d_xnw.p;
+        const char* llv = std::getenv("RSVIO_P2P_LL");  // "1": K5's system exchange flag-in-word (A/B)
+        P.ll = llv && llv[0] == '1';
         for (int r = 0; r < nr; ++r) {
             if (r == rk) {
                 P.peer[r] = xbuf;

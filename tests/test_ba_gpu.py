@@ -748,3 +748,18 @@ def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level):
     for a, b in zip(fold, sep):
         for k in ("pose", "pw", "res"):
             assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_p2p_flag_in_word_equals_flag_protocol(gpu, tmp_path, world):
+    """K5's system exchange in flag-in-word form (RSVIO_P2P_LL=1: every entry as two tagged 8-byte
+    words, the reader polling the words, no fence and no flags) against the data + flags
+    protocol: the same sums in the same rank order, so the solves are bit-identical on every
+    rank (2 and 4 ranks sharing the GPU)."""
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    ll = _run_p2p(world, 2000 * world, tmp_path / "a", env={"RSVIO_P2P_LL": "1"})
+    fl = _run_p2p(world, 2000 * world, tmp_path / "b")
+    for a, b in zip(ll, fl):
+        for k in ("pose", "pw", "res"):
+            assert np.array_equal(a[k], b[k]), k

@@ -35,7 +35,7 @@ def worker(rank, world, port, reps):
             r = ba.run()
             if k >= 3:
                 ms.append(r.solve_ms / max(r.iterations, 1))
-        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '1')} status {r.status} it {r.iterations} "
+        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '1')} ll {os.environ.get('RSVIO_P2P_LL', '0')} status {r.status} it {r.iterations} "
               f"ms/iter median {float(np.median(ms)):.4f} min {min(ms):.4f}", flush=True)
         ba.close()
         dist.barrier()
