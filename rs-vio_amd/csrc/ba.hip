@@ -287,6 +287,26 @@ __device__ __forceinline__ void p2p_rank_sum(const double* mine, int nr, int e, 
         if (r < nr) acc += v[r];
 }
 
+// sums[i] += every rank's entry tid + T i, in rank order: ranks in groups of W whose loads are in
+// flight together (a clamped index past the last rank, not added)
+template <int KE, int W>
+__device__ __forceinline__ void p2p_group_sums(const double* mine, int nr, int ne, int tid, int T, double (&sums)[KE]) {
+    for (int r0 = 0; r0 < nr; r0 += W) {
+        double v[KE][W];
+#pragma unroll
+        for (int i = 0; i < KE; ++i)
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                v[i][q] = __hip_atomic_load(mine + (size_t)min(r0 + q, nr - 1) * kP2PMsg + min(tid + T * i, ne - 1),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int i = 0; i < KE; ++i)
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (r0 + q < nr) sums[i] += v[i][q];
+    }
+}
+
 // flag-in-word slot [parity][source rank] (2 kP2PLLMax words)
 __device__ __forceinline__ unsigned long long* p2p_ll(double* xbuf, int par, int r) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PLL) + ((size_t)par * kP2PMax + r) * 2 * kP2PLLMax;
@@ -294,6 +314,47 @@ __device__ __forceinline__ unsigned long long* p2p_ll(double* xbuf, int par, int
 __device__ __forceinline__ unsigned long long* p2p_llsys(double* xbuf, int par, int r) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PLLSys) + ((size_t)par * kP2PMax + r) * 2 * kP2PMsg;
 }
+// acc[i] += every rank's tagged entry tid + T i, in rank order: ranks in groups of W, each group's
+// words polled together until all carry tag g; true if a peer never arrived (bounded)
+template <int KE, int W>
+__device__ __forceinline__ bool ll_group_sums(const unsigned long long* mine, int nr, int ne, int tid, int T,
+                                              unsigned g, double (&acc)[KE]) {
+    bool late = false;
+    for (int r0 = 0; r0 < nr; r0 += W) {
+        unsigned long long w[KE][W][2];
+        long long spins = 0;
+        for (;;) {
+#pragma unroll
+            for (int i = 0; i < KE; ++i)
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    const unsigned long long* a =
+                        mine + (size_t)min(r0 + q, nr - 1) * 2 * kP2PMsg + 2 * (size_t)min(tid + T * i, ne - 1);
+                    w[i][q][0] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    w[i][q][1] = __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < KE; ++i)
+#pragma unroll
+                for (int q = 0; q < W; ++q) ok &= (unsigned)(w[i][q][0] >> 32) == g && (unsigned)(w[i][q][1] >> 32) == g;
+            if (ok) break;
+            if (++spins > (1ll << 25)) {
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int i = 0; i < KE; ++i)
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (r0 + q < nr)
+                    acc[i] += __longlong_as_double((long long)((w[i][q][0] & 0xffffffffull) | (w[i][q][1] << 32)));
+    }
+    return late;
+}
+
 __device__ __forceinline__ void ll_put(unsigned long long* w, double v, unsigned g) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)g << 32;
     __hip_atomic_store(w, (b & 0xffffffffull) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1717,47 +1778,13 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
             ll_put(d + 4, (double)G.n_wave, g32);
         }
     }
-    // entries: every rank's two words of this thread's entries, ranks in groups of 4
+    // entries: every rank's two words of this thread's entries, ranks in groups of 2 or 4
     const unsigned long long* mine = p2p_llsys(P.peer[me], par, 0);
     double acc[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) acc[i] = 0.0;
-    bool late = false;
-#pragma unroll
-    for (int r0 = 0; r0 < kP2PMax; r0 += 4) {
-        if (r0 >= nr) break;
-        unsigned long long w[kE][4][2];
-        long long spins = 0;
-        for (;;) {
-#pragma unroll
-            for (int i = 0; i < kE; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const unsigned long long* a =
-                        mine + (size_t)min(r0 + q, nr - 1) * 2 * kP2PMsg + 2 * (size_t)min(tid + T * i, ne - 1);
-                    w[i][q][0] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    w[i][q][1] = __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            bool ok = true;
-#pragma unroll
-            for (int i = 0; i < kE; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    ok &= (unsigned)(w[i][q][0] >> 32) == g32 && (unsigned)(w[i][q][1] >> 32) == g32;
-            if (ok) break;
-            if (++spins > (1ll << 25)) {
-                late = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int i = 0; i < kE; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (r0 + q < nr)
-                    acc[i] += __longlong_as_double((long long)((w[i][q][0] & 0xffffffffull) | (w[i][q][1] << 32)));
-    }
+    const bool late = nr <= 2 ? ll_group_sums<kE, 2>(mine, nr, ne, tid, T, g32, acc)
+                              : ll_group_sums<kE, 4>(mine, nr, ne, tid, T, g32, acc);
     if (late) atomicExch(err, 1);
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
@@ -1893,26 +1920,16 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     }
     __syncthreads();
     const double* mine = p2p_slot(P.peer[me], par, 0);
-    // every value of this thread from every rank in flight together (clamped indices; only real
-    // entries of real ranks are added), then the rank-ordered sums
+    // this thread's values from a group of ranks in flight together (clamped indices; only real
+    // entries of real ranks are added), groups in rank order: one round trip per group of 2 (two
+    // ranks) or 4 ranks, then the rank-ordered sums
     double sums[kE];
-    {
-        double v[kE][kP2PMax];
 #pragma unroll
-        for (int i = 0; i < kE; ++i)
-#pragma unroll
-            for (int r = 0; r < kP2PMax; ++r)
-                v[i][r] = __hip_atomic_load(mine + (size_t)min(r, nr - 1) * kP2PMsg + min(tid + T * i, ne - 1),
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-        for (int i = 0; i < kE; ++i) {
-            double a = 0.0;
-#pragma unroll
-            for (int r = 0; r < kP2PMax; ++r)
-                if (r < nr) a += v[i][r];
-            sums[i] = a;
-        }
-    }
+    for (int i = 0; i < kE; ++i) sums[i] = 0.0;
+    if (nr <= 2)
+        p2p_group_sums<kE, 2>(mine, nr, ne, tid, T, sums);
+    else
+        p2p_group_sums<kE, 4>(mine, nr, ne, tid, T, sums);
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
