@@ -1276,7 +1276,9 @@ def main():
     }
     if world > 1:
         out["ba_exchange"] = {"collective": ba.collective, "p2p_latency_us": ba.p2p_us,
-                              "fold": os.environ.get("RSVIO_P2P_FOLD", "1") if ba.collective == "p2p" else None}
+                              "fold": os.environ.get("RSVIO_P2P_FOLD", "1") if ba.collective == "p2p" else None,
+                              "flag_in_word_system": os.environ.get("RSVIO_P2P_LL", "0") == "1"
+                              if ba.collective == "p2p" else None}
     if rank == 0 and not args.no_rows:
         out["rows"] = measure_rows(local, cpu=(world == 1 and not args.no_cpu))
     if rank == 0 and not args.no_rows and args.batch_streams > 0:
