@@ -432,7 +432,6 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         from oracle import oracle as O
         from oracle.estimator import OracleBackend, outcome_difference
         host = [(l.cpu().numpy(), r.cpu().numpy()) for l, r in s.frames]
-        pnp_tail = []
 
         def oracle_leg(threads, budget_s, compare):
             """The same Estimator host logic over the oracle backend: `threads` = 1 sequential,
@@ -452,10 +451,7 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
                         rd = out[k]
                         d = float(np.abs(rd.T_W_B - ro.T_W_B).max())
                         maxd = max(maxd, d)
-                        diff = outcome_difference(rd, ro)
-                        if diff == "pnp_tail":
-                            pnp_tail.append(k)
-                        if first is None and (d > 1e-6 or diff not in (None, "pnp_tail")):
+                        if first is None and (d > 1e-6 or outcome_difference(rd, ro) is not None):
                             first = k
                     k += 1
             finally:
@@ -470,10 +466,8 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
         row["gpu_max_position_error_m_same_frames"] = round(gerr_k, 5)
         row["first_divergent_frame"] = first
         row["max_pose_diff_vs_oracle"] = maxd
-        row["parity_checks"] = ("per frame: keyframe flag and BA status + LM iterations exactly; PnP status + LM "
-                                "iterations exactly except in the converged tail (both succeed, final costs equal "
-                                "to 1e-12: oracle/estimator.py outcome_difference); T_W_B within 1e-6")
-        row["pnp_converged_tail_frames"] = pnp_tail
+        row["parity_checks"] = ("per frame: keyframe flag, PnP status + LM iterations and BA status + LM "
+                                "iterations exactly (oracle/estimator.py outcome_difference); T_W_B within 1e-6")
         row["parity"] = "ok" if first is None else "failed"
         if first is not None:  # a number whose outputs differ from the reference path's is no result
             row["value_unchecked"] = row["value"]
@@ -980,38 +974,7 @@ class BAWorkload:
     def _attach(self, world, rank, collective, rccl_ok):
         """RCCL communicator first (the fallback), then the P2P one-shot all-reduce when every rank
         can map every peer's exchange buffer; all ranks agree on the outcome."""
-        import torch.distributed as dist
-        from rsvio.ba import BundleAdjuster
-        have_rccl = False
-        if collective in ("auto", "rccl") and rccl_ok:
-            obj = [BundleAdjuster.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            self.ba.attach_comm(world, rank, obj[0])
-            have_rccl = True
-        if collective == "rccl":
-            return "rccl"
-        mine = None
-        try:
-            mine = self.ba.p2p_export(world)
-        except Exception as e:  # noqa: BLE001 - reported, then agreed on below
-            log(f"[bench] rank {rank}: p2p export failed: {e}")
-        handles = [None] * world
-        dist.all_gather_object(handles, mine)
-        ok = all(h is not None for h in handles)
-        if ok:
-            try:
-                self.ba.attach_p2p(world, rank, handles)
-            except Exception as e:  # noqa: BLE001
-                log(f"[bench] rank {rank}: p2p attach failed: {e}")
-                ok = False
-        all_ok = reduce_scalar(1.0 if ok else 0.0, world, "min") > 0.5
-        if all_ok:
-            return "p2p"
-        if ok:
-            self.ba.detach_p2p()
-        if not have_rccl:
-            raise RuntimeError("P2P exchange unavailable and no RCCL communicator attached")
-        return "rccl"
+        return self.ba.attach_sharded(world, rank, collective, rccl_ok, log=lambda m: log(f"[bench] {m}"))
 
     def start(self):
         self.ba.run_async()
@@ -1113,10 +1076,8 @@ def main():
     args = ap.parse_args()
     if args.same_device:
         args.collective = "p2p"
-        # ranks sharing one GPU: never the 3-launch A/B iteration (RSVIO_P2P_FOLD=2), whose K4c
-        # (hundreds of workgroups waiting for every rank's K6 partials) can fill the shared CUs
-        # and starve the other rank's K6; the default 4-launch one
-        os.environ["RSVIO_P2P_FOLD"] = "1"
+        # (ranks sharing one GPU never take the 3-launch A/B iteration RSVIO_P2P_FOLD=2: attach_p2p
+        # sees the shared device and lowers it to the default 4-launch one)
 
     world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:

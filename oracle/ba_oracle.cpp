@@ -736,9 +736,15 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
         for (int k = 0; k < n_kf; ++k) tposes[k] = pose_from7(&x7t[7 * k]);
         double new_cost = eval_cost(pr, tposes, pwt.data());
         double pred = 0.5 * (lambda * dx2 - gdx);
-        double rho = (cost - new_cost) / pred;
+        double dcost = cost - new_cost;
+        double rho = dcost / pred;
+        if (std::isfinite(new_cost) && std::fabs(dcost) <= cfg->cost_tolerance * cost) {
+            // converged: |change| within the tolerance whatever its sign; the candidate is not
+            // applied (DESIGN.md section 5 -- a rounding-level change decides nothing)
+            status = LM_COST_TOL;
+            break;
+        }
         if (std::isfinite(new_cost) && rho > 0.0) {
-            double dcost = cost - new_cost;
             x7.swap(x7t);
             pw.swap(pwt);
             poses.swap(tposes);
@@ -746,10 +752,6 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
             lambda *= std::max(1.0 / 3.0, 1.0 - f * f * f);
             nu = 2.0;
             cost = new_cost;
-            if (dcost <= cfg->cost_tolerance * (cost + dcost)) {
-                status = LM_COST_TOL;
-                break;
-            }
         } else {
             lambda *= nu;
             nu *= 2.0;
@@ -922,9 +924,13 @@ extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_
             double Ht[36], gt[6], new_cost;
             pnp_system(obs, pose_from7(xt), TCB2, cfg->huber_delta, Ht, gt, &new_cost);
             double pred = 0.5 * (lambda * dx2 - gdx);
-            double rho = (cost - new_cost) / pred;
+            double dcost = cost - new_cost;
+            double rho = dcost / pred;
+            if (std::isfinite(new_cost) && std::fabs(dcost) <= cfg->cost_tolerance * cost) {
+                status = LM_COST_TOL;  // converged, the candidate not applied (as the BA above)
+                break;
+            }
             if (std::isfinite(new_cost) && rho > 0.0) {
-                double dcost = cost - new_cost;
                 memcpy(x, xt, sizeof(x));
                 memcpy(H, Ht, sizeof(H));
                 memcpy(g, gt, sizeof(g));
@@ -932,10 +938,6 @@ extern "C" int orc_track_motion(const uint64_t* ids_l, const float* uv_l, int n_
                 lambda *= std::max(1.0 / 3.0, 1.0 - f * f * f);
                 nu = 2.0;
                 cost = new_cost;
-                if (dcost <= cfg->cost_tolerance * (cost + dcost)) {
-                    status = LM_COST_TOL;
-                    break;
-                }
             } else {
                 lambda *= nu;
                 nu *= 2.0;

@@ -77,24 +77,18 @@ class OracleBackend:
 
 
 
-PNP_TAIL_COST_RTOL = 1e-12
-
-
 def outcome_difference(rd, ro):
     """How the device FrameResult rd differs from the oracle's ro in its integer outcomes: None
-    (keyframe flag, PnP status + LM iterations, BA status + LM iterations all equal), "pnp_tail"
-    (only the PnP's status / iteration count differ, both runs succeeded and their final costs
-    agree to PNP_TAIL_COST_RTOL -- the LM iterated in its converged tail, where the accept test
-    compares cost changes at rounding level, ~1e-15 relative, and the device's fixed-order tree
-    sums and the oracle's sequential sums round differently), or a description of a divergence."""
+    when the keyframe flag, the PnP status + LM iterations and the BA status + LM iterations are
+    all equal, else a description of the divergence.  No exception: since round 5 the LM's
+    cost-tolerance test takes |change| <= tol * cost whatever the change's sign, before the
+    accept test, so a change at rounding level -- where the device's tree
+    sums and the oracle's sequential sums round differently -- no longer decides an outcome."""
     if rd.is_keyframe != ro.is_keyframe:
         return f"keyframe flag {rd.is_keyframe} vs {ro.is_keyframe}"
     if (rd.ba_status, rd.ba_iterations) != (ro.ba_status, ro.ba_iterations):
         return f"BA (status, iterations) {(rd.ba_status, rd.ba_iterations)} vs {(ro.ba_status, ro.ba_iterations)}"
     pd, po = (rd.pnp_status, rd.pnp_iterations), (ro.pnp_status, ro.pnp_iterations)
-    if pd == po:
-        return None
-    if (rd.pnp_status is not None and ro.pnp_status is not None and rd.pnp_status > 0 and ro.pnp_status > 0
-            and abs(rd.pnp_cost - ro.pnp_cost) <= PNP_TAIL_COST_RTOL * abs(ro.pnp_cost)):
-        return "pnp_tail"
-    return f"PnP (status, iterations) {pd} vs {po}, final cost {rd.pnp_cost} vs {ro.pnp_cost}"
+    if pd != po:
+        return f"PnP (status, iterations) {pd} vs {po}, final cost {rd.pnp_cost} vs {ro.pnp_cost}"
+    return None

@@ -914,19 +914,22 @@ __device__ void lm_update(LmState& s, double cost, const double tv[4], int max_i
             s.done = 1;
         } else {
             const double pred = 0.5 * (s.lambda * dx2 - (s.gcdc + s.gpdp));
-            const double rho = (cost - s.new_cost) / pred;
-            if (isfinite(s.new_cost) && rho > 0.0) {
-                const double dcost = cost - s.new_cost;
+            const double dcost = cost - s.new_cost;
+            const double rho = dcost / pred;
+            if (isfinite(s.new_cost) && fabs(dcost) <= cost_tol * cost) {
+                // converged: the candidate's cost change is within the
+                // tolerance, whatever its sign, and the candidate is not applied -- so a change
+                // at rounding level, whose sign two summation orders may disagree on, decides
+                // neither the outcome nor the state
+                s.status = RSVIO_LM_COST_TOLERANCE;
+                s.done = 1;
+            } else if (isfinite(s.new_cost) && rho > 0.0) {
                 s.accepted = 1;
                 s.cur = 1 - s.cur;  // the trial buffers become current
                 const double f = 2.0 * rho - 1.0;
                 s.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
                 s.nu = 2.0;
                 s.cost = s.new_cost;
-                if (dcost <= cost_tol * (s.cost + dcost)) {
-                    s.status = RSVIO_LM_COST_TOLERANCE;
-                    s.done = 1;
-                }
             } else {
                 s.lambda *= s.nu;
                 s.nu *= 2.0;
@@ -3159,6 +3162,8 @@ struct BundleAdjuster {
     // rank, every K4c block's decision then polling every wave's partial of every rank,
     // profiles/r04k_p2p_fold_kstats.txt); 0: 5 launches (X1 as its own kernel)
     int fold_lvl = 1;
+    int fold_req = 1;             // the level asked for (RSVIO_P2P_FOLD); attach_p2p may lower fold_lvl
+    bool p2p_shared_gpu = false;  // attach_p2p found two ranks on one device (fold 2 -> 1)
     bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
     bool p2p_fold2() const { return fold_lvl >= 2 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
@@ -3349,7 +3354,7 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
         const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0" / "1" / "2" (A/B switch)
-        if (fv && fv[0] >= '0' && fv[0] <= '2') fold_lvl = fv[0] - '0';
+        if (fv && fv[0] >= '0' && fv[0] <= '2') fold_lvl = fold_req = fv[0] - '0';
         const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
         desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
@@ -3946,9 +3951,9 @@ struct BundleAdjuster {
             res->solve_ms = 0.0;
             return;
         }
-        // single rank: return as soon as the last decision's ticket lands in pinned host memory
-        // (its state was written before it); the stream settles before anything else touches
-        // the handle's buffers (require_idle).  Sharded, or RSVIO_BA_WAIT=sync: stream sync.
+        // return as soon as the last decision's ticket lands in pinned host memory (its state was
+        // written before it); the stream settles before anything else touches the handle's
+        // buffers (require_idle).  RSVIO_BA_WAIT=sync: stream sync.
         const bool by_tick = pend.by_tick;
         while (true) {
             if (by_tick)
@@ -4030,18 +4035,46 @@ struct BundleAdjuster {
             P.peer[r] = static_cast<double*>(ptr);
             p2p_opened[r] = true;
         }
-        // self-test: rank r contributes r + 1 (and 1); every rank must read nr (nr + 1) / 2, nr
-        DevBuf<double> t(2);
-        const double tv[2] = {(double)(rk + 1), 1.0};
-        RSVIO_HIP(hipMemcpy(t.p, tv, sizeof tv, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, 2, P, d_xgen.p, d_p2p_err.p);
+        // self-test, which also makes the ranks agree on the exchange protocol: rank r contributes
+        // r + 1 and 1 (every rank must read nr (nr + 1) / 2 and nr), its fold level and flag-in-word
+        // switch with their squares (all ranks hold the same value iff sum = nr v and sum of squares
+        // = nr v^2 on every rank: a mismatch fails on EVERY rank, so all keep their previous
+        // collective together), and its device's PCI location in entry 6 + r (so every rank sees
+        // which ranks share a GPU)
+        int pci_dom = 0, pci_bus = 0, pci_dev = 0;
+        RSVIO_HIP(hipDeviceGetAttribute(&pci_dom, hipDeviceAttributePciDomainID, this->P.device));
+        RSVIO_HIP(hipDeviceGetAttribute(&pci_bus, hipDeviceAttributePciBusId, this->P.device));
+        RSVIO_HIP(hipDeviceGetAttribute(&pci_dev, hipDeviceAttributePciDeviceId, this->P.device));
+        constexpr int kSelf = 6 + kP2PMax;
+        static_assert(kSelf <= kP2PLLMax, "the self-test is one flag-in-word message");
+        double tv[kSelf] = {};
+        const double fl = (double)fold_req, lv = P.ll ? 1.0 : 0.0;
+        tv[0] = rk + 1; tv[1] = 1.0; tv[2] = fl; tv[3] = fl * fl; tv[4] = lv; tv[5] = lv * lv;
+        tv[6 + rk] = 1.0 + (double)(((long long)pci_dom << 16) | (pci_bus << 8) | pci_dev);
+        const int n_self = 6 + nr;
+        DevBuf<double> t(kSelf);
+        RSVIO_HIP(hipMemcpy(t.p, tv, sizeof(double) * n_self, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(ba_p2p_allreduce, dim3(1), dim3(256), 0, stream, t.p, n_self, P, d_xgen.p, d_p2p_err.p);
         RSVIO_HIP(hipGetLastError());
-        double out[2] = {0.0, 0.0};
-        RSVIO_HIP(hipMemcpyAsync(out, t.p, sizeof out, hipMemcpyDeviceToHost, stream));
+        double out[kSelf] = {};
+        RSVIO_HIP(hipMemcpyAsync(out, t.p, sizeof(double) * n_self, hipMemcpyDeviceToHost, stream));
         RSVIO_HIP(hipStreamSynchronize(stream));
         p2p_check();
         if (out[0] != nr * (nr + 1) / 2.0 || out[1] != (double)nr)
             throw std::runtime_error("P2P all-reduce self-test returned wrong sums");
+        if (out[2] != nr * fl || out[3] != nr * fl * fl || out[4] != nr * lv || out[5] != nr * lv)
+            throw std::runtime_error("P2P: the ranks disagree on RSVIO_P2P_FOLD / RSVIO_P2P_LL");
+        bool shared_gpu = false;
+        for (int a = 0; a < nr; ++a)
+            for (int b = a + 1; b < nr; ++b) shared_gpu |= out[6 + a] == out[6 + b];
+        // fold 2's K4c blocks poll every rank's K6 partials while they hold CUs: on a shared GPU
+        // they can starve a peer's K6 until the spin bound, so co-resident ranks take fold 1 (all
+        // ranks see the same codes and decide alike)
+        // (RSVIO_P2P_FOLD_SHARED=1 keeps fold 2 anyway: the A/B test of its sums on one GPU)
+        const char* fsv = std::getenv("RSVIO_P2P_FOLD_SHARED");
+        const bool keep2 = fsv && fsv[0] == '1';
+        fold_lvl = shared_gpu && fold_req >= 2 && !keep2 ? 1 : fold_req;
+        p2p_shared_gpu = shared_gpu;
         p2p = P;
         nranks = nr;
         rank = rk;
@@ -4103,10 +4136,12 @@ struct BundleAdjuster {
 
     // entry points that read or replace what an in-flight solve uses (rsvio_ba_run_async before
     // rsvio_ba_wait) are refused, as set_stream is
-    // single rank waits on the decision ticket (RSVIO_BA_WAIT=sync: on the stream + events)
-    // single rank or sharded over P2P (the exchanges are kernels of the stream; K7 publishes their
-    // error flag with the ticket); RCCL keeps the stream sync
-    bool by_tick() const { return tick_wait && coll != 1; }
+    // every collective waits on the decision ticket (RSVIO_BA_WAIT=sync: on the stream + events):
+    // K7 is enqueued after the chunk's last exchange on the same stream, so its ticket lands only
+    // after the exchanges completed -- ours (P2P: K7 also publishes their error flag with it) or
+    // RCCL's all-reduces.  A failed RCCL collective never lets K7 run: the bounded spin (1 s) then
+    // synchronises the stream, which reports the error (a slow peer merely ends the spin late).
+    bool by_tick() const { return tick_wait; }
 
     void require_idle(const char* what) {
         if (pend.active) throw CallOrderError(std::string(what) + ": a solve is in flight (call rsvio_ba_wait first)");

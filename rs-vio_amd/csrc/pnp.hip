@@ -264,9 +264,14 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
         C->phase = 1;
     } else {
         const double new_cost = s_sum[27];
-        const double rho = (C->cost - new_cost) / C->pred;
-        if (isfinite(new_cost) && rho > 0.0) {
-            const double dcost = C->cost - new_cost;
+        const double dcost = C->cost - new_cost;
+        const double rho = dcost / C->pred;
+        if (isfinite(new_cost) && fabs(dcost) <= A.cost_tol * C->cost) {
+            // converged: the change is within the tolerance whatever its sign, the candidate not
+            // applied (the BA's lm_update takes the same decision)
+            C->status = LM_COST_TOL;
+            done = true;
+        } else if (isfinite(new_cost) && rho > 0.0) {
 #pragma unroll
             for (int k = 0; k < 7; ++k) C->x[k] = C->xt[k];
 #pragma unroll
@@ -279,10 +284,6 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
             C->lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
             C->nu = 2.0;
             C->cost = new_cost;
-            if (dcost <= A.cost_tol * (C->cost + dcost)) {
-                C->status = LM_COST_TOL;
-                done = true;
-            }
         } else {
             C->lambda *= C->nu;
             C->nu *= 2.0;

@@ -293,7 +293,9 @@ struct Tracker {
     CamPair cams{};                 // T12 unprojection fused into append_pack_kernel when on
     DevBuf<float2> undist;          // 2 slots x 2 x cap
     DevBuf<float2> tmp_und;         // cap (remove_ids compaction scratch)
-    HostBuf<float2> h_undist;       // last process_frame's undistorted coordinates
+    HostBuf<float2> h_undist;       // pinned read-back of the undistorted coordinates, one per output
+                                    // slot (2 slots x 2 cams x cap): a submit's copies land in its own
+                                    // slot, undistorted() reads the collected one
     HostBuf<rsvio_feature> h_out;   // pinned staging of both packed feature lists (2 x cap)
     size_t last_n[2] = {0, 0};
     int wslot = 0;                  // the output slot the next submitted frame writes
@@ -354,6 +356,7 @@ struct Tracker {
     uint64_t* mid(int c) { return ids.p + (size_t)c * cap; }
     rsvio_feature* outp(int slot, int c) { return out.p + (size_t)(2 * slot + c) * cap; }
     float2* undp(int slot, int c) { return cams.on ? undist.p + (size_t)(2 * slot + c) * cap : nullptr; }
+    float2* hund(int slot, int c) { return h_undist.p + (size_t)(2 * slot + c) * cap; }
 
     // Enqueue one frame; images already in device memory.
     void enqueue_frame(const uint8_t* d_left, const uint8_t* d_right) {
@@ -405,9 +408,9 @@ struct Tracker {
         if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_out.p + cap + r0, outp(slot, 1) + r0, (r1 - r0) * sizeof(rsvio_feature),
                                               hipMemcpyDeviceToHost, stream));
         if (cams.on) {
-            if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + l0, undp(slot, 0) + l0, (l1 - l0) * sizeof(float2),
+            if (l1 > l0) RSVIO_HIP(hipMemcpyAsync(hund(slot, 0) + l0, undp(slot, 0) + l0, (l1 - l0) * sizeof(float2),
                                                   hipMemcpyDeviceToHost, stream));
-            if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(h_undist.p + cap + r0, undp(slot, 1) + r0,
+            if (r1 > r0) RSVIO_HIP(hipMemcpyAsync(hund(slot, 1) + r0, undp(slot, 1) + r0,
                                                   (r1 - r0) * sizeof(float2), hipMemcpyDeviceToHost, stream));
         }
     }
@@ -639,7 +642,7 @@ int rsvio_tracker_set_cameras(rsvio_tracker* t, const rsvio_camera* left, const 
         }
         if (!T.undist.p) {
             T.undist.alloc((size_t)4 * T.cap);
-            T.h_undist.alloc((size_t)2 * T.cap);
+            T.h_undist.alloc((size_t)4 * T.cap);
             T.tmp_und.alloc((size_t)T.cap);
         }
         T.cams.cam[0] = *left;
@@ -657,8 +660,9 @@ int rsvio_tracker_undistorted(rsvio_tracker* t, float* out_l, size_t cap_l, floa
         return RSVIO_ERR_INVALID_ARG;
     }
     if (cap_l < T.last_n[0] || cap_r < T.last_n[1]) return RSVIO_ERR_CAPACITY;
-    std::memcpy(out_l, T.h_undist.p, T.last_n[0] * sizeof(float2));
-    std::memcpy(out_r, T.h_undist.p + T.cap, T.last_n[1] * sizeof(float2));
+    // the collected frame's slot: a frame submitted since copies into the other one
+    std::memcpy(out_l, T.hund(T.rslot, 0), T.last_n[0] * sizeof(float2));
+    std::memcpy(out_r, T.hund(T.rslot, 1), T.last_n[1] * sizeof(float2));
     return RSVIO_OK;
 }
 
@@ -683,8 +687,8 @@ int rsvio_tracker_remove_ids(rsvio_tracker* t, const uint64_t* ids, size_t n) {
         if (T.cams.on) {  // undistorted() stays aligned with the compacted feature lists
             const size_t nl = std::min(T.last_n[0], (size_t)T.host_count[0]);
             const size_t nr = std::min(T.last_n[1], (size_t)T.host_count[1]);
-            if (nl) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p, T.undp(T.rslot, 0), nl * sizeof(float2), hipMemcpyDeviceToHost, T.stream));
-            if (nr) RSVIO_HIP(hipMemcpyAsync(T.h_undist.p + T.cap, T.undp(T.rslot, 1), nr * sizeof(float2),
+            if (nl) RSVIO_HIP(hipMemcpyAsync(T.hund(T.rslot, 0), T.undp(T.rslot, 0), nl * sizeof(float2), hipMemcpyDeviceToHost, T.stream));
+            if (nr) RSVIO_HIP(hipMemcpyAsync(T.hund(T.rslot, 1), T.undp(T.rslot, 1), nr * sizeof(float2),
                                              hipMemcpyDeviceToHost, T.stream));
             RSVIO_HIP(hipStreamSynchronize(T.stream));
             T.last_n[0] = nl;

@@ -46,6 +46,59 @@ def _c(a, dt):
     return np.ascontiguousarray(a, dtype=dt)
 
 
+def _all_min(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def attach_agreed(ba, world: int, rank: int, collective: str = "auto", rccl_ok: bool = True, log=None) -> str:
+    """Every rank of the torch.distributed control group takes the SAME branch: the RCCL
+    communicator first (the fallback; only when rccl_ok -- RCCL refuses two ranks on one GPU),
+    then the P2P one-shot all-reduce, kept only if EVERY rank exported a buffer and passed the
+    self-test (which also fails on every rank when their exchange settings differ).  Otherwise the
+    ranks that attached detach, and all go on over RCCL -- or, without it, all raise RuntimeError.
+    Returns "p2p" or "rccl".  `ba` needs p2p_export / attach_p2p / detach_p2p / attach_comm /
+    rccl_unique_id (BundleAdjuster's)."""
+    import torch.distributed as dist
+    say = log or (lambda m: None)
+    have_rccl = False
+    if collective in ("auto", "rccl") and rccl_ok:
+        obj = [ba.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ba.attach_comm(world, rank, obj[0])
+        have_rccl = True
+    if collective == "rccl":
+        if not have_rccl:
+            raise RuntimeError("RCCL requested but not available")
+        return "rccl"
+    mine = None
+    try:
+        mine = ba.p2p_export(world)
+    except Exception as e:  # noqa: BLE001 - reported, then agreed on below
+        say(f"rank {rank}: p2p export failed: {e}")
+    handles = [None] * world
+    dist.all_gather_object(handles, mine)
+    ok = all(h is not None for h in handles)
+    if ok:
+        try:
+            ba.attach_p2p(world, rank, handles)
+        except Exception as e:  # noqa: BLE001
+            say(f"rank {rank}: p2p attach failed: {e}")
+            ok = False
+    all_ok = world == 1 and ok or world > 1 and _all_min(1.0 if ok else 0.0) > 0.5
+    if all_ok:
+        return "p2p"
+    if ok:
+        ba.detach_p2p()
+    if not have_rccl:
+        raise RuntimeError("P2P exchange unavailable on some rank and no RCCL communicator attached")
+    return "rccl"
+
+
 class BundleAdjuster:
     """One device-resident BA solver (one HIP stream)."""
 
@@ -94,6 +147,12 @@ class BundleAdjuster:
 
     def detach_p2p(self) -> None:
         check(_lib.load().rsvio_ba_detach_p2p(self._h))
+
+    def attach_sharded(self, world: int, rank: int, collective: str = "auto", rccl_ok: bool = True,
+                       log=None) -> str:
+        """Attach this rank's landmark shard (sliding_window.rs:325's solve, split over ranks) to
+        its peers over the initialised torch.distributed control group; see attach_agreed."""
+        return attach_agreed(self, world, rank, collective, rccl_ok, log)
 
     @staticmethod
     def rccl_unique_id() -> bytes:

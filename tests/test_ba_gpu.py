@@ -744,7 +744,8 @@ def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level):
     (tmp_path / "a").mkdir()
     (tmp_path / "b").mkdir()
     fold = _run_p2p(2, 4000, tmp_path / "a", env={"RSVIO_P2P_FOLD": "1"})
-    sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": level})
+    # (on this shared GPU attach_p2p would lower fold 2 to 1; the test keeps it to compare its sums)
+    sep = _run_p2p(2, 4000, tmp_path / "b", env={"RSVIO_P2P_FOLD": level, "RSVIO_P2P_FOLD_SHARED": "1"})
     for a, b in zip(fold, sep):
         for k in ("pose", "pw", "res"):
             assert np.array_equal(a[k], b[k]), k
@@ -763,3 +764,48 @@ def test_sharded_p2p_flag_in_word_equals_flag_protocol(gpu, tmp_path, world):
     for a, b in zip(ll, fl):
         for k in ("pose", "pw", "res"):
             assert np.array_equal(a[k], b[k]), k
+
+
+def _mismatch_worker(rank, world, port, out_dir):
+    import os
+
+    import torch.distributed as dist
+    # the injected fault: rank 1 asks for the flag-in-word system exchange, rank 0 does not
+    os.environ["RSVIO_P2P_LL"] = "1" if rank == 1 else "0"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rsvio import synthetic as S
+        from rsvio.ba import BundleAdjuster
+        shard = S.ba_problem(n_lm=400, seed=5, init_seed=6).shard(rank, world)
+        ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
+        try:
+            got = ba.attach_sharded(world, rank, "p2p", rccl_ok=False)
+        except RuntimeError as e:
+            got = "error: " + str(e)[:60]
+        ba.set_problem_from(shard)      # the handle is intact and unsharded: its own shard solves
+        r = ba.run()
+        with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+            f.write(f"{got}\n{r.status}\n")
+        ba.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_attach_disagreement_fails_on_every_rank(gpu, tmp_path):
+    """Verdict r04 item 5: a fault injected on ONE rank (its exchange settings differ) makes the
+    P2P self-test fail on EVERY rank; no RCCL on a shared GPU, so every rank raises RuntimeError
+    (none hangs: the test's own timeout) and keeps a working unsharded handle."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_mismatch_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    outs = [(tmp_path / f"r{r}.txt").read_text().split("\n") for r in range(2)]
+    for got, status, _ in outs:
+        assert got.startswith("error: P2P exchange unavailable"), got
+        assert int(status) > 0

@@ -137,3 +137,22 @@ def test_threaded_oracle_legs_match_sequential(oracle):
         t = oracle.StereoTracker(320, 240, 3, 30, 20, 0.01, threads=threads)
         outs.append([t.process_frame(l, r) for l, r in frames])
     assert outs[0] == outs[1]
+
+
+def test_oracle_solve_reproduces_the_ba_golden():
+    """tests/golden/ba_small.npz (made by tests/golden/make_golden.py from this oracle): the oracle
+    still solves it to the same status, iteration count and bits -- the golden pins the oracle's
+    LM against drift on CPU, as test_ba_gpu pins the device against it."""
+    from pathlib import Path
+    from types import SimpleNamespace
+
+    import numpy as np
+
+    from oracle import oracle as O
+    g = np.load(Path(__file__).resolve().parent / "golden" / "ba_small.npz", allow_pickle=False)
+    prob = SimpleNamespace(**{k: g[k] for k in ("pose7", "kf_fixed", "p_W", "obs_lm", "obs_kf", "obs_cam",
+                                                 "obs_uv", "T_C_B2")})
+    po, pwo, ro = O.ba_solve(prob)
+    assert (ro.status, ro.iterations) == (int(g["status"]), int(g["iterations"]))
+    assert np.array_equal(po, g["sol_pose7"]) and np.array_equal(pwo, g["sol_p_W"])
+    assert ro.final_cost == float(g["final_cost"])

@@ -48,7 +48,7 @@ def compare(n_frames, pipelined=True, log_every=50):
     ed = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=dev, pipelined=pipelined)
     eo = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=orc)
     dev_frames = ed.run(s.frames) if pipelined else (ed.process_frame(l, r) for l, r in s.frames)
-    pairs, tail = [], []
+    pairs = []
     first = {"ids": None, "uv_bits": None, "keyframe": None, "status_class": None, "status_exact": None,
              "pose_1e-6": None}
     max_pose = 0.0
@@ -73,10 +73,7 @@ def compare(n_frames, pipelined=True, log_every=50):
         for a, b in ((rd.pnp_status, ro.pnp_status), (rd.ba_status, ro.ba_status)):
             if first["status_class"] is None and not ((a is None) == (b is None) and (a is None or (a > 0) == (b > 0))):
                 first["status_class"] = k
-        diff = outcome_difference(rd, ro)
-        if diff == "pnp_tail":
-            tail.append(k)
-        elif first["status_exact"] is None and diff is not None:
+        if first["status_exact"] is None and outcome_difference(rd, ro) is not None:
             first["status_exact"] = k
         d = float(np.abs(rd.T_W_B - ro.T_W_B).max())
         max_pose = max(max_pose, d)
@@ -89,9 +86,8 @@ def compare(n_frames, pipelined=True, log_every=50):
     md, mo = ed.window.map_points, eo.window.map_points
     dev.be.close()
     return {"frames": n_frames, "mode": "Estimator.run (look-ahead, pipelined)" if pipelined else "sequential",
-            "status_exact_means": "keyframe flag, BA status + LM iterations, PnP status + LM iterations outside "
-                                  "the converged tail (oracle/estimator.py outcome_difference)",
-            "pnp_converged_tail_frames": tail,
+            "status_exact_means": "keyframe flag, BA status + LM iterations, PnP status + LM iterations "
+                                  "(oracle/estimator.py outcome_difference)",
             "keyframes": n_kf, "first_divergent_frame": first,
             "max_pose_diff_vs_oracle": max_pose, "max_trajectory_diff_vs_oracle": traj,
             "map_ids_equal": sorted(md) == sorted(mo),

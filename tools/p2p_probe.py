@@ -3,7 +3,11 @@ P2P exchange over IPC-mapped buffers), each rank re-solving its 2,000-landmark s
 config-3-per-rank window R times; prints per rank the device ms per LM iteration (the solve's
 device stamps) -- run it under rocprofv3 --kernel-trace --stats for the per-kernel split of the
 sharded iteration (K4c, K5, K6[, X1][, X2]) at each RSVIO_P2P_FOLD level.
-  python tools/p2p_probe.py [ranks] [repeats]"""
+  python tools/p2p_probe.py [ranks] [repeats]          # spawns the ranks itself
+  RANK=r WORLD_SIZE=n MASTER_PORT=p python tools/p2p_probe.py n [repeats]
+                                                       # one rank per process, started by the shell:
+                                                       # the form to run under rocprofv3 (the
+                                                       # profiled program is then the rank itself)"""
 import os
 import socket
 import sys
@@ -44,9 +48,12 @@ def worker(rank, world, port, reps):
 
 
 if __name__ == "__main__":
-    import torch.multiprocessing as mp
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    if "RANK" in os.environ:
+        worker(int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), int(os.environ["MASTER_PORT"]), reps)
+        sys.exit(0)
+    import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
