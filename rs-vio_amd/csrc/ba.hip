@@ -2073,6 +2073,223 @@ __device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// K5 by 6x6 block pivots (round 5, the default; -DRSVIO_K5_PANEL8 builds the 8-column panels
+// above).  The camera system's own blocks: step k factors keyframe k's diagonal block as a whole.
+//   * Chain wave (wave 0, lane = row; rows lane and lane + 64 past 64 rows): it holds column
+//     block k of its rows in registers, fully updated.  The diagonal block's 21 lower entries go
+//     to every lane through LDS (one store by its 6 rows, one broadcast read), and every lane
+//     factors it redundantly in registers -- 6 pivots, the 1/d chain with no readlane or LDS on
+//     it.  Every row below then solves its 6 multipliers against it (t forward-substituted,
+//     u = t = the row of D L, l = t D^-1), writes L in place into M's columns and U into a U
+//     buffer, and -- the look-ahead -- updates its row of column block k + 1 with this block's
+//     contribution in registers, so the next step's columns never go back through LDS.
+//   * Update waves (waves 1..): the block's rank-6 update of the columns past block k + 1 on the
+//     matrix cores, C_IJ += (-U_I) L_J^T per 16x16 tile (the 6 columns padded to 8: two
+//     v_mfma_f64_16x16x4f64), lanes whose column lies before block k + 2 neither load nor store.
+// One workgroup barrier per block: 9 block steps at config 3 instead of 54 pivots each with its
+// readlanes and LDS stores.  Row NP is b, whose multipliers end as z = D^-1 L^-1 b.  Tolerance
+// parity like the panel version (the same pivots, sums reassociated).
+// ---------------------------------------------------------------------------------------
+// phase stamps of the block steps (stamps build only): lane 0 of wave w, after its memory drains
+#ifdef RSVIO_STAMPS
+#define WSTAMP(w, k)                                                                           \
+    do {                                                                                       \
+        if (threadIdx.x == 64 * (w) && blockIdx.x < 4096) {                                    \
+            __builtin_amdgcn_s_waitcnt(0);                                                     \
+            g_dbg[blockIdx.x * 32 + (k)] = (unsigned long long)clock64();                      \
+        }                                                                                      \
+    } while (0)
+#else
+#define WSTAMP(w, k) \
+    do {             \
+    } while (0)
+#endif
+
+template <int NF>
+struct BkDims {
+    static constexpr int NP = 6 * NF;
+    static constexpr int RPL = NP + 1 <= 64 ? 1 : 2;  // rows per lane of the chain wave
+    static constexpr int NT = (NP + 1 + 15) / 16;     // 16-row tiles, the b row included
+    static constexpr int NPP = 16 * NT;
+    static constexpr int NTC = (NP + 15) / 16;        // 16-column tiles
+    static constexpr int LD = NF <= 10 ? kMfLd : 129; // odd leading dimension of M and U
+};
+
+// Step K's rank-6 update of the columns >= 6 (K + 2) by update wave `wid` of `nw`.  Uk: U of
+// block K (6 columns of LD doubles, zero on the rows before block K + 1); L of block K lives in
+// M's columns 6K .. 6K + 5.
+template <int NF, int K, int NWU>
+__device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane, int wid) {
+    using D = BkDims<NF>;
+    constexpr int c0 = 6 * K, cmin = c0 + 12;
+    if constexpr (cmin < D::NP) {
+        constexpr int TJ0 = cmin / 16;
+        constexpr int ntile = (D::NTC - TJ0) * D::NT - (D::NTC - 1 + TJ0) * (D::NTC - TJ0) / 2;
+        constexpr int Q = (ntile + NWU - 1) / NWU;  // tiles per update wave
+        const int i16 = lane & 15, k4 = lane >> 4;
+        // every tile's operands and accumulator loaded first, then the MFMAs, then the stores:
+        // one LDS round trip per step instead of one per tile
+        double av[Q][2], bv[Q][2];
+        mf_dbl4 c[Q];
+        int base[Q];
+        bool live[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int t = wid + NWU * q;
+            int TJ = TJ0, rem = t < ntile ? t : 0;
+            while (rem >= D::NT - TJ) {
+                rem -= D::NT - TJ;
+                ++TJ;
+            }
+            const int TI = TJ + rem;
+            const int col = 16 * TJ + i16;  // this lane's column of the C tile (= a row of L)
+            live[q] = t < ntile && col >= cmin && col < D::NP;
+            base[q] = col * D::LD + 16 * TI + k4;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int kk = 4 * m + k4;
+                av[q][m] = kk < 6 ? -Uk[kk * D::LD + 16 * TI + i16] : 0.0;
+                bv[q][m] = (kk < 6 && live[q]) ? M[(c0 + kk) * D::LD + col] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[q][r] = live[q] ? M[base[q] + 4 * r] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][0], bv[q][0], c[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][1], bv[q][1], c[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (live[q])
+#pragma unroll
+                for (int r = 0; r < 4; ++r) M[base[q] + 4 * r] = c[q][r];
+    }
+}
+
+// Block step K.  a: column block K of the chain wave's rows (updated); U: 2 x 6 x LD doubles
+// (blocks alternate); Dsc / Lsc: 36 doubles each of chain-wave scratch.  Every wave of the block
+// runs every step (one barrier each).
+template <int NF, int K, int NW>
+__device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, double* Lsc,
+                                         double (&a)[BkDims<NF>::RPL][6], int tid, bool& bad) {
+    using D = BkDims<NF>;
+    constexpr int RPL = D::RPL, LD = D::LD, c0 = 6 * K;
+    const int lane = tid & 63, wave = tid >> 6;
+    double u[RPL][6];
+    if constexpr (K < 9) WSTAMP(0, 8 + K);  // slots 8..16: wave 0 at the step's start
+    if (wave == 0) {
+        // the diagonal block to every lane: its 6 rows store, every lane reads the lower 21
+#pragma unroll
+        for (int h = 0; h < RPL; ++h) {
+            const int i = lane + 64 * h - c0;
+            if (i >= 0 && i < 6)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) Dsc[6 * i + j] = a[h][j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        double Dg[6][6], Lg[6][6], inv[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) Dg[i][j] = Dsc[6 * i + j];
+        // its LDL^T, redundantly on every lane: Dg[i][j] (i > j) ends as U = (D L)[i][j], Lg = L
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const double piv = Dg[j][j];
+            bad |= !(piv > 0.0) || !isfinite(piv);
+            inv[j] = rcp_f64(piv);
+#pragma unroll
+            for (int i = j + 1; i < 6; ++i) Lg[i][j] = Dg[i][j] * inv[j];
+#pragma unroll
+            for (int i = j + 1; i < 6; ++i)
+#pragma unroll
+                for (int i2 = j + 1; i2 <= i; ++i2) Dg[i][i2] = fma(-Lg[i][j], Dg[i2][j], Dg[i][i2]);
+        }
+        // the rows' multipliers, L and U stores, the next block's L rows to Lsc
+#pragma unroll
+        for (int h = 0; h < RPL; ++h) {
+            const int r = lane + 64 * h, i = r - c0;
+            double t[6], l[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) t[j] = a[h][j];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                u[h][j] = t[j];
+                l[j] = t[j] * inv[j];
+#pragma unroll
+                for (int j2 = j + 1; j2 < 6; ++j2) t[j2] = fma(-l[j], Dg[j2][j], t[j2]);
+            }
+            // (a row i of the diagonal block gets l_j = Lg[i][j] bit for bit for j < i: the same
+            // operations on the same values as the factor's; its entries j >= i land on M's
+            // diagonal and upper part, which nothing reads)
+            const bool below = i >= 6 && r <= D::NP;
+            if (i >= 0 && r <= D::NP)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) M[(c0 + j) * LD + r] = l[j];
+            if (r < D::NPP)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) U[(K & 1) * 6 * LD + j * LD + r] = below ? u[h][j] : 0.0;
+            if constexpr (K + 1 < NF)
+                if (i >= 6 && i < 12)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) Lsc[6 * (i - 6) + j] = l[j];
+        }
+    }
+    if constexpr (K == 0) WSTAMP(0, 30);  // wave 0's part A of step 0 done
+    if constexpr (K == 4) WSTAMP(0, 31);
+    if constexpr (K >= 1 && K <= 4) WSTAMP(1, 25 + K);  // slots 26..29: wave 1 done with step K - 1
+    __syncthreads();  // L and U of block K visible; the update waves finished block K - 1's update
+    if constexpr (K < 8) WSTAMP(0, 17 + K);  // slots 17..24: wave 0 released by barrier K
+    if (wave == 0) {
+        if constexpr (K + 1 < NF) {
+            // the look-ahead: column block K + 1 (block K - 1's update applied by the update
+            // waves) minus this block's contribution, in registers
+            double Ls[6][6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int m = 0; m < 6; ++m) Ls[j][m] = Lsc[6 * j + m];
+#pragma unroll
+            for (int h = 0; h < RPL; ++h) {
+                const int r = lane + 64 * h < D::NPP ? lane + 64 * h : D::NPP - 1;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) a[h][j] = M[(c0 + 6 + j) * LD + r];
+            }
+#pragma unroll
+            for (int h = 0; h < RPL; ++h)
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) a[h][j] = fma(-u[h][m], Ls[j][m], a[h][j]);
+        }
+    } else {
+        bk_update<NF, K, NW - 1>(M, U + (K & 1) * 6 * LD, lane, wave - 1);
+    }
+    if constexpr (K + 1 < NF) bk_steps<NF, K + 1, NW>(M, U, Dsc, Lsc, a, tid, bad);
+}
+
+// The whole factorisation (every wave of the block); afterwards M's columns hold L (unit lower)
+// and row NP holds z.  U: 2 x 6 x LD doubles, S: 72 doubles of scratch.  (A rolled loop over
+// the steps -- one step's code reused instead of ~37 KB of straight-line code -- measured
+// slower: 17.1 vs 13.9 us per K5 launch at config 3, profiles/r05d_k5_stamps.txt.)
+template <int NF, int NW>
+__device__ __forceinline__ void bk_factor(double* M, double* U, double* S, int tid, bool& bad) {
+    using D = BkDims<NF>;
+    double a[D::RPL][6];
+    if ((tid >> 6) == 0) {
+        const int lane = tid & 63;
+#pragma unroll
+        for (int h = 0; h < D::RPL; ++h) {
+            const int r = lane + 64 * h < D::NPP ? lane + 64 * h : D::NPP - 1;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) a[h][j] = M[j * D::LD + r];
+        }
+    }
+    bk_steps<NF, 0, NW>(M, U, S, S + 36, a, tid, bad);
+}
+
 template <int NF>
 __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine,
                                        const P2P* P = nullptr, unsigned long long* xgen = nullptr, int* err = nullptr) {
@@ -2148,9 +2365,16 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
         return;
     }
     bool bad = false;
+#ifndef RSVIO_K5_BLOCK
     if (wave == 0) mf_factor<NF, 0>(M, Lf, Up, lane, bad);
     __syncthreads();
     mf_panel<NF, 0>(M, Lf, Up, tid, bad);
+    double* const Lres = Lf;
+#else
+    static_assert(BkDims<NF>::NPP == NPP && BkDims<NF>::LD == kMfLd, "one M layout for both factorisations");
+    bk_factor<NF, kK5Threads / 64>(M, Up, Lf, tid, bad);
+    double* const Lres = M;  // L in place in M's columns
+#endif
     if (wave != 0) return;
     if (bad) {
         if (lane == 0) k5_result(st, 0, 0.0, 0.0);
@@ -2159,11 +2383,11 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     // z_j = L[NP][j] (row NP of the eliminated augmented matrix); L^T x = z (unit diagonal):
     // lane j, L[i][j] = Lf[j][i] column-major, zero for i <= j so the update needs no select
     const int lj = lane < NP ? lane : 0;
-    double yv = lane < NP ? Lf[lj * kMfLd + NP] : 0.0;
+    double yv = lane < NP ? Lres[lj * kMfLd + NP] : 0.0;
     double lt[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const double m = Lf[lj * kMfLd + j];
+        const double m = Lres[lj * kMfLd + j];
         lt[j] = lane < j ? m : 0.0;
     }
 #pragma unroll
