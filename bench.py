@@ -1064,11 +1064,13 @@ def main():
                          "best (round 2 sweep: K4c's 360 two-wave-per-SIMD workgroups fit the BA's 192 CUs "
                          "in one round)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
-    ap.add_argument("--order", default="ba-first", choices=["frame-first", "ba-first", "split"],
-                    help="protocol step: enqueue the frame (image upload, pyramids, LK, feature download) "
-                         "before the keyframe window's upload + solve start, or after; both run concurrently "
-                         "either way (the tracker does not depend on the solve); ba-first measured faster (3.93k vs 3.64-3.68k "
-                         "frames/s, profiles/r03s_order_ab.txt): the solve is the longer path once delayed")
+    ap.add_argument("--order", default="split", choices=["frame-first", "ba-first", "split"],
+                    help="protocol step: the frame's image upload first, then the keyframe window's upload + "
+                         "solve start, then the frame's kernels and downloads (split, the default: 4.16-4.35k vs "
+                         "3.98-4.08k frames/s for ba-first and 3.74-3.96k for frame-first on one box, "
+                         "profiles/r05h_order_ab.txt -- the image and window uploads share the copy engine, and "
+                         "the image then lands first without holding the window back behind the frame's kernels "
+                         "enqueue); both paths run concurrently either way (the tracker does not depend on the solve)")
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "p2p"],
                     help="BA exchange for N>1: P2P one-shot all-reduce (auto: if every rank attaches) or RCCL")
     ap.add_argument("--same-device", action="store_true",

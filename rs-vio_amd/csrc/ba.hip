@@ -548,8 +548,9 @@ struct SlotSrc {
     const int* wave_fill;            // n_wave: real slots of the wave (the rest are padding lanes)
     const int* wave_lm;              // n_wave + 1: first landmark of each wave, then n_lm
     const unsigned* key;             // n_obs: landmark << 6 | kf << 1 | cam
-    const double2* uv;               // n_obs
+    const double2* uv;               // n_obs, f64 -- or, when uv32 is set, the same values as f32 pairs
     int nb_lm, nb_pad;               // blocks of the landmark and padding parts of the grid
+    int uv32;                        // the upload holds (u, v) as float2 (every value exact in f32)
 };
 constexpr unsigned long long kEvenBits = 0x5555555555555555ull;
 
@@ -594,7 +595,12 @@ __device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSr
         const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
         const size_t q = (size_t)S.lm_base[l] + __popcll(below);
         const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
-        huv[2 * q + sub] = S.uv[i];
+        if (S.uv32) {  // widened exactly: the same f64 values as the caller's
+            const float2 f = reinterpret_cast<const float2*>(S.uv)[i];
+            huv[2 * q + sub] = make_double2((double)f.x, (double)f.y);
+        } else {
+            huv[2 * q + sub] = S.uv[i];
+        }
     }
 }
 
@@ -1644,6 +1650,9 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve(Geometry G, Prob P
 // ---------------------------------------------------------------------------------------
 typedef double mf_dbl4 __attribute__((ext_vector_type(4)));
 constexpr int kMfLd = 65;  // f64 leading dimension of the LDS matrices (odd: column reads spread banks)
+constexpr int kBkLd = 129;  // the same for the 6x6-block solver past 10 free keyframes (up to 121 rows)
+// the block solver's instantiations past 10 free keyframes (a window pads up to the next one)
+inline int bk_template_nf(int n_free) { return n_free <= 13 ? 13 : n_free <= 16 ? 16 : 20; }
 constexpr int kMfPanel = 8;  // panel width: 8 pivots of in-panel VALU work between matrix-core updates
 
 // The augmented system [[S, .], [b^T, .]] padded to NPP = 16 NT >= NP + 1 rows: row NP is b, so
@@ -1663,19 +1672,20 @@ struct MfDims {
 // in K5's LDS: >= 0 a column-major position of M (bit 30: + lambda after the sum), -1 none (the
 // upper half of a diagonal block), -2 - i the i-th g_c.  Built on the host per problem.
 constexpr int kMfMapLambda = 1 << 30;
-inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, int* map, int np_target = 0) {
+inline void mf_dense_map(int nf, int n_pb, const int* pb_fa, const int* pb_fb, int* map, int np_target = 0,
+                         int ld = kMfLd) {
     const int np = np_target > 0 ? np_target : 6 * nf;  // the b row (the template's NP)
     for (int pb = 0; pb < n_pb; ++pb)
         for (int k = 0; k < 36; ++k) {
             const int ra = k / 6, ca = k % 6, fa = pb_fa[pb], fb = pb_fb[pb];
             int v;
             if (fa == fb)
-                v = ra >= ca ? ((6 * fa + ca) * kMfLd + 6 * fa + ra) | (ra == ca ? kMfMapLambda : 0) : -1;
+                v = ra >= ca ? ((6 * fa + ca) * ld + 6 * fa + ra) | (ra == ca ? kMfMapLambda : 0) : -1;
             else
-                v = (6 * fa + ra) * kMfLd + 6 * fb + ca;  // S[6fa+ra][6fb+ca] -> its lower mirror
+                v = (6 * fa + ra) * ld + 6 * fb + ca;  // S[6fa+ra][6fb+ca] -> its lower mirror
             map[36 * pb + k] = v;
         }
-    for (int i = 0; i < 6 * nf; ++i) map[36 * n_pb + i] = i * kMfLd + np;  // b_i -> row NP, column i
+    for (int i = 0; i < 6 * nf; ++i) map[36 * n_pb + i] = i * ld + np;  // b_i -> row NP, column i
     for (int i = 0; i < 6 * nf; ++i) map[36 * n_pb + 6 * nf + i] = -2 - i;
 }
 
@@ -2113,7 +2123,7 @@ struct BkDims {
     static constexpr int NT = (NP + 1 + 15) / 16;     // 16-row tiles, the b row included
     static constexpr int NPP = 16 * NT;
     static constexpr int NTC = (NP + 15) / 16;        // 16-column tiles
-    static constexpr int LD = NF <= 10 ? kMfLd : 129; // odd leading dimension of M and U
+    static constexpr int LD = NF <= 10 ? kMfLd : kBkLd; // odd leading dimension of M and U
 };
 
 // Step K's rank-6 update of the columns >= 6 (K + 2) by update wave `wid` of `nw`.  Uk: U of
@@ -2408,6 +2418,195 @@ template <int NF>
 __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma_p2p(Geometry G, Prob Pr, Work Wk, P2P P,
                                                                         unsigned long long* xgen, int* err) {
     camera_solve_mfma_body<NF>(G, Pr, Wk, 2, &P, xgen, err);
+}
+
+// ---------------------------------------------------------------------------------------
+// K5 for 11..20 free keyframes (config 5's 19): the 6x6-block LDL^T above with MFMA trailing
+// updates, 8 waves (the chain wave holds rows lane and lane + 64; 7 update waves), the system
+// padded to NF in {13, 16, 20} with identity rows / columns (pivot 1, no coupling: every real
+// entry sees the unpadded factorisation's operations).  The partial systems are summed in rounds
+// (4 entries of 8 partials per thread in flight) and scattered into M by the window's map
+// (leading dimension kBkLd).  The default past 10 free keyframes; RSVIO_K5=pipe4 / gj1 keep the
+// VALU ba_camera_solve_x2 below.
+// ---------------------------------------------------------------------------------------
+constexpr int kBkWaves = 8;
+
+template <int NF>
+__device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine) {
+    using D = BkDims<NF>;
+    constexpr int NP = D::NP, LD = D::LD;
+    static_assert(NF > 10 && D::RPL == 2 && D::NPP <= LD, "the 11..20 free-keyframe solver");
+    constexpr int T = 64 * kBkWaves;
+    __shared__ __attribute__((aligned(16))) double M[16 * D::NTC * LD];
+    __shared__ __attribute__((aligned(16))) double U[2 * 6 * LD];
+    __shared__ __attribute__((aligned(16))) double S[72];
+    __shared__ double gsh[NP];
+    __shared__ double dcs[128];
+    __shared__ int fail;
+    LmState* st = Wk.st;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nF = G.n_free, n = 6 * nF;
+    const int ne = G.n_pb * 36 + 12 * nF;
+    double p7b[2][7];
+    int fidx = -1;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 7; ++i) p7b[b][i] = i == 3 ? 1.0 : 0.0;
+    if (wave == 0 && lane < G.n_kf) {
+        fidx = Pr.free_idx[lane];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 7; ++i) p7b[b][i] = Wk.pose[b][7 * lane + i];
+    }
+    if (combine) {
+        // single rank: the cost of the initial linearisation (K4 wave partials) and the singular
+        // flag with the first round's loads; then the partial systems in rounds
+        double pa[16];
+        int sing = 0;
+        if (tid < 64) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) pa[k] = tid + 64 * k < G.n_wave ? Wk.partA[(tid + 64 * k) * kPartA] : 0.0;
+            sing = *Wk.singular;
+        }
+        const int done = st->done;
+        const double lambda = st->lambda;
+        if (done) return;
+        const size_t L = sys_len(G);
+        constexpr int kR = 4;
+        for (int e0 = 0; e0 < ne; e0 += T * kR) {
+            double v[kR][kGrp];
+            int dst[kR];
+#pragma unroll
+            for (int i = 0; i < kR; ++i) {
+                const int e = e0 + tid + T * i;
+                dst[i] = e < ne ? Pr.dmap[e] : -1;
+#pragma unroll
+                for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < kR; ++i) {
+                double a = v[i][0];
+#pragma unroll
+                for (int x = 1; x < kGrp; ++x) a += v[i][x];
+                const int d = dst[i];
+                if (d >= 0) {
+                    if (d & kMfMapLambda) a += lambda;
+                    M[d & (kMfMapLambda - 1)] = a;
+                } else if (d <= -2) {
+                    gsh[-2 - d] = a;
+                }
+            }
+        }
+        if (tid < 64) {
+            double c = 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c += pa[k];
+            for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+            c = wave_sum_det(c);
+            if (tid == 0) {
+                Wk.sys[ne] = c;  // the decision of iteration 0 reads the initial cost here
+                fail = sing;
+            }
+        }
+    } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
+        if (st->done) return;
+        const double* sys = Wk.sys;
+        for (int e = tid; e < ne; e += T) {
+            const int d = Pr.dmap[e];
+            if (d >= 0)
+                M[d & (kMfMapLambda - 1)] = sys[e];
+            else if (d <= -2)
+                gsh[-2 - d] = sys[e];
+        }
+        if (tid == 0) fail = sys[ne + 1] != 0.0;
+    }
+    const int cur = st->cur;
+    double p7[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) p7[i] = cur ? p7b[1][i] : p7b[0][i];
+    if (n < NP)  // identity padding: rows / columns [n, NP), the b row zero there
+        for (int e = tid; e < NP * (NP + 1); e += T) {
+            const int c = e / (NP + 1), r = e - c * (NP + 1);
+            if (r >= c && ((r >= n && r < NP) || (c >= n && c < NP))) M[c * LD + r] = r == c ? 1.0 : 0.0;
+        }
+    __syncthreads();
+    if (tid == 0) *Wk.singular = 0;
+    double gcl[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) gcl[q] = (wave == 0 && lane + 64 * q < n) ? gsh[lane + 64 * q] : 0.0;
+    __syncthreads();
+    if (fail) {
+        if (tid == 0) k5_result(st, 0, 0.0, 0.0);
+        return;
+    }
+    bool bad = false;
+    bk_factor<NF, kBkWaves>(M, U, S, tid, bad);
+    if (wave != 0) return;
+    if (bad) {
+        if (lane == 0) k5_result(st, 0, 0.0, 0.0);
+        return;
+    }
+    // L^T x = z (unit diagonal), z = row NP: lane holds the unknowns i = lane, lane + 64, L[j][i] =
+    // M[i LD + j] (zero for j <= i by the select); the padded unknowns have z = 0: start at n - 1
+    double yv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) yv[q] = M[min(lane + 64 * q, NP - 1) * LD + NP];
+    constexpr int kBs = 8;
+    for (int j0 = n - 1; j0 >= 0; j0 -= kBs) {
+        double lt[kBs][2];
+#pragma unroll
+        for (int t = 0; t < kBs; ++t) {
+            const int j = max(j0 - t, 0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) lt[t][q] = M[min(lane + 64 * q, NP - 1) * LD + j];
+        }
+#pragma unroll
+        for (int t = 0; t < kBs; ++t) {
+            const int j = j0 - t;
+            if (j < 0) break;
+            const double xj = j >= 64 ? rl64(yv[1], j - 64) : rl64(yv[0], j);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const double upd = fma(-lt[t][q], xj, yv[q]);
+                yv[q] = lane + 64 * q < j ? upd : yv[q];
+            }
+        }
+    }
+    double x[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) x[q] = lane + 64 * q < n ? yv[q] : 0.0;
+    const double d2 = wave_sum_det(x[0] * x[0] + x[1] * x[1]);
+    const double gd = wave_sum_det(gcl[0] * x[0] + gcl[1] * x[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = lane + 64 * q;
+        if (i < n) {
+            Wk.dc[i] = x[q];
+            dcs[i] = x[q];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the LDS copy (not the dc store's acknowledgement)
+    __builtin_amdgcn_wave_barrier();
+    if (lane < G.n_kf) {
+        double* qd = Wk.pose[1 - cur] + 7 * lane;
+        if (fidx < 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) qd[i] = p7[i];
+        } else {
+            double qv[7];
+            se3_plus(p7, dcs + 6 * fidx, qv);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) qd[i] = qv[i];
+        }
+    }
+    if (lane == 0) k5_result(st, 1, d2, gd);
+}
+
+template <int NF>
+__global__ __launch_bounds__(64 * kBkWaves) void ba_camera_solve_blk(Geometry G, Prob Pr, Work Wk, int combine) {
+    camera_solve_blk_body<NF>(G, Pr, Wk, combine);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3020,6 +3219,19 @@ __global__ __launch_bounds__(kK5Threads) void bab_camera_solve(const WinDesc* __
     camera_solve_mfma_body<NF>(d.G, Pr, Wk, 1);
 }
 
+// the batched mode's K5 past 10 free keyframes: the 6x6-block solver of the window in row
+// blockIdx.x of the descriptor table
+template <int NF>
+__global__ __launch_bounds__(64 * kBkWaves) void bab_camera_solve_blk(const WinDesc* __restrict__ D, int wi) {
+    const WinDesc& d = D[blockIdx.x];
+    const int skip = d.skip;
+    const Prob Pr = d.Pr;
+    const Work& Wk = d.W[wi];
+    desc_touch(Pr.free_idx, Pr.dmap, Wk.pose[0], Wk.pose[1], Wk.cpart, Wk.partA, Wk.singular, Wk.st);
+    if (skip) return;
+    camera_solve_blk_body<NF>(d.G, Pr, Wk, 1);
+}
+
 __global__ __launch_bounds__(64) void bab_backsub_relinearize(const WinDesc* __restrict__ D, int wi) {
     const WinDesc& d = D[blockIdx.y];
     const int skip = d.skip, bound = d.G.n_wave;
@@ -3200,6 +3412,38 @@ __global__ __launch_bounds__(256) void ba_p2p_trial(Geometry G, Prob Pr, Work Wk
 
 RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 RSVIO_RT_READER(rsvio_dbg_ba_rt)
+
+// ======================================================================================
+// The observations' (u, v) into the staging image as f32 when every value is exactly an f32 (the
+// estimator's are: normalised coordinates unprojected from f32 pixels and stored as f32 features,
+// frame.rs:107-134 -> sliding_window.rs:274-300), halving the largest part of the window's PCIe
+// upload; false (nothing usable written) if one is not, and the caller copies the f64 values.
+__attribute__((target("avx2"))) static bool uv_narrow_avx2(size_t n2, const double* uv, float* out) {
+    size_t i = 0;
+    __m256d bad = _mm256_setzero_pd();
+    for (; i + 4 <= n2; i += 4) {
+        const __m256d d = _mm256_loadu_pd(uv + i);
+        const __m128 f = _mm256_cvtpd_ps(d);
+        bad = _mm256_or_pd(bad, _mm256_cmp_pd(_mm256_cvtps_pd(f), d, _CMP_NEQ_UQ));
+        _mm_storeu_ps(out + i, f);
+    }
+    bool ok = _mm256_movemask_pd(bad) == 0;
+    for (; i < n2; ++i) {
+        out[i] = (float)uv[i];
+        ok &= (double)out[i] == uv[i];
+    }
+    return ok;
+}
+static bool uv_narrow(size_t n2, const double* uv, float* out) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) return uv_narrow_avx2(n2, uv, out);
+    bool ok = true;
+    for (size_t i = 0; i < n2; ++i) {
+        out[i] = (float)uv[i];
+        ok &= (double)out[i] == uv[i];
+    }
+    return ok;
+}
 
 // ======================================================================================
 // set_problem's observation pass, fast path (host).  Keys l << 6 | k << 1 | c with the index
@@ -3531,6 +3775,7 @@ struct BundleAdjuster {
         size_t hdr, uv, pairs, total;  // built on the device
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
+    bool uv_env = true;         // RSVIO_BA_UV32=0: always upload (u, v) as f64 (A/B)
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
     // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
@@ -3602,6 +3847,8 @@ struct BundleAdjuster {
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
         prof_env = std::getenv("RSVIO_BA_PROFILE") != nullptr;
+        const char* u32v = std::getenv("RSVIO_BA_UV32");
+        uv_env = !(u32v && u32v[0] == '0');
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
@@ -3808,7 +4055,10 @@ struct BundleAdjuster {
             }
             if (cl >= 0) m2[cl] = cm;
         }
-        std::memcpy(hb + L.ouv, obs_uv, sizeof(double2) * (size_t)n_obs);
+        // (u, v) as f32 when exact (half the bytes to copy and to upload), else as given
+        const bool uv32 = uv_env && uv_narrow(2 * (size_t)n_obs, obs_uv, reinterpret_cast<float*>(hb + L.ouv));
+        if (!uv32) std::memcpy(hb + L.ouv, obs_uv, sizeof(double2) * (size_t)n_obs);
+        L.upload = L.ouv + al((uv32 ? sizeof(float2) : sizeof(double2)) * std::max(n_obs, 1));
         if (d_arena.n < L.upload) {  // (grown for the whole arena below once its size is known)
             d_arena.alloc(2 * L.upload);
         }
@@ -3865,7 +4115,11 @@ struct BundleAdjuster {
         std::memcpy(hb + L.free_idx, free_idx.data(), sizeof(int) * (size_t)n_kf);
         std::memcpy(hb + L.pb_fa, pb_fa.data(), sizeof(int) * (size_t)n_pb);
         std::memcpy(hb + L.pb_fb, pb_fb.data(), sizeof(int) * (size_t)n_pb);
-        mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
+        if (n_free <= 10)
+            mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap));
+        else  // the 6x6-block solver's padded template (13 / 16 / 20 free keyframes), leading dimension 129
+            mf_dense_map(n_free, n_pb, pb_fa.data(), pb_fb.data(), reinterpret_cast<int*>(hb + L.dmap),
+                         6 * bk_template_nf(n_free), kBkLd);
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
         for (int c = 0; c < 2; ++c)
@@ -3884,6 +4138,7 @@ struct BundleAdjuster {
             S.wave_fill = reinterpret_cast<const int*>(d_arena.p + L.wave_fill);
             S.key = reinterpret_cast<const unsigned*>(d_arena.p + L.key);
             S.uv = reinterpret_cast<const double2*>(d_arena.p + L.ouv);
+            S.uv32 = uv32 ? 1 : 0;
             S.wave_lm = reinterpret_cast<const int*>(d_arena.p + L.wave_lm);
             S.nb_lm = (n_lm + 255) / 256;
             S.nb_pad = (int)((n_pad + 255) / 256);
@@ -3976,6 +4231,15 @@ struct BundleAdjuster {
             RSVIO_CAM(6) RSVIO_CAM(7) RSVIO_CAM(8) RSVIO_CAM(9) RSVIO_CAM(10)
 #undef RSVIO_CAM
             default: {
+                if (k5_variant == 2) {  // the 6x6-block solver with MFMA updates (the default)
+                    const dim3 b3(64 * kBkWaves);
+                    switch (bk_template_nf(G.n_free)) {
+                        case 13: hipLaunchKernelGGL(ba_camera_solve_blk<13>, g, b3, 0, stream, G, pr, wk, combine); break;
+                        case 16: hipLaunchKernelGGL(ba_camera_solve_blk<16>, g, b3, 0, stream, G, pr, wk, combine); break;
+                        default: hipLaunchKernelGGL(ba_camera_solve_blk<20>, g, b3, 0, stream, G, pr, wk, combine); break;
+                    }
+                    break;
+                }
                 const dim3 b2(64 * kX2Waves);
                 if (G.n_free <= 13) hipLaunchKernelGGL(ba_camera_solve_x2<13>, g, b2, 0, stream, G, pr, wk, combine);
                 else if (G.n_free <= 16) hipLaunchKernelGGL(ba_camera_solve_x2<16>, g, b2, 0, stream, G, pr, wk, combine);
@@ -4533,7 +4797,10 @@ struct BundleBatch {
             RSVIO_BAB(1) RSVIO_BAB(2) RSVIO_BAB(3) RSVIO_BAB(4) RSVIO_BAB(5)
             RSVIO_BAB(6) RSVIO_BAB(7) RSVIO_BAB(8) RSVIO_BAB(9) RSVIO_BAB(10)
 #undef RSVIO_BAB
-            default: throw std::invalid_argument("batched mode: at most 10 free keyframes per window");
+            case 13: hipLaunchKernelGGL(bab_camera_solve_blk<13>, dim3(B), dim3(64 * kBkWaves), 0, stream, d_desc.p, wi); break;
+            case 16: hipLaunchKernelGGL(bab_camera_solve_blk<16>, dim3(B), dim3(64 * kBkWaves), 0, stream, d_desc.p, wi); break;
+            case 20: hipLaunchKernelGGL(bab_camera_solve_blk<20>, dim3(B), dim3(64 * kBkWaves), 0, stream, d_desc.p, wi); break;
+            default: throw std::logic_error("batched mode: no camera-solve template for this window size");
         }
         RSVIO_HIP(hipGetLastError());
     }
@@ -4558,7 +4825,8 @@ struct BundleBatch {
             max_chunk = std::max(max_chunk, G.n_chunk);
             ne_total += (size_t)36 * G.n_pb + 12 * G.n_free;
         }
-        if (nf > 10) throw std::invalid_argument("batched mode: at most 10 free keyframes per window");
+        // past 10 free keyframes every window runs the 6x6-block solver's padded template
+        if (nf > 10) nf = bk_template_nf(nf);
         max_wave = (max_wave + kGrp - 1) / kGrp * kGrp;  // wave w on XCD w % 8 in every window
         // descriptors and the camera-solve maps for the batch's template (b row at 6 nf)
         if (h_dmap.n < std::max<size_t>(ne_total, 1)) {
@@ -4580,7 +4848,8 @@ struct BundleBatch {
             d.W[3] = w.work_at(1);
             if (skip[i]) continue;
             const size_t ne = (size_t)36 * w.G.n_pb + 12 * w.G.n_free;
-            mf_dense_map(w.G.n_free, w.G.n_pb, w.hs_pb_fa.data(), w.hs_pb_fb.data(), h_dmap.p + off, 6 * nf);
+            mf_dense_map(w.G.n_free, w.G.n_pb, w.hs_pb_fa.data(), w.hs_pb_fb.data(), h_dmap.p + off, 6 * nf,
+                         nf > 10 ? kBkLd : kMfLd);
             d.Pr.dmap = d_dmap.p + off;
             off += ne;
         }

@@ -243,7 +243,9 @@ class BAProblem:
 def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int = 7,
                noise_px: float = 0.5, init_seed: int = 11, pose_noise=(0.02, math.radians(0.5)),
                depth_noise: float = 0.05) -> BAProblem:
-    """Config 3 (and, with other arguments, config 5's shape)."""
+    """Config 3 (and, with other arguments, config 5's shape).  The observations are f32 values
+    widened to f64, as the reference's are: SlidingWindow::optimize builds each factor from a
+    feature's f32 undistorted_coord cast to f64 (sliding_window.rs:276)."""
     rng = np.random.default_rng(seed)
     T_W_B = []
     for k in range(n_kf):
@@ -287,7 +289,8 @@ def ba_problem(n_kf: int = 10, n_lm: int = 2000, kf_per_lm: int = 6, seed: int =
     p_W = np.ascontiguousarray(p_W)
     return BAProblem(pose7=pose7, kf_fixed=kf_fixed, p_W=p_init,
                      obs_lm=np.asarray(obs_lm, np.int32), obs_kf=np.asarray(obs_kf, np.int32),
-                     obs_cam=np.asarray(obs_cam, np.uint8), obs_uv=np.asarray(obs_uv, np.float64),
+                     obs_cam=np.asarray(obs_cam, np.uint8),
+                     obs_uv=np.asarray(obs_uv, np.float64).astype(np.float32).astype(np.float64),
                      T_C_B2=np.stack([T_C_B[0].reshape(16), T_C_B[1].reshape(16)]),
                      true_pose7=true_pose7, true_p_W=p_W)
 

@@ -200,12 +200,13 @@ def test_window_sizes_match_oracle(gpu, oracle, n_kf):
 
 
 @pytest.mark.parametrize("variant", ["pipe4", "gj1"])
-@pytest.mark.parametrize("n_kf", [2, 3, 4, 5, 7, 8, 10, 11])
+@pytest.mark.parametrize("n_kf", [2, 3, 4, 5, 7, 8, 10, 11, 14, 21])
 def test_camera_solve_variants_match_oracle(gpu, oracle, monkeypatch, variant, n_kf):
-    """The K5 A/B variants (RSVIO_K5, read at handle creation) for 1..10 free keyframes: the
-    pipelined 4-wave VALU LDL^T and the one-wave Gauss-Jordan solve give the oracle's status and
-    iteration count and its state within the stated tolerances, and the camera step of one
-    system within 1e-9 of the default blocked LDL^T with MFMA trailing updates."""
+    """The K5 A/B variants (RSVIO_K5, read at handle creation): the pipelined VALU LDL^T (one row
+    per lane up to 10 free keyframes, two rows per lane past them) and the one-wave Gauss-Jordan
+    solve give the oracle's status and iteration count and its state within the stated
+    tolerances, and the camera step of one system within 1e-9 of the default MFMA solve (8-column
+    panels up to 10 free keyframes, 6x6 block pivots past them)."""
     from rsvio import synthetic as S
     if variant == "gj1" and n_kf > 10:
         pytest.skip("gj1 is instantiated up to 9 free keyframes")
@@ -662,6 +663,35 @@ def test_batched_windows_match_single_and_oracle(gpu, oracle):
             po, pwo, ro = oracle.ba_solve(pr)
             assert r.status == ro.status and r.iterations == ro.iterations, i
             assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6, i
+    batch.close()
+    for w in wins:
+        w.close()
+
+
+def test_batched_windows_past_ten_free_keyframes(gpu, oracle):
+    """Batched mode with windows of 13, 16 and 20 free keyframes (the batch's K5 is the 6x6-block
+    MFMA solver's padded template, bab_camera_solve_blk<20>) next to a 3-free-keyframe window padded
+    to the same template: every window equals its own single-handle solve (status, iterations,
+    state within 1e-9) and the oracle's solve within the stated tolerances."""
+    from rsvio import synthetic as S
+    from rsvio.ba import BundleBatch
+    shapes = [(4, 90, 3), (14, 300, 5), (17, 200, 4), (21, 400, 6)]
+    probs = [S.ba_problem(n_kf=k, n_lm=m, kf_per_lm=p, seed=900 + i, init_seed=950 + i)
+             for i, (k, m, p) in enumerate(shapes)]
+    wins = [_adjuster(gpu, pr) for pr in probs]
+    batch = BundleBatch(wins)
+    res = batch.run()
+    for i, (w, pr, r) in enumerate(zip(wins, probs, res)):
+        pose, pw = w.state()
+        one = _adjuster(gpu, pr)
+        r1 = one.run()
+        p1, w1 = one.state()
+        one.close()
+        assert (r.status, r.iterations) == (r1.status, r1.iterations), i
+        assert np.abs(pose - p1).max() <= 1e-9 and np.abs(pw - w1).max() <= 1e-9, i
+        po, pwo, ro = oracle.ba_solve(pr)
+        assert r.status == ro.status and r.iterations == ro.iterations, i
+        assert np.abs(pose - po).max() < 1e-7 and np.abs(pw - pwo).max() < 1e-6, i
     batch.close()
     for w in wins:
         w.close()
