@@ -696,6 +696,9 @@ class TrackerWorkload:
         self.stream = (torch.cuda.ExternalStream(stream_ptr, device=dev) if stream_ptr
                        else torch.cuda.current_stream(dev))
         self.ev = []
+        # per-frame enqueue as captured graphs (_capture; --tracker-graphs), built on first use
+        self.graphs = False
+        self._graphs, self._graph_objs = {}, []
         # prime: pyramids of the first frame
         self._pyramids(self.seq[0], self.slot)
 
@@ -777,10 +780,27 @@ class TrackerWorkload:
         assert self.slot == phase % 2
         plan = self._plan(phase, pcie)
         s = self.stream.cuda_stream
+        timed = timed and self.k % 4 == 0  # LK launch time sampled on every 4th frame (event overhead)
+        if self.graphs and not timed:
+            # the frame's copies and kernels as one captured graph per (phase, pcie, uploaded):
+            # one hipGraphLaunch instead of up to five enqueue calls (the same work, the same order)
+            key = (phase, pcie, uploaded)
+            ex = self._graphs.get(key)
+            if ex is None:
+                ex = self._capture(plan, pcie, uploaded, s)
+                self._graphs[key] = ex
+            self.L.check(self._graph_launch(ex, s))
+            if pcie:
+                self.L.check(self._ev_record(self._done_ev, s))
+                self._pending = True
+                if wait:
+                    self.sync()
+            self.slot = 1 - self.slot
+            self.k += 1
+            return
         if pcie and not uploaded:
             self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, s))
         self.L.check(self.lib.rsvio_build_pyramids_d(self.ctx, plan["src"], 2, plan["dst"], s))
-        timed = timed and self.k % 4 == 0  # LK launch time sampled on every 4th frame (event overhead)
         if timed:
             e0 = self.torch.cuda.Event(enable_timing=True)
             e1 = self.torch.cuda.Event(enable_timing=True)
@@ -798,6 +818,35 @@ class TrackerWorkload:
                 self.sync()
         self.slot = 1 - self.slot
         self.k += 1
+
+    def _capture(self, plan, pcie, uploaded, s):
+        """Capture the frame's enqueue sequence on the tracker stream (relaxed mode) into an
+        instantiated graph executable."""
+        C = self.C
+        lib = self.lib
+        if not hasattr(self, "_graph_launch"):
+            for name, res, args in (("hipStreamBeginCapture", C.c_int, [C.c_void_p, C.c_int]),
+                                    ("hipStreamEndCapture", C.c_int, [C.c_void_p, C.c_void_p]),
+                                    ("hipGraphInstantiate", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                                      C.c_size_t]),
+                                    ("hipGraphLaunch", C.c_int, [C.c_void_p, C.c_void_p])):
+                f = getattr(lib, name)
+                f.restype, f.argtypes = res, args
+            self._graph_launch = lib.hipGraphLaunch
+        self.L.check(lib.hipStreamBeginCapture(s, 2))  # hipStreamCaptureModeRelaxed
+        if pcie and not uploaded:
+            self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, s))
+        self.L.check(lib.rsvio_build_pyramids_d(self.ctx, plan["src"], 2, plan["dst"], s))
+        self.L.check(lib.rsvio_track_points_d(self.ctx, plan["batches"], 3, MAX_IT, C.c_float(THRESH), s))
+        if pcie:
+            self.L.check(self._memcpy(self.h_out.data_ptr(), self.out.data_ptr(), self.out.numel() * 4, 2, s))
+            self.L.check(self._memcpy(self.h_valid.data_ptr(), self.valid.data_ptr(), self.valid.numel(), 2, s))
+        g = C.c_void_p()
+        self.L.check(lib.hipStreamEndCapture(s, C.byref(g)))
+        ex = C.c_void_p()
+        self.L.check(lib.hipGraphInstantiate(C.byref(ex), g, None, None, 0))
+        self._graph_objs.append(g)
+        return ex
 
     def sync(self):
         if getattr(self, "_pending", False):
@@ -826,6 +875,16 @@ class TrackerWorkload:
             destroy.argtypes = [self.C.c_void_p]
             destroy(self._done_ev)
             self._done_ev = None
+        if self._graphs or self._graph_objs:
+            C = self.C
+            for name in ("hipGraphExecDestroy", "hipGraphDestroy"):
+                f = getattr(self.lib, name)
+                f.restype, f.argtypes = C.c_int, [C.c_void_p]
+            for ex in self._graphs.values():
+                self.lib.hipGraphExecDestroy(ex)
+            for g in self._graph_objs:
+                self.lib.hipGraphDestroy(g)
+            self._graphs, self._graph_objs = {}, []
         if self.ctx:
             self.lib.rsvio_track_ctx_destroy(self.ctx)
             self.ctx = None
@@ -1071,6 +1130,9 @@ def main():
                          "profiles/r05h_order_ab.txt -- the image and window uploads share the copy engine, and "
                          "the image then lands first without holding the window back behind the frame's kernels "
                          "enqueue); both paths run concurrently either way (the tracker does not depend on the solve)")
+    ap.add_argument("--tracker-graphs", type=int, default=1,
+                    help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
+                         "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "p2p"],
                     help="BA exchange for N>1: P2P one-shot all-reduce (auto: if every rank attaches) or RCCL")
     ap.add_argument("--same-device", action="store_true",
@@ -1096,6 +1158,7 @@ def main():
         streams = [CuStream(local, cu_trk), CuStream(local, cu_ba)]
         log(f"[bench] CU partition ({args.cu_layout}): tracker {len(cu_trk)} CUs, BA {len(cu_ba)} CUs")
     trk = TrackerWorkload(local, streams[0].ptr if streams else None)
+    trk.graphs = bool(args.tracker_graphs)
     ba = BAWorkload(local, world, rank, streams[1].ptr if streams else None, args.collective,
                     rccl_ok=not args.same_device)
 

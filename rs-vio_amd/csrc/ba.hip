@@ -307,6 +307,32 @@ __device__ __forceinline__ void p2p_group_sums(const double* mine, int nr, int n
     }
 }
 
+// p2p_group_sums with this rank's own contribution taken from registers (own[i], substituted at
+// rank `me` in the rank order: the same adds, the same bits): only the PEERS' slots are read
+// from the uncached exchange buffer, and at one rank nothing is
+template <int KE, int W>
+__device__ __forceinline__ void p2p_group_sums_own(const double* mine, int nr, int me, int ne, int tid, int T,
+                                                   const double (&own)[KE], double (&sums)[KE]) {
+    for (int r0 = 0; r0 < nr; r0 += W) {
+        double v[KE][W];
+#pragma unroll
+        for (int i = 0; i < KE; ++i)
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const int r = r0 + q;
+                v[i][q] = (r < nr && r != me)
+                              ? __hip_atomic_load(mine + (size_t)r * kP2PMsg + min(tid + T * i, ne - 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                              : own[i];
+            }
+#pragma unroll
+        for (int i = 0; i < KE; ++i)
+#pragma unroll
+            for (int q = 0; q < W; ++q)
+                if (r0 + q < nr) sums[i] += v[i][q];
+    }
+}
+
 // flag-in-word slot [parity][source rank] (2 kP2PLLMax words)
 __device__ __forceinline__ unsigned long long* p2p_ll(double* xbuf, int par, int r) {
     return reinterpret_cast<unsigned long long*>(xbuf + kP2PLL) + ((size_t)par * kP2PMax + r) * 2 * kP2PLLMax;
@@ -353,6 +379,13 @@ __device__ __forceinline__ bool ll_group_sums(const unsigned long long* mine, in
                     acc[i] += __longlong_as_double((long long)((w[i][q][0] & 0xffffffffull) | (w[i][q][1] << 32)));
     }
     return late;
+}
+
+template <int SCOPE>
+__device__ __forceinline__ void ll_put_scope(unsigned long long* w, double v, unsigned g) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)g << 32;
+    __hip_atomic_store(w, (b & 0xffffffffull) | t, __ATOMIC_RELAXED, SCOPE);
+    __hip_atomic_store(w + 1, (b >> 32) | t, __ATOMIC_RELAXED, SCOPE);
 }
 
 __device__ __forceinline__ void ll_put(unsigned long long* w, double v, unsigned g) {
@@ -1892,35 +1925,46 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     const unsigned long long gen = sgen;
     const int par = (int)(gen & 1);
     if (P.ll) return combine_p2p_ll<NF>(G, Wk, M, gsh, fail, P, xgen, err, v, dst, pa, sing, lambda, gen);
+    // this rank's entries stay in registers (own): only the peers' slots are written, flagged,
+    // waited for and read back (round 5; the own slot's uncached write, flag and re-read were the
+    // exchange's whole cost at one rank)
+    double own[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
-        if (e >= ne) break;
         double a = v[i][0];
 #pragma unroll
         for (int x = 1; x < kGrp; ++x) a += v[i][x];
         if (me == 0 && dst[i] >= 0 && (dst[i] & kMfMapLambda)) a += lambda;
-        for (int r = 0; r < nr; ++r) p2p_slot(P.peer[r], par, me)[e] = a;
+        own[i] = a;
+        if (e < ne)
+            for (int r = 0; r < nr; ++r)
+                if (r != me) p2p_slot(P.peer[r], par, me)[e] = a;
     }
+    __shared__ double osc[2];  // this rank's initial cost and singular flag
     if (tid < 64) {
         double c = 0.0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c += pa[k];
         for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
         c = wave_sum_det(c);
-        if (tid < nr) {  // lane r pushes the scalars to rank r
+        if (tid == 0) {
+            osc[0] = c;
+            osc[1] = sing ? 1.0 : 0.0;
+        }
+        if (tid < nr && tid != me) {  // lane r pushes the scalars to rank r
             double* d = p2p_slot(P.peer[tid], par, me);
             d[ne] = c;
             d[ne + 1] = sing ? 1.0 : 0.0;
             d[ne + 2] = (double)G.n_wave;  // (per rank, not summed: the folded trial exchange's bound)
         }
     }
-    __threadfence_system();
+    if (nr > 1) __threadfence_system();
     __syncthreads();
-    if (tid < nr)
+    if (tid < nr && tid != me)
         __hip_atomic_store(p2p_flags(P.peer[tid]) + par * kP2PMax + me, gen, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid < nr) {
+    if (tid < nr && tid != me) {
         const unsigned long long* f = p2p_flags(P.peer[me]) + par * kP2PMax + tid;
         long long spins = 0;
         while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
@@ -1933,16 +1977,16 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     }
     __syncthreads();
     const double* mine = p2p_slot(P.peer[me], par, 0);
-    // this thread's values from a group of ranks in flight together (clamped indices; only real
-    // entries of real ranks are added), groups in rank order: one round trip per group of 2 (two
-    // ranks) or 4 ranks, then the rank-ordered sums
+    // this thread's values from a group of ranks in flight together (own from registers, peers'
+    // from their slots), groups in rank order: one round trip per group of 2 (two ranks) or 4
+    // ranks, then the rank-ordered sums
     double sums[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) sums[i] = 0.0;
     if (nr <= 2)
-        p2p_group_sums<kE, 2>(mine, nr, ne, tid, T, sums);
+        p2p_group_sums_own<kE, 2>(mine, nr, me, ne, tid, T, own, sums);
     else
-        p2p_group_sums<kE, 4>(mine, nr, ne, tid, T, sums);
+        p2p_group_sums_own<kE, 4>(mine, nr, me, ne, tid, T, own, sums);
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;
@@ -1955,16 +1999,33 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
             gsh[-2 - d] = a;
     }
     if (tid == 0) {
+        // every peer's two scalars in flight together (unrolled over the rank bound), then the
+        // rank-ordered sums with this rank's own values substituted
+        double cv[kP2PMax], fv[kP2PMax];
+#pragma unroll
+        for (int r = 0; r < kP2PMax; ++r) {
+            const bool peer = r < nr && r != me;
+            cv[r] = peer ? __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                         : osc[0];
+            fv[r] = peer ? __hip_atomic_load(mine + (size_t)r * kP2PMsg + ne + 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM)
+                         : osc[1];
+        }
         double c = 0.0, f = 0.0;
-        p2p_rank_sum(mine, nr, ne, c);
-        p2p_rank_sum(mine, nr, ne + 1, f);
+#pragma unroll
+        for (int r = 0; r < kP2PMax; ++r)
+            if (r < nr) {
+                c += cv[r];
+                f += fv[r];
+            }
         Wk.sys[ne] = c;  // the decision of iteration 0 reads the (all-reduced) initial cost here
         *fail = f != 0.0;
         *xgen = gen;
     }
     if (tid < nr && P.xnw)
-        P.xnw[tid] = (int)__hip_atomic_load(mine + (size_t)tid * kP2PMsg + ne + 2, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_SYSTEM);
+        P.xnw[tid] = tid == me ? G.n_wave
+                               : (int)__hip_atomic_load(mine + (size_t)tid * kP2PMsg + ne + 2, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM);
     return false;
 }
 
@@ -2902,7 +2963,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
 template <bool FUSED>
 __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w, int lane, double (*sh)[64],
                         double (*shp)[64], double (*shs)[64], const P2P* PP = nullptr,
-                        unsigned long long gen = 0) {
+                        unsigned long long gen = 0, unsigned long long* k6tag = nullptr) {
     // sh: W_s^T dc_f per slot, then the linearisation scratch; shp: trial point at the
     // landmark's first lane; shs: per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int s = 64 * w + lane;
@@ -3034,6 +3095,18 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w
         if (lane == 0)
 #pragma unroll
             for (int i = 0; i < kPartD; ++i) Wk.partD[w * kPartD + i] = v[i];
+        if (k6tag && lane < kPartD) {  // the reducer's copy, flag-in-word at device scope (fold 3):
+            // word-major planes (word q of every wave contiguous), so the reducer's polls coalesce
+            double vl = v[0];
+#pragma unroll
+            for (int i = 1; i < kPartD; ++i) vl = lane == i ? v[i] : vl;
+            const unsigned long long b = (unsigned long long)__double_as_longlong(vl), t = gen << 32;
+            const size_t nw = (size_t)G.n_wave;
+            __hip_atomic_store(k6tag + (2 * lane) * nw + w, (b & 0xffffffffull) | t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(k6tag + (2 * lane + 1) * nw + w, (b >> 32) | t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (PP && lane < PP->nranks) {  // folded trial exchange: lane r pushes this wave's partial to rank r
             const int par = (int)(gen & 1);
             double* q = p2p_tval(PP->peer[lane], par, PP->rank, w);
@@ -3067,6 +3140,140 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p(Geometry G, Pro
     unsigned long long gen = *xgen;
     __asm__ volatile("" : "+s"(gen));  // loaded with the kernel's first loads, not at its end
     k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs, &P, gen);
+}
+
+// Fold 3 (round 5, the default P2P iteration: K4c, K5 with the system exchange, K6 -- three
+// launches, no X2): K6's workgroup n_wave is the REDUCER.  Every K6 wave writes its 4 partials
+// flag-in-word at device scope (k6tag, tag = this trial exchange's generation); the reducer polls
+// them, sums them exactly as trial_scalars_wave does (the same lane-strided accumulation and
+// fixed-pairing wave sums, + |x|^2 of the free poses on rank 0), pushes the 4 scalars to every
+// peer flag-in-word (the X2 exchange's slots and generation), polls the peers', and writes the
+// rank-ordered sums to trial4 -- the same bits X2 wrote, read by the next K4c / K7 after the
+// boundary.  It is dispatched last, after every wave it waits for (all of K6 is co-resident), and
+// its spins are bounded like every exchange's (the error flag the host checks).
+__device__ void k6_reduce_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, const P2P& P,
+                              unsigned long long* xgen, int* err, const unsigned long long* k6tag) {
+    const int lane = threadIdx.x & 63;
+    const LmState s = *Wk.st;
+    const unsigned long long gen = *xgen + 1;  // (X2's: the exchange after K5's)
+    if (s.done) return;
+    const unsigned g32 = (unsigned)gen;
+    const int nr = P.nranks, me = P.rank, par = (int)(gen & 1);
+    // the poses' |x|^2 (trial_scalars_wave's loads and sums)
+    const int el = 7 * G.n_kf - 1;
+    double p0[3], p1[3];
+    int fi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int e = min(lane + 64 * k, el);
+        fi[k] = Pr.free_idx[e / 7];
+        p0[k] = Wk.pose[0][e];
+        p1[k] = Wk.pose[1][e];
+    }
+    constexpr int kU = 8;
+    double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
+    bool late = false;
+    if (s.solve_ok) {  // (no step: K6's waves returned early, the partials are zeros)
+        for (int i0 = 0; i0 < max(G.n_wave, 64 * kU); i0 += 64 * kU) {
+            // this lane's waves i0 + lane + 64 k, polled together until every tag is this exchange's
+            unsigned long long wd[kU][kPartD][2];
+            long long spins = 0;
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    const int wv = i0 + lane + 64 * k;
+                    const size_t nw = (size_t)G.n_wave;
+                    const unsigned long long* a = k6tag + min(wv, max(G.n_wave - 1, 0));
+#pragma unroll
+                    for (int j = 0; j < kPartD; ++j) {
+                        wd[k][j][0] = __hip_atomic_load(a + (2 * j) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        wd[k][j][1] = __hip_atomic_load(a + (2 * j + 1) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+#pragma unroll
+                    for (int j = 0; j < kPartD; ++j)
+                        ok &= wv >= G.n_wave || ((unsigned)(wd[k][j][0] >> 32) == g32 && (unsigned)(wd[k][j][1] >> 32) == g32);
+                }
+                if (__all(ok)) break;
+                if (++spins > (1ll << 25)) {
+                    late = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+#pragma unroll
+            for (int k = 0; k < kU; ++k)
+                if (i0 + lane + 64 * k < G.n_wave)
+#pragma unroll
+                    for (int j = 0; j < kPartD; ++j)
+                        acc[j] += __longlong_as_double((long long)((wd[k][j][0] & 0xffffffffull) | (wd[k][j][1] << 32)));
+        }
+    }
+    double sq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (me == 0 && lane + 64 * k <= el && fi[k] >= 0) {
+            sq[0] += p0[k] * p0[k];
+            sq[1] += p1[k] * p1[k];
+        }
+    acc[3] += sq[s.cur];
+    double out[kPartD];
+#pragma unroll
+    for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
+    // the exchange (X2's flag-in-word protocol): lane 4 r + i pushes value i to rank r, then polls
+    // rank r's value i in this rank's buffer; this rank's own from registers
+    const int r = lane >> 2, i = lane & 3;
+    double mv = out[0];
+#pragma unroll
+    for (int k = 1; k < kPartD; ++k) mv = i == k ? out[k] : mv;
+    double got = mv;
+    if (r < nr && r != me) {
+        ll_put(p2p_ll(P.peer[r], par, me) + 2 * i, mv, g32);
+        const unsigned long long* w = p2p_ll(P.peer[me], par, r) + 2 * i;
+        long long spins = 0;
+        for (;;) {
+            const unsigned long long a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((unsigned)(a >> 32) == g32 && (unsigned)(b >> 32) == g32) {
+                got = __longlong_as_double((long long)((a & 0xffffffffull) | (b << 32)));
+                break;
+            }
+            if (++spins > (1ll << 25)) {
+                late = true;
+                got = 0.0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (late) atomicExch(err, 1);
+    double v4[kPartD];
+#pragma unroll
+    for (int k = 0; k < kPartD; ++k) {
+        double v = 0.0;
+        for (int q = 0; q < nr; ++q) v += rl64(got, 4 * q + k);  // rank order from 0.0: X2's sum
+        v4[k] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kPartD; ++k) Wk.trial4[k] = v4[k];
+        *xgen = gen;
+    }
+}
+
+__global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p3(Geometry G, Prob Pr, Work Wk, P2P P,
+                                                                  unsigned long long* xgen, int* err,
+                                                                  unsigned long long* k6tag) {
+    __shared__ double sh[10][64];
+    __shared__ double shp[3][64];
+    __shared__ double shs[4][64];
+    if ((int)blockIdx.x == G.n_wave) {
+        k6_reduce_p2p(G, Pr, Wk, P, xgen, err, k6tag);
+        return;
+    }
+    unsigned long long gen = *xgen + 1;
+    __asm__ volatile("" : "+s"(gen));  // loaded with the kernel's first loads, not at its end
+    k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs, nullptr, gen, k6tag);
 }
 
 // K6r (sharded): this rank's trial scalars (|x|^2 of the poses on the owner rank) -> trial4,
@@ -3633,7 +3840,8 @@ struct BundleAdjuster {
     int fold_req = 1;             // the level asked for (RSVIO_P2P_FOLD); attach_p2p may lower fold_lvl
     bool p2p_shared_gpu = false;  // attach_p2p found two ranks on one device (fold 2 -> 1)
     bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
-    bool p2p_fold2() const { return fold_lvl >= 2 && p2p_fold(); }
+    bool p2p_fold2() const { return fold_lvl == 2 && p2p_fold(); }
+    bool p2p_fold3() const { return fold_lvl == 3 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
     void fill_desc(WinDesc& d) const {
         d = WinDesc{};
@@ -3808,6 +4016,7 @@ struct BundleAdjuster {
     DevBuf<int> d_p2p_err;
     DevBuf<unsigned long long> d_xgen;  // P2P exchange generation (advanced on the device)
     DevBuf<int> d_xnw;                  // every rank's wave count (K5's exchange carries it)
+    DevBuf<unsigned long long> d_k6tag; // fold 3: K6 wave partials, flag-in-word (2 kPartD words per wave)
 
     void init(const rsvio_ba_params& p) {
         P = p;
@@ -3823,7 +4032,7 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
         const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0" / "1" / "2" (A/B switch)
-        if (fv && fv[0] >= '0' && fv[0] <= '2') fold_lvl = fold_req = fv[0] - '0';
+        if (fv && fv[0] >= '0' && fv[0] <= '3') fold_lvl = fold_req = fv[0] - '0';
         const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
         desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
@@ -3945,6 +4154,10 @@ struct BundleAdjuster {
         grow(d_dc, (size_t)6 * n_free);
         grow(d_trial4, 4);
         grow(d_state, 2);
+        if (d_k6tag.n < (size_t)2 * kPartD * std::max(n_wave, 1)) {  // fold 3's tagged K6 partials
+            grow(d_k6tag, (size_t)2 * kPartD * std::max(n_wave, 1));
+            RSVIO_HIP(hipMemsetAsync(d_k6tag.p, 0, sizeof(unsigned long long) * d_k6tag.n, stream));
+        }
     }
 
     void set_problem(int n_kf, const double* pose7, const uint8_t* kf_fixed, int n_lm, const double* pW, int n_obs,
@@ -4096,7 +4309,7 @@ struct BundleAdjuster {
         int stride = 1;
         for (int x = 0; x < kGrp; ++x) stride = std::max(stride, gl[x]);
         n_pad = (size_t)64 * n_wave;
-        if (coll == 2 && fold_lvl >= 2 && n_wave > kP2PWaves)  // (every rank must take the same path)
+        if (coll == 2 && fold_lvl == 2 && n_wave > kP2PWaves)  // (every rank must take the same path)
             throw std::invalid_argument("shard exceeds the folded P2P trial exchange (16384 waves): RSVIO_P2P_FOLD=1");
         mark();
         // device-built part of the arena
@@ -4286,6 +4499,12 @@ struct BundleAdjuster {
             if (G.n_wave)
                 hipLaunchKernelGGL(ba_backsub_relinearize_p2p, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, p2p,
                                    d_xgen.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
+        if (p2p_fold3()) {  // K6 + its reducer workgroup: the trial exchange without X2
+            hipLaunchKernelGGL(ba_backsub_relinearize_p2p3, dim3(G.n_wave + 1), dim3(64), 0, stream, G, pr, wk, p2p,
+                               d_xgen.p, d_p2p_err.p, d_k6tag.p);
             RSVIO_HIP(hipGetLastError());
             return;
         }
@@ -4561,7 +4780,7 @@ struct BundleAdjuster {
         // (RSVIO_P2P_FOLD_SHARED=1 keeps fold 2 anyway: the A/B test of its sums on one GPU)
         const char* fsv = std::getenv("RSVIO_P2P_FOLD_SHARED");
         const bool keep2 = fsv && fsv[0] == '1';
-        fold_lvl = shared_gpu && fold_req >= 2 && !keep2 ? 1 : fold_req;
+        fold_lvl = shared_gpu && fold_req == 2 && !keep2 ? 1 : fold_req;
         p2p_shared_gpu = shared_gpu;
         p2p = P;
         nranks = nr;

@@ -28,20 +28,36 @@ def worker(rank, world, port, reps):
         from rsvio.ba import BundleAdjuster
         shard = S.ba_problem(n_lm=2000 * world).shard(rank, world)
         ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
-        handles = [None] * world
-        dist.all_gather_object(handles, ba.p2p_export(world))
-        ba.attach_p2p(world, rank, handles)
-        lat = {n: ba.p2p_latency_us(200, n) for n in (4, 1600)}
-        print(f"rank {rank}: exchange latency us {lat}", flush=True)
+        # PROBE_CU_SPLIT=f: the BA on bench.py's CU partition (the CUs past the tracker's block
+        # fraction f), so sharded and unsharded chains compare on the same CUs as the headline
+        split = float(os.environ.get("PROBE_CU_SPLIT", "0"))
+        cs = None
+        if split > 0:
+            import bench
+            from rsvio._lib import CuStream
+            _, cu_ba = bench.cu_partition(0, split, "block")
+            cs = CuStream(0, cu_ba)
+            ba.set_stream(cs.ptr)
+        # PROBE_SINGLE=1: the unsharded single-rank chain (no exchange attached) on the same stream
+        single = os.environ.get("PROBE_SINGLE", "0") == "1"
+        if not single:
+            handles = [None] * world
+            dist.all_gather_object(handles, ba.p2p_export(world))
+            ba.attach_p2p(world, rank, handles)
+            lat = {n: ba.p2p_latency_us(200, n) for n in (4, 1600)}
+            print(f"rank {rank}: exchange latency us {lat}", flush=True)
         ba.set_problem_from(shard)
         ms = []
         for k in range(reps + 3):
             r = ba.run()
             if k >= 3:
                 ms.append(r.solve_ms / max(r.iterations, 1))
-        print(f"rank {rank}: fold {os.environ.get('RSVIO_P2P_FOLD', '1')} ll {os.environ.get('RSVIO_P2P_LL', '0')} status {r.status} it {r.iterations} "
+        mode = "single (unsharded)" if single else f"fold {os.environ.get('RSVIO_P2P_FOLD', '1')}"
+        print(f"rank {rank}: {mode} cu_split {split} ll {os.environ.get('RSVIO_P2P_LL', '0')} status {r.status} it {r.iterations} "
               f"ms/iter median {float(np.median(ms)):.4f} min {min(ms):.4f}", flush=True)
         ba.close()
+        if cs is not None:
+            cs.close()
         dist.barrier()
     finally:
         dist.destroy_process_group()
