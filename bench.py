@@ -1140,8 +1140,9 @@ def main():
     args = ap.parse_args()
     if args.same_device:
         args.collective = "p2p"
-        # (ranks sharing one GPU never take the 3-launch A/B iteration RSVIO_P2P_FOLD=2: attach_p2p
-        # sees the shared device and lowers it to the default 4-launch one)
+        # (ranks sharing one GPU never take the iterations whose next decision waits in K4c,
+        # RSVIO_P2P_FOLD=2 and 4: attach_p2p sees the shared device and lowers them to 1 and 3,
+        # DESIGN.md section 8)
 
     world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:
@@ -1302,7 +1303,7 @@ def main():
     }
     if world > 1:
         out["ba_exchange"] = {"collective": ba.collective, "p2p_latency_us": ba.p2p_us,
-                              "fold": os.environ.get("RSVIO_P2P_FOLD", "1") if ba.collective == "p2p" else None,
+                              "fold": os.environ.get("RSVIO_P2P_FOLD", "3") if ba.collective == "p2p" else None,
                               "flag_in_word_system": os.environ.get("RSVIO_P2P_LL", "0") == "1"
                               if ba.collective == "p2p" else None}
     if rank == 0 and not args.no_rows:

@@ -369,7 +369,13 @@ __device__ __forceinline__ bool ll_group_sums(const unsigned long long* mine, in
                 late = true;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            // back off after the first polls: every re-poll reads all KE x W x 2 words of every
+            // thread from uncached memory, and on a GPU the ranks share (the rehearsals) a tight
+            // loop starves the late rank whose words it waits for
+            if (spins > 4)
+                __builtin_amdgcn_s_sleep(16);
+            else
+                __builtin_amdgcn_s_sleep(1);
         }
 #pragma unroll
         for (int i = 0; i < KE; ++i)
@@ -1004,7 +1010,38 @@ __device__ LmState lm_decide(const Geometry& G, const Prob& Pr, const Work& Wk, 
     // in flight together with the state's (one round trip) -- except from the P2P exchange
     // (pre_reduced 2), which waits for flags only a pending decision has
     double tv[4];
-    if (pre_reduced == 2) {
+    if (pre_reduced == 4) {
+        // fold 4: every rank's 4 scalars, flag-in-word in this rank's X2 slots (K6's last wave
+        // pushed them): lane 4 r + i holds rank r's value i; the first read is issued with the
+        // state's load, re-polled (bounded) only if a pending decision finds a tag not yet there
+        const int lane = threadIdx.x & 63, r = lane >> 2, i = lane & 3, nr = PP->nranks;
+        const unsigned long long gen = *xgen;
+        const unsigned g32 = (unsigned)gen;
+        const unsigned long long* wv = p2p_ll(PP->peer[PP->rank], (int)(gen & 1), min(r, nr - 1)) + 2 * i;
+        unsigned long long a = __hip_atomic_load(wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned long long b = __hip_atomic_load(wv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < 4; ++k) tv[k] = 0.0;
+        if (s.pending && !s.done && s.solve_ok) {
+            long long spins = 0;
+            bool late = false;
+            while (r < nr && !((unsigned)(a >> 32) == g32 && (unsigned)(b >> 32) == g32)) {
+                if (++spins > (1ll << 25)) {
+                    late = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                a = __hip_atomic_load(wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                b = __hip_atomic_load(wv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (late) atomicExch(err, 1);
+            const double got = late ? 0.0 : __longlong_as_double((long long)((a & 0xffffffffull) | (b << 32)));
+            for (int k = 0; k < 4; ++k) {
+                double v = 0.0;
+                for (int q = 0; q < nr; ++q) v += rl64(got, 4 * q + k);  // rank order from 0.0: X2's sum
+                tv[k] = v;
+            }
+        }
+    } else if (pre_reduced == 2) {
         const unsigned long long gen = *xgen;  // K5 of the iteration that produced the trial
         for (int k = 0; k < 4; ++k) tv[k] = 0.0;
         if (s.pending && !s.done && s.solve_ok) trial_scalars_p2p(G, Pr, Wk, s, *PP, gen, err, tv);
@@ -1197,9 +1234,11 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks(Geometry G, Pro
 
 // K4c of the P2P-sharded iteration with the trial-scalar exchange folded in (RSVIO_P2P_FOLD=2):
 // the pending decision from every rank's K6 wave partials in this rank's exchange buffer
+// (mode 4, fold 4: from the 4 scalars per rank K6's last wave pushed)
 __global__ __launch_bounds__(kSchurThreads) void ba_schur_chunks_p2p(Geometry G, Prob Pr, Work Wk, LmArgs la, P2P P,
-                                                                      const unsigned long long* xgen, int* err) {
-    schur_chunks_body(G, Pr, Wk, la, 2, blockIdx.x, &P, xgen, err);
+                                                                      const unsigned long long* xgen, int* err,
+                                                                      int mode) {
+    schur_chunks_body(G, Pr, Wk, la, mode, blockIdx.x, &P, xgen, err);
 }
 
 // The reduced system of this rank into dst (sys layout): S, b, g_c summed over the kGrp partial
@@ -1734,21 +1773,26 @@ __device__ bool combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
     const size_t L = sys_len(G);
     const int ne = G.n_pb * 36 + 12 * G.n_free;  // this window's entries (batched: may be fewer)
     const int tid = threadIdx.x;
-    double pa[16];
-    int sing = 0;
-    if (tid < 64) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) pa[k] = tid + 64 * k < G.n_wave ? Wk.partA[(tid + 64 * k) * kPartA] : 0.0;
-        sing = *Wk.singular;
-    }
     double v[kE][kGrp];
     int dst[kE];
 #pragma unroll
-    for (int i = 0; i < kE; ++i) {
-        const int e = tid + T * i;
-        dst[i] = e < ne ? Pr.dmap[e] : -1;
+    for (int i = 0; i < kE; ++i) {  // (branch-free: clamped loads; an entry past ne is never stored)
+        const int e = tid + T * i, ec = min(e, ne - 1);
+        const int d = Pr.dmap[ec];
+        dst[i] = e < ne ? d : -1;
 #pragma unroll
-        for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
+        for (int x = 0; x < kGrp; ++x) v[i][x] = Wk.cpart[(size_t)x * L + ec];
+    }
+    // then the K4 wave partials (initial cost) and the singular flag, behind them (branch-free:
+    // clamped loads, the ones past the last wave dropped at the sum -- a zeroing select here made
+    // the compiler wait for these loads before issuing the partial systems')
+    double pa[16];
+    int sing = 0;
+    if (tid < 64) {
+        const int wl = max(G.n_wave - 1, 0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pa[k] = Wk.partA[min(tid + 64 * k, wl) * kPartA];
+        sing = *Wk.singular;
     }
     const int done = st->done;
     const double lambda = st->lambda;
@@ -1774,7 +1818,7 @@ __device__ bool combine_mapped(const Geometry& G, const Prob& Pr, const Work& Wk
     if (tid < 64) {
         double c = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int k = 0; k < 16; ++k) c += tid + 64 * k < G.n_wave ? pa[k] : 0.0;
         for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
         c = wave_sum_det(c);
         if (tid == 0) {
@@ -1814,7 +1858,7 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
     if (tid < 64) {
         double c = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int k = 0; k < 16; ++k) c += tid + 64 * k < G.n_wave ? pa[k] : 0.0;
         for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
         c = wave_sum_det(c);
         if (tid < nr) {  // lane r pushes the scalars to rank r
@@ -1887,32 +1931,43 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
 // system-scope flags of every rank have arrived, each thread sums its entries over the slots in
 // RANK ORDER (identical bits on every rank, and the same bits as X1's exchange into sys followed
 // by K5's read of sys) and scatters them into M / gsh by the map.  Returns the state's done flag:
-// every rank takes the same decision, so either all exchange or none does.
-template <int NF>
+// every rank takes the same decision, so either all exchange or none does.  LL: the flag-in-word
+// form (combine_p2p_ll) -- a kernel of its own, so that its polling loops' registers do not
+// inflate the flag protocol's (one kernel holding both took 399 VGPRs, AGPR copies on the
+// prologue's path, +1.3 us per K5 at one rank against the unsharded combine)
+template <int NF, bool LL>
 __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, double* M, double* gsh,
                             const LmState* st, int* fail, const P2P& P, unsigned long long* xgen, int* err) {
     constexpr int NE = (NF * (NF + 1) / 2) * 36 + 12 * NF;
     constexpr int T = kK5Threads, kE = (NE + T - 1) / T;
-    __shared__ unsigned long long sgen;
     const size_t L = sys_len(G);
     const int ne = G.n_pb * 36 + 12 * G.n_free;
     const int tid = threadIdx.x, nr = P.nranks, me = P.rank;
-    double pa[16];
-    int sing = 0;
-    if (tid < 64) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) pa[k] = tid + 64 * k < G.n_wave ? Wk.partA[(tid + 64 * k) * kPartA] : 0.0;
-        sing = *Wk.singular;
-    }
-    if (tid == 0) sgen = *xgen + 1;
+    // the exchange's generation: loaded by every thread (one address), waited for at its first
+    // use after the partial systems' loads are in flight -- not an LDS broadcast by one thread,
+    // whose store made wave 0 wait a whole round trip (with the pose loads ahead of it) before
+    // issuing its share of those loads, and cost a barrier
+    const unsigned long long gen0 = *xgen;
     double v[kE][kGrp];
     int dst[kE];
 #pragma unroll
-    for (int i = 0; i < kE; ++i) {
-        const int e = tid + T * i;
-        dst[i] = e < ne ? Pr.dmap[e] : -1;
+    for (int i = 0; i < kE; ++i) {  // (branch-free: clamped loads; an entry past ne is never stored)
+        const int e = tid + T * i, ec = min(e, ne - 1);
+        const int d = Pr.dmap[ec];
+        dst[i] = e < ne ? d : -1;
 #pragma unroll
-        for (int x = 0; x < kGrp; ++x) v[i][x] = e < ne ? Wk.cpart[(size_t)x * L + e] : 0.0;
+        for (int x = 0; x < kGrp; ++x) v[i][x] = Wk.cpart[(size_t)x * L + ec];
+    }
+    // then the K4 wave partials (initial cost) and the singular flag, behind them (branch-free:
+    // clamped loads, the ones past the last wave dropped at the sum -- a zeroing select here made
+    // the compiler wait for these loads before issuing the partial systems')
+    double pa[16];
+    int sing = 0;
+    if (tid < 64) {
+        const int wl = max(G.n_wave - 1, 0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pa[k] = Wk.partA[min(tid + 64 * k, wl) * kPartA];
+        sing = *Wk.singular;
     }
     const int done = st->done;
     const double lambda = st->lambda;
@@ -1921,10 +1976,10 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
 #pragma unroll
         for (int x = 0; x < kGrp; ++x) __asm__ volatile("" ::"v"(v[i][x]));
     if (done) return true;
-    __syncthreads();  // sgen
-    const unsigned long long gen = sgen;
+    const unsigned long long gen = (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)gen0) +
+                                   ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(gen0 >> 32)) << 32) + 1;
     const int par = (int)(gen & 1);
-    if (P.ll) return combine_p2p_ll<NF>(G, Wk, M, gsh, fail, P, xgen, err, v, dst, pa, sing, lambda, gen);
+    if constexpr (LL) return combine_p2p_ll<NF>(G, Wk, M, gsh, fail, P, xgen, err, v, dst, pa, sing, lambda, gen);
     // this rank's entries stay in registers (own): only the peers' slots are written, flagged,
     // waited for and read back (round 5; the own slot's uncached write, flag and re-read were the
     // exchange's whole cost at one rank)
@@ -1945,7 +2000,7 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     if (tid < 64) {
         double c = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) c += pa[k];
+        for (int k = 0; k < 16; ++k) c += tid + 64 * k < G.n_wave ? pa[k] : 0.0;
         for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
         c = wave_sum_det(c);
         if (tid == 0) {
@@ -2361,7 +2416,7 @@ __device__ __forceinline__ void bk_factor(double* M, double* U, double* S, int t
     bk_steps<NF, 0, NW>(M, U, S, S + 36, a, tid, bad);
 }
 
-template <int NF>
+template <int NF, bool LL = false>
 __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const Work& Wk, int combine,
                                        const P2P* P = nullptr, unsigned long long* xgen = nullptr, int* err = nullptr) {
     static_assert(NF >= 1 && NF <= 10, "one row per lane: n <= 60");
@@ -2394,7 +2449,7 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     }
     STAMP(0);
     if (combine == 2) {  // sharded over P2P: this rank's system exchanged in the prologue (X1 folded in)
-        if (combine_p2p<NF>(G, Pr, Wk, M, gsh, st, &fail, *P, xgen, err)) return;
+        if (combine_p2p<NF, LL>(G, Pr, Wk, M, gsh, st, &fail, *P, xgen, err)) return;
     } else if (combine) {
         if (combine_mapped<NF>(G, Pr, Wk, M, gsh, st, &fail)) return;
     } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
@@ -2475,10 +2530,10 @@ __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma(Geometry G, P
 
 // K5 of the landmark-sharded iteration over the P2P exchange: the exchange of the reduced system
 // (X1: combine + push + flags + rank-ordered sum) in the prologue, then the same factorisation
-template <int NF>
+template <int NF, bool LL>
 __global__ __launch_bounds__(kK5Threads) void ba_camera_solve_mfma_p2p(Geometry G, Prob Pr, Work Wk, P2P P,
                                                                         unsigned long long* xgen, int* err) {
-    camera_solve_mfma_body<NF>(G, Pr, Wk, 2, &P, xgen, err);
+    camera_solve_mfma_body<NF, LL>(G, Pr, Wk, 2, &P, xgen, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2963,7 +3018,8 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
 template <bool FUSED>
 __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w, int lane, double (*sh)[64],
                         double (*shp)[64], double (*shs)[64], const P2P* PP = nullptr,
-                        unsigned long long gen = 0, unsigned long long* k6tag = nullptr) {
+                        unsigned long long gen = 0, unsigned long long* k6tag = nullptr,
+                        unsigned long long* k6part = nullptr) {
     // sh: W_s^T dc_f per slot, then the linearisation scratch; shp: trial point at the
     // landmark's first lane; shs: per-slot trial cost; per-landmark |dp|^2, g_p.dp, |p|^2
     const int s = 64 * w + lane;
@@ -3106,6 +3162,13 @@ __device__ void k6_body(const Geometry& G, const Prob& Pr, const Work& Wk, int w
                                __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(k6tag + (2 * lane + 1) * nw + w, (b >> 32) | t, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (k6part && lane < kPartD) {  // fold 4: the last-arriving wave's copy, at device scope
+            double vl = v[0];
+#pragma unroll
+            for (int i = 1; i < kPartD; ++i) vl = lane == i ? v[i] : vl;
+            __hip_atomic_store(k6part + (size_t)w * kPartD + lane, (unsigned long long)__double_as_longlong(vl),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (PP && lane < PP->nranks) {  // folded trial exchange: lane r pushes this wave's partial to rank r
             const int par = (int)(gen & 1);
@@ -3276,6 +3339,96 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p3(Geometry G, Pr
     k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs, nullptr, gen, k6tag);
 }
 
+// Fold 4 (round 5): no reducer workgroup and no wait inside K6.  Every K6 wave stores its 4
+// partials at device scope (k6part), waits for them to complete and takes a ticket (a relaxed
+// device-scope counter); the wave that draws the last ticket sums the partials exactly as
+// trial_scalars_wave does (+ |x|^2 of the free poses on rank 0), pushes the 4 scalars flag-in-word
+// to every rank (itself included, X2's slots and generation) and returns -- it waits for nobody.
+// The next decision (K4c's wave 0, or K7) polls the nranks x 4 tagged words and sums them in rank
+// order: the same bits as X2 / fold 3.  A rank without landmarks (no K6 wave) pushes from
+// workgroup 0 of a one-workgroup grid.
+__device__ void k6_last_push(const Geometry& G, const Prob& Pr, const Work& Wk, const P2P& P,
+                             unsigned long long* xgen, unsigned long long gen, const unsigned long long* k6part,
+                             const LmState& s) {
+    const int lane = threadIdx.x & 63;
+    constexpr int kU = 8;
+    const int wl = max(G.n_wave - 1, 0), el = 7 * G.n_kf - 1;
+    unsigned long long pw[kU][kPartD];
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+#pragma unroll
+        for (int j = 0; j < kPartD; ++j)
+            pw[k][j] = __hip_atomic_load(k6part + (size_t)min(lane + 64 * k, wl) * kPartD + j, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    double p0[3], p1[3];
+    int fi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int e = min(lane + 64 * k, el);
+        fi[k] = Pr.free_idx[e / 7];
+        p0[k] = Wk.pose[0][e];
+        p1[k] = Wk.pose[1][e];
+    }
+    // trial_scalars_wave's order: per lane the waves lane + 64 k ascending (zeros past the last),
+    // a tail loop past 512 waves, then the poses' squares, then the fixed-pairing wave sums
+    double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+#pragma unroll
+        for (int j = 0; j < kPartD; ++j)
+            acc[j] += lane + 64 * k < G.n_wave ? __longlong_as_double((long long)pw[k][j]) : 0.0;
+    for (int i = lane + 64 * kU; i < G.n_wave; i += 64)
+#pragma unroll
+        for (int j = 0; j < kPartD; ++j)
+            acc[j] += __longlong_as_double((long long)__hip_atomic_load(k6part + (size_t)i * kPartD + j, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT));
+    double sq[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (P.rank == 0 && lane + 64 * k <= el && fi[k] >= 0) {
+            sq[0] += p0[k] * p0[k];
+            sq[1] += p1[k] * p1[k];
+        }
+    acc[3] += sq[s.cur];
+    double out[kPartD];
+#pragma unroll
+    for (int k = 0; k < kPartD; ++k) out[k] = wave_sum_det(acc[k]);
+    const int r = lane >> 2, i = lane & 3, par = (int)(gen & 1);
+    double mv = out[0];
+#pragma unroll
+    for (int k = 1; k < kPartD; ++k) mv = i == k ? out[k] : mv;
+    if (r < P.nranks) ll_put(p2p_ll(P.peer[r], par, P.rank) + 2 * i, mv, (unsigned)gen);
+    if (lane == 0) *xgen = gen;
+}
+
+__global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p4(Geometry G, Prob Pr, Work Wk, P2P P,
+                                                                  unsigned long long* xgen, unsigned* k6cnt,
+                                                                  unsigned long long* k6part) {
+    __shared__ double sh[10][64];
+    __shared__ double shp[3][64];
+    __shared__ double shs[4][64];
+    unsigned long long gen = *xgen + 1;
+    __asm__ volatile("" : "+s"(gen));  // loaded with the kernel's first loads, not at its end
+    if (G.n_wave > 0) {
+        k6_body<false>(G, Pr, Wk, blockIdx.x, threadIdx.x, sh, shp, shs, nullptr, gen, nullptr, k6part);
+        const LmState s = *Wk.st;
+        if (s.done || !s.solve_ok) return;  // (k6_body's own early exit: no partials, no decision pending)
+        // this wave's partial stores complete before its ticket (vmcnt(0): a store at device scope
+        // is acknowledged once it is visible at that scope), so the last ticket sees every partial
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        unsigned t = 0;
+        if (threadIdx.x == 0) t = __hip_atomic_fetch_add(k6cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t != (unsigned)G.n_wave - 1) return;
+        if (threadIdx.x == 0) __hip_atomic_store(k6cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        k6_last_push(G, Pr, Wk, P, xgen, gen, k6part, s);
+    } else {
+        const LmState s = *Wk.st;
+        if (s.done || !s.solve_ok) return;
+        k6_last_push(G, Pr, Wk, P, xgen, gen, k6part, s);
+    }
+}
+
 // K6r (sharded): this rank's trial scalars (|x|^2 of the poses on the owner rank) -> trial4,
 // ready for the all-reduce
 __global__ __launch_bounds__(64) void ba_reduce_trial(Geometry G, Prob Pr, Work Wk, int include_poses) {
@@ -3354,11 +3507,11 @@ __global__ __launch_bounds__(kK7Threads) void ba_lm_decide(Geometry G, Prob Pr, 
     lm_decide_body(G, Pr, Wk, pre_reduced, la, host, htick, hout);
 }
 
-// K7 of the P2P-sharded solve with the folded trial exchange (RSVIO_P2P_FOLD=2)
+// K7 of the P2P-sharded solve with the folded trial exchange (RSVIO_P2P_FOLD=2; mode 4: fold 4)
 __global__ __launch_bounds__(kK7Threads) void ba_lm_decide_p2p(Geometry G, Prob Pr, Work Wk, LmArgs la, LmState* host,
                                                                unsigned long long* htick, double* hout, P2P P,
-                                                               const unsigned long long* xgen, int* err) {
-    lm_decide_body(G, Pr, Wk, 2, la, host, htick, hout, &P, xgen, err);
+                                                               const unsigned long long* xgen, int* err, int mode) {
+    lm_decide_body(G, Pr, Wk, mode, la, host, htick, hout, &P, xgen, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3831,17 +3984,21 @@ struct BundleAdjuster {
     hipEvent_t ev_desc = nullptr;
     bool desc_pending = false;
     bool desc_mode() const { return desc_on && coll == 0 && k5_variant == 2 && G.n_free <= 10 && G.n_wave > 0; }
-    // the P2P-sharded iteration: RSVIO_P2P_FOLD=1 (default) 4 launches -- the reduced system's
-    // exchange in K5's prologue, the trial scalars by X2; 2: 3 launches (the trial scalars pushed
-    // by K6's waves and summed by the next decision: measured 10.6 us per iteration slower on one
-    // rank, every K4c block's decision then polling every wave's partial of every rank,
+    // the P2P-sharded iteration (RSVIO_P2P_FOLD): 3 (default since round 5) 3 launches -- the
+    // reduced system's exchange in K5's prologue, K6 with a reducer workgroup that sums the rank's
+    // tagged wave partials and runs the trial exchange (no X2; 0.8 us per iteration below fold 1
+    // on the same partition, profiles/r05k_same_basis.txt); 1: 4 launches (the trial scalars by
+    // X2); 4: 3 launches, K6's last-arriving wave pushes the rank's scalars and the next decision
+    // polls them (measured no faster than 3, profiles/r05l_fold4_same_basis.txt); 2: 3 launches,
+    // the next decision summing every wave's partial of every rank (10.6 us slower,
     // profiles/r04k_p2p_fold_kstats.txt); 0: 5 launches (X1 as its own kernel)
-    int fold_lvl = 1;
-    int fold_req = 1;             // the level asked for (RSVIO_P2P_FOLD); attach_p2p may lower fold_lvl
-    bool p2p_shared_gpu = false;  // attach_p2p found two ranks on one device (fold 2 -> 1)
+    int fold_lvl = 3;
+    int fold_req = 3;             // the level asked for (RSVIO_P2P_FOLD); attach_p2p may lower fold_lvl
+    bool p2p_shared_gpu = false;  // attach_p2p found two ranks on one device (fold 2 -> 1, 4 -> 3)
     bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
     bool p2p_fold2() const { return fold_lvl == 2 && p2p_fold(); }
     bool p2p_fold3() const { return fold_lvl == 3 && p2p_fold(); }
+    bool p2p_fold4() const { return fold_lvl == 4 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
     void fill_desc(WinDesc& d) const {
         d = WinDesc{};
@@ -4016,7 +4173,9 @@ struct BundleAdjuster {
     DevBuf<int> d_p2p_err;
     DevBuf<unsigned long long> d_xgen;  // P2P exchange generation (advanced on the device)
     DevBuf<int> d_xnw;                  // every rank's wave count (K5's exchange carries it)
-    DevBuf<unsigned long long> d_k6tag; // fold 3: K6 wave partials, flag-in-word (2 kPartD words per wave)
+    DevBuf<unsigned long long> d_k6tag; // fold 3: K6 wave partials, flag-in-word (2 kPartD words per wave);
+                                        // fold 4: the plain partials (kPartD words per wave)
+    DevBuf<unsigned> d_k6cnt;           // fold 4: K6's ticket counter (back to 0 by the last wave)
 
     void init(const rsvio_ba_params& p) {
         P = p;
@@ -4031,8 +4190,8 @@ struct BundleAdjuster {
         RSVIO_HIP(hipEventCreateWithFlags(&gv.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
-        const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0" / "1" / "2" (A/B switch)
-        if (fv && fv[0] >= '0' && fv[0] <= '3') fold_lvl = fold_req = fv[0] - '0';
+        const char* fv = std::getenv("RSVIO_P2P_FOLD");  // "0" .. "4" (A/B switch)
+        if (fv && fv[0] >= '0' && fv[0] <= '4') fold_lvl = fold_req = fv[0] - '0';
         const char* dv = std::getenv("RSVIO_BA_DESC");  // "0": by-value kernels captured per window
         desc_on = !(dv && dv[0] == '0');
         const char* gu = std::getenv("RSVIO_BA_GRAPH_UPDATE");  // "0": instantiate every new problem
@@ -4157,6 +4316,10 @@ struct BundleAdjuster {
         if (d_k6tag.n < (size_t)2 * kPartD * std::max(n_wave, 1)) {  // fold 3's tagged K6 partials
             grow(d_k6tag, (size_t)2 * kPartD * std::max(n_wave, 1));
             RSVIO_HIP(hipMemsetAsync(d_k6tag.p, 0, sizeof(unsigned long long) * d_k6tag.n, stream));
+        }
+        if (d_k6cnt.n < 1) {
+            grow(d_k6cnt, 1);
+            RSVIO_HIP(hipMemsetAsync(d_k6cnt.p, 0, sizeof(unsigned), stream));
         }
     }
 
@@ -4474,17 +4637,23 @@ struct BundleAdjuster {
         const Prob pr = prob();
         const Work wk = work(it);
         if (p2p_fold()) {  // sharded over P2P: K4c, K5 with X1 folded in, K6[, X2]
-            if (p2p_fold2())
+            if (p2p_fold2() || p2p_fold4())
                 hipLaunchKernelGGL(ba_schur_chunks_p2p, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
-                                   lm_args(cfg), p2p, d_xgen.p, d_p2p_err.p);
+                                   lm_args(cfg), p2p, d_xgen.p, d_p2p_err.p, p2p_fold4() ? 4 : 2);
             else
                 hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk,
                                    lm_args(cfg), 1);
             RSVIO_HIP(hipGetLastError());
             switch (G.n_free) {
 #define RSVIO_CAMP(NF) \
-    case NF: hipLaunchKernelGGL(ba_camera_solve_mfma_p2p<NF>, dim3(1), dim3(kK5Threads), 0, stream, G, pr, wk, p2p, \
-                                d_xgen.p, d_p2p_err.p); break;
+    case NF:                                                                                                            \
+        if (p2p.ll)                                                                                                     \
+            hipLaunchKernelGGL((ba_camera_solve_mfma_p2p<NF, true>), dim3(1), dim3(kK5Threads), 0, stream, G, pr, wk,  \
+                               p2p, d_xgen.p, d_p2p_err.p);                                                            \
+        else                                                                                                            \
+            hipLaunchKernelGGL((ba_camera_solve_mfma_p2p<NF, false>), dim3(1), dim3(kK5Threads), 0, stream, G, pr, wk, \
+                               p2p, d_xgen.p, d_p2p_err.p);                                                            \
+        break;
                 RSVIO_CAMP(1) RSVIO_CAMP(2) RSVIO_CAMP(3) RSVIO_CAMP(4) RSVIO_CAMP(5)
                 RSVIO_CAMP(6) RSVIO_CAMP(7) RSVIO_CAMP(8) RSVIO_CAMP(9) RSVIO_CAMP(10)
 #undef RSVIO_CAMP
@@ -4499,6 +4668,12 @@ struct BundleAdjuster {
             if (G.n_wave)
                 hipLaunchKernelGGL(ba_backsub_relinearize_p2p, dim3(G.n_wave), dim3(64), 0, stream, G, pr, wk, p2p,
                                    d_xgen.p);
+            RSVIO_HIP(hipGetLastError());
+            return;
+        }
+        if (p2p_fold4()) {  // K6, its last wave pushing this rank's trial scalars (no X2, no wait)
+            hipLaunchKernelGGL(ba_backsub_relinearize_p2p4, dim3(std::max(G.n_wave, 1)), dim3(64), 0, stream, G, pr,
+                               wk, p2p, d_xgen.p, d_k6cnt.p, d_k6tag.p);
             RSVIO_HIP(hipGetLastError());
             return;
         }
@@ -4523,10 +4698,10 @@ struct BundleAdjuster {
     // K7: the decision pending after `it` iterations, in place in state copy it & 1
     void enqueue_decide(const rsvio_lm_cfg& cfg, int it) {
         // reads state copy it & 1 (the last iteration's pending trial), writes copy (it + 1) & 1
-        if (p2p_fold2()) {
+        if (p2p_fold2() || p2p_fold4()) {
             hipLaunchKernelGGL(ba_lm_decide_p2p, dim3(export_on ? kK7Blocks : 1), dim3(kK7Threads), 0, stream, G,
                                prob(), work(it), lm_args(cfg), h_state.p, h_tick, export_on ? h_out.p : nullptr, p2p,
-                               d_xgen.p, d_p2p_err.p);
+                               d_xgen.p, d_p2p_err.p, p2p_fold4() ? 4 : 2);
             RSVIO_HIP(hipGetLastError());
             return;
         }
@@ -4780,7 +4955,9 @@ struct BundleAdjuster {
         // (RSVIO_P2P_FOLD_SHARED=1 keeps fold 2 anyway: the A/B test of its sums on one GPU)
         const char* fsv = std::getenv("RSVIO_P2P_FOLD_SHARED");
         const bool keep2 = fsv && fsv[0] == '1';
-        fold_lvl = shared_gpu && fold_req == 2 && !keep2 ? 1 : fold_req;
+        // (ranks sharing one GPU: a decision that waits in K4c -- folds 2 and 4 -- can starve a
+        // peer's K6 of CUs; they take the nearest level that waits inside K6 or K5 instead)
+        fold_lvl = shared_gpu && !keep2 && (fold_req == 2 || fold_req == 4) ? fold_req - 1 : fold_req;
         p2p_shared_gpu = shared_gpu;
         p2p = P;
         nranks = nr;

@@ -109,6 +109,13 @@ struct TrackerView {
 };
 TrackerView tracker_view(rsvio_tracker* t);
 
+// Rust's saturating `as u32` (NaN and v <= 0 -> 0, v >= 2^32 -> u32::MAX) as selects, not
+// branches: the range tests and the conversion are all evaluated, no exec-mask round trips
+__device__ __forceinline__ uint32_t sat_u32(float v) {
+    const uint32_t t = (uint32_t)fminf(fmaxf(v, 0.0f), 4294967040.0f);
+    return v >= 4294967296.0f ? 0xFFFFFFFFu : (v > 0.0f ? t : 0u);
+}
+
 // Pyramid level geometry: level i = (w / 2^i) x (h / 2^i), packed back to back
 // (feature_tracker.rs:215-216).
 __host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }

@@ -29,12 +29,6 @@ inline GridGeom make_grid(int w, int h, int g) {
     return G;
 }
 
-__device__ __forceinline__ uint32_t sat_u32(float v) {
-    if (!(v > 0.0f)) return 0u;
-    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)v;
-}
-
 // FAST-9 score of a candidate (largest t with a contiguous 9-arc all brighter than c + t or all
 // darker than c - t); equals imageproc's binary-searched fast_corner_score whenever the pixel is
 // a corner at the starting threshold.

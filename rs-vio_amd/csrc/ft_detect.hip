@@ -27,12 +27,6 @@ namespace ft {
 
 namespace {
 
-__device__ __forceinline__ uint32_t sat_u32(float v) {
-    if (!(v > 0.0f)) return 0u;
-    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)v;
-}
-
 // feature_detection.rs:90-119: dx, dy by imageproc horizontal/vertical_filter([-1, 0, 1]) --
 // correlation, pads by continuity, acc = 0; acc = acc + p * k in kernel order -- then products.
 __global__ __launch_bounds__(256) void ft_grad_kernel(const float* __restrict__ im, int w, int h,

@@ -183,12 +183,6 @@ __device__ __forceinline__ void chains(const float (&v)[N], const float (&init)[
     for (int i = 0; i < N; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), i));
 }
 
-__device__ __forceinline__ uint32_t sat_u32(float v) {
-    if (!(v > 0.0f)) return 0u;
-    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)v;
-}
-
 // image_operations.rs:231-282
 __device__ __forceinline__ float bicubic_1d(float f0, float f1, float f2, float f3, float t) {
     const float a0 = f1;

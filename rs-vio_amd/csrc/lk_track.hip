@@ -86,12 +86,6 @@ __device__ __forceinline__ void lane_chains(const float (&v)[N], float (&out)[N]
     for (int i = 0; i < N; ++i) out[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), i));
 }
 
-__device__ __forceinline__ uint32_t sat_u32(float v) {
-    if (!(v > 0.0f)) return 0u;
-    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)v;
-}
-
 struct LevelImg {
     const uint8_t* __restrict__ p;
     uint32_t w, h;

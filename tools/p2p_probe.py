@@ -48,11 +48,27 @@ def worker(rank, world, port, reps):
             print(f"rank {rank}: exchange latency us {lat}", flush=True)
         ba.set_problem_from(shard)
         ms = []
+        # PROBE_STAMPS=1 (with RSVIO_LIB = the stamps build): K5's phase stamps of the solve's last
+        # iteration, block 0 -- STAMP 0 (entry), 1 (system in LDS), 2 (fail checked), 3 (solved)
+        stamps = os.environ.get("PROBE_STAMPS", "0") == "1"
+        ph = []
+        if stamps:
+            import ctypes as C
+            from rsvio import _lib
+            buf = (C.c_ulonglong * 64)()
         for k in range(reps + 3):
             r = ba.run()
             if k >= 3:
                 ms.append(r.solve_ms / max(r.iterations, 1))
-        mode = "single (unsharded)" if single else f"fold {os.environ.get('RSVIO_P2P_FOLD', '1')}"
+                if stamps:
+                    _lib.load().rsvio_dbg_ba_stamps(buf, 64)
+                    st = [int(buf[i]) for i in range(4)]
+                    ph.append([st[i + 1] - st[i] for i in range(len(st) - 1)])  # shader clock cycles
+        if stamps:
+            med = np.median(np.array(ph), axis=0)
+            print(f"rank {rank}: K5 phases, cycles (entry->system, ->checked, ->solved) "
+                  f"{' '.join(f'{v:.0f}' for v in med)}", flush=True)
+        mode = "single (unsharded)" if single else f"fold {os.environ.get('RSVIO_P2P_FOLD', '3')}"
         print(f"rank {rank}: {mode} cu_split {split} ll {os.environ.get('RSVIO_P2P_LL', '0')} status {r.status} it {r.iterations} "
               f"ms/iter median {float(np.median(ms)):.4f} min {min(ms):.4f}", flush=True)
         ba.close()
