@@ -2200,8 +2200,10 @@ __device__ __forceinline__ void mf_panel(double* M, double* Lf, double* Up, int 
 }
 
 // ---------------------------------------------------------------------------------------
-// K5 by 6x6 block pivots (round 5, the default; -DRSVIO_K5_PANEL8 builds the 8-column panels
-// above).  The camera system's own blocks: step k factors keyframe k's diagonal block as a whole.
+// K5 by 6x6 block pivots (round 5): the solver of 11..20 free keyframes (camera_solve_blk_body);
+// for <= 10 the 8-column panels above stay the default (measured faster at config 3, 12.7 vs
+// 13.9 us) and -DRSVIO_K5_BLOCK builds this one there (A/B).  The camera system's own blocks:
+// step k factors keyframe k's diagonal block as a whole.
 //   * Chain wave (wave 0, lane = row; rows lane and lane + 64 past 64 rows): it holds column
 //     block k of its rows in registers, fully updated.  The diagonal block's 21 lower entries go
 //     to every lane through LDS (one store by its 6 rows, one broadcast read), and every lane

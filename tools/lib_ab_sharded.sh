@@ -1,12 +1,12 @@
 #!/bin/bash
-# GPU box: the 1-rank P2P-sharded chain (fold F) under rocprofv3 for each library variant given
+# GPU box: the 1-rank P2P-sharded chain (fold F; PROBE_SINGLE=1: the unsharded chain) under rocprofv3 for each library variant given
 # (lib/librsvio_gpu_<name>.so; "-" = the product library), bench.py's BA CU partition; per
 # variant the probe's ms/iter and the per-kernel averages.
 # usage: tools/lib_ab_sharded.sh TAG FOLD name...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-export TMPDIR=/tmp PROBE_CU_SPLIT=0.25 WORLD_SIZE=1 RANK=0 MASTER_ADDR=127.0.0.1 PROBE_SINGLE=0
+export TMPDIR=/tmp PROBE_CU_SPLIT=0.25 WORLD_SIZE=1 RANK=0 MASTER_ADDR=127.0.0.1 PROBE_SINGLE=${PROBE_SINGLE:-0}
 TAG=$1; F=$2; shift 2
 for name in "$@"; do
   D=gpurun_out/lab_${TAG}_$name

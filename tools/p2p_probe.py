@@ -50,7 +50,8 @@ def worker(rank, world, port, reps):
         ms = []
         # PROBE_STAMPS=1 (with RSVIO_LIB = the stamps build): K5's phase stamps of the solve's last
         # iteration, block 0 -- STAMP 0 (entry), 1 (system in LDS), 2 (fail checked), 3 (solved)
-        stamps = os.environ.get("PROBE_STAMPS", "0") == "1"
+        stamps = os.environ.get("PROBE_STAMPS", "0") in ("1", "2")
+        panels = os.environ.get("PROBE_STAMPS", "0") == "2"
         ph = []
         if stamps:
             import ctypes as C
@@ -62,11 +63,16 @@ def worker(rank, world, port, reps):
                 ms.append(r.solve_ms / max(r.iterations, 1))
                 if stamps:
                     _lib.load().rsvio_dbg_ba_stamps(buf, 64)
-                    st = [int(buf[i]) for i in range(4)]
+                    # PROBE_STAMPS=2: the 8-column panels' steps instead (2 = factor start, 9 /
+                    # 13 / 15 / 19 / 30 / 31 around panels 0, 2, 4, 7 = last panel, 3 = solved)
+                    order = [2, 9, 13, 15, 19, 30, 31, 7, 3] if panels else [0, 1, 2, 3]
+                    st = [int(buf[i]) for i in order]
                     ph.append([st[i + 1] - st[i] for i in range(len(st) - 1)])  # shader clock cycles
         if stamps:
             med = np.median(np.array(ph), axis=0)
-            print(f"rank {rank}: K5 phases, cycles (entry->system, ->checked, ->solved) "
+            what = ("panel 0, 0-1, 1-2, 2-3, 3-4, 4-5, 5-6 steps, back-substitution" if panels else
+                    "entry->system, ->checked, ->solved")
+            print(f"rank {rank}: K5 phases, cycles ({what}) "
                   f"{' '.join(f'{v:.0f}' for v in med)}", flush=True)
         mode = "single (unsharded)" if single else f"fold {os.environ.get('RSVIO_P2P_FOLD', '3')}"
         print(f"rank {rank}: {mode} cu_split {split} ll {os.environ.get('RSVIO_P2P_LL', '0')} status {r.status} it {r.iterations} "
