@@ -3216,6 +3216,9 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p(Geometry G, Pro
 // rank-ordered sums to trial4 -- the same bits X2 wrote, read by the next K4c / K7 after the
 // boundary.  It is dispatched last, after every wave it waits for (all of K6 is co-resident), and
 // its spins are bounded like every exchange's (the error flag the host checks).
+// KU: waves per lane and sweep (4 when n_wave <= 256: the sums of the waves past the last are
+// zeros either way, so trial_scalars_wave's 8 give the same bits; half the uncached words per sweep)
+template <int KU>
 __device__ void k6_reduce_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, const P2P& P,
                               unsigned long long* xgen, int* err, const unsigned long long* k6tag) {
     const int lane = threadIdx.x & 63;
@@ -3235,7 +3238,7 @@ __device__ void k6_reduce_p2p(const Geometry& G, const Prob& Pr, const Work& Wk,
         p0[k] = Wk.pose[0][e];
         p1[k] = Wk.pose[1][e];
     }
-    constexpr int kU = 8;
+    constexpr int kU = KU;
     double acc[kPartD] = {0.0, 0.0, 0.0, 0.0};
     bool late = false;
     if (s.solve_ok) {  // (no step: K6's waves returned early, the partials are zeros)
@@ -3333,7 +3336,10 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p3(Geometry G, Pr
     __shared__ double shp[3][64];
     __shared__ double shs[4][64];
     if ((int)blockIdx.x == G.n_wave) {
-        k6_reduce_p2p(G, Pr, Wk, P, xgen, err, k6tag);
+        if (G.n_wave <= 256)
+            k6_reduce_p2p<4>(G, Pr, Wk, P, xgen, err, k6tag);
+        else
+            k6_reduce_p2p<8>(G, Pr, Wk, P, xgen, err, k6tag);
         return;
     }
     unsigned long long gen = *xgen + 1;
