@@ -764,18 +764,20 @@ def test_sharded_p2p_four_ranks_match_oracle(gpu, oracle, tmp_path):
     assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
 
 
-@pytest.mark.parametrize("level,world", [("4", 2), ("4", 4), ("3", 2), ("2", 2), ("0", 2)])
-def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level, world):
+@pytest.mark.parametrize("level,world,per_rank", [("4", 2, 2000), ("4", 4, 2000), ("3", 2, 2000), ("3", 2, 7000),
+                                                  ("2", 2, 2000), ("0", 2, 2000)])
+def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level, world, per_rank):
     """The 4-launch iteration (RSVIO_P2P_FOLD=1: the reduced system's exchange in K5's prologue,
     the trial scalars through X2's flag-in-word exchange) against the 3-launch ones (4: K6's
     last-arriving wave sums the rank's wave partials and pushes the 4 scalars, the next decision
     polls them; 3: K6's reducer workgroup sums the rank's tagged wave partials and runs the trial
     exchange; 2: the trial scalars pushed by K6's waves and summed by the next decision) and the
     5-launch one (0: X1 as a kernel of its own): the same sums in the same order, so the solves are
-    bit-identical on every rank."""
+    bit-identical on every rank.  7,000 landmarks per rank (> 512 waves) take fold 3's reducer
+    through its full-width sweeps and their second chunk (2,000: the half-width one)."""
     (tmp_path / "a").mkdir()
     (tmp_path / "b").mkdir()
-    n = 2000 * world
+    n = per_rank * world
     fold = _run_p2p(world, n, tmp_path / "a", env={"RSVIO_P2P_FOLD": "1"})
     # (on this shared GPU attach_p2p would lower fold 2 to 1; the test keeps it to compare its sums)
     sep = _run_p2p(world, n, tmp_path / "b", env={"RSVIO_P2P_FOLD": level, "RSVIO_P2P_FOLD_SHARED": "1"})
