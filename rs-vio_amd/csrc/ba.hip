@@ -905,13 +905,15 @@ __device__ void trial_scalars_p2p(const Geometry& G, const Prob& Pr, const Work&
             if (w < nw) {
                 const unsigned long long* f = p2p_tflag(own, par, r, w);
                 long long spins = 0;
-                while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+                while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1ll << 25)) {
                         late = true;
                         break;
                     }
                 }
+                // relaxed polls (no L2 invalidate per poll), one acquire once the flag is seen
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 const double* q = p2p_tval(own, par, r, w);
                 v.x = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 v.y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1855,38 +1857,28 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
         if (me == 0 && dst[i] >= 0 && (dst[i] & kMfMapLambda)) a += lambda;
         for (int r = 0; r < nr; ++r) ll_put(p2p_llsys(P.peer[r], par, me) + 2 * (size_t)e, a, g32);
     }
+    double c = 0.0;
     if (tid < 64) {
-        double c = 0.0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c += tid + 64 * k < G.n_wave ? pa[k] : 0.0;
         for (int w = tid + 64 * 16; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
         c = wave_sum_det(c);
-        if (tid < nr) {  // lane r pushes the scalars to rank r
-            unsigned long long* d = p2p_llsys(P.peer[tid], par, me) + 2 * (size_t)ne;
-            ll_put(d, c, g32);
-            ll_put(d + 2, sing ? 1.0 : 0.0, g32);
-            ll_put(d + 4, (double)G.n_wave, g32);
-        }
     }
-    // entries: every rank's two words of this thread's entries, ranks in groups of 2 or 4
+    // the scalars go last, once every thread's entry stores have completed (vmcnt(0), then the
+    // barrier), so a reader that sees a rank's scalars finds its entries there too: the readers
+    // poll the 6 scalar words of each rank and read the entries once (still tag-checked), instead
+    // of every thread re-reading all its entries' words of every rank until they arrive -- traffic
+    // that, with four ranks on one GPU, starved the last rank's own progress until the spin bound
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    if (tid < nr) {  // lane r pushes the scalars to rank r
+        unsigned long long* d = p2p_llsys(P.peer[tid], par, me) + 2 * (size_t)ne;
+        ll_put(d, c, g32);
+        ll_put(d + 2, sing ? 1.0 : 0.0, g32);
+        ll_put(d + 4, (double)G.n_wave, g32);
+    }
     const unsigned long long* mine = p2p_llsys(P.peer[me], par, 0);
-    double acc[kE];
-#pragma unroll
-    for (int i = 0; i < kE; ++i) acc[i] = 0.0;
-    const bool late = nr <= 2 ? ll_group_sums<kE, 2>(mine, nr, ne, tid, T, g32, acc)
-                              : ll_group_sums<kE, 4>(mine, nr, ne, tid, T, g32, acc);
-    if (late) atomicExch(err, 1);
-#pragma unroll
-    for (int i = 0; i < kE; ++i) {
-        const int e = tid + T * i;
-        if (e >= ne) break;
-        const int d = dst[i];
-        if (d >= 0)
-            M[d & (kMfMapLambda - 1)] = acc[i];
-        else if (d <= -2)
-            gsh[-2 - d] = acc[i];
-    }
-    // scalars: lane r of wave 0 reads rank r's three; the sums in rank order by lane 0
+    // scalars: lane r of wave 0 reads rank r's three (the sums in rank order by lane 0, below)
     __shared__ double sc[kP2PMax][3];
     if (tid < nr) {
         const unsigned long long* a = mine + (size_t)tid * 2 * kP2PMsg + 2 * (size_t)ne;
@@ -1903,20 +1895,37 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
                 atomicExch(err, 1);
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(2);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             sc[tid][k] = __longlong_as_double((long long)((ws[2 * k] & 0xffffffffull) | (ws[2 * k + 1] << 32)));
     }
     __syncthreads();
+    // entries: every rank's two words of this thread's entries, ranks in groups of 2 or 4
+    double acc[kE];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) acc[i] = 0.0;
+    const bool late = nr <= 2 ? ll_group_sums<kE, 2>(mine, nr, ne, tid, T, g32, acc)
+                              : ll_group_sums<kE, 4>(mine, nr, ne, tid, T, g32, acc);
+    if (late) atomicExch(err, 1);
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = tid + T * i;
+        if (e >= ne) break;
+        const int d = dst[i];
+        if (d >= 0)
+            M[d & (kMfMapLambda - 1)] = acc[i];
+        else if (d <= -2)
+            gsh[-2 - d] = acc[i];
+    }
     if (tid == 0) {
-        double c = 0.0, f = 0.0;
+        double cs = 0.0, f = 0.0;
         for (int r = 0; r < nr; ++r) {
-            c += sc[r][0];
+            cs += sc[r][0];
             f += sc[r][1];
         }
-        Wk.sys[ne] = c;  // the decision of iteration 0 reads the (all-reduced) initial cost here
+        Wk.sys[ne] = cs;  // the decision of iteration 0 reads the (all-reduced) initial cost here
         *fail = f != 0.0;
         *xgen = gen;
     }
@@ -2022,13 +2031,15 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     if (tid < nr && tid != me) {
         const unsigned long long* f = p2p_flags(P.peer[me]) + par * kP2PMax + tid;
         long long spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1ll << 25)) {  // a peer never arrived: report, do not hang
                 atomicExch(err, 1);
                 break;
             }
         }
+        // relaxed polls (no L2 invalidate per poll), one acquire once the flag is seen
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     const double* mine = p2p_slot(P.peer[me], par, 0);
@@ -3708,13 +3719,15 @@ __device__ void p2p_exchange(const double* msg, int n, const P2P& P, unsigned lo
     if (tid < nr) {
         const unsigned long long* f = p2p_flags(P.peer[me]) + par * kP2PMax + tid;
         long long spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1ll << 25)) {  // a peer never arrived: report, do not hang
                 atomicExch(err, 1);
                 break;
             }
         }
+        // relaxed polls (no L2 invalidate per poll), one acquire once the flag is seen
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     const double* mine = P.peer[me] + (size_t)(par * kP2PMax) * kP2PMsg;
