@@ -2044,15 +2044,17 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
     __syncthreads();
     const double* mine = p2p_slot(P.peer[me], par, 0);
     // this thread's values from a group of ranks in flight together (own from registers, peers'
-    // from their slots), groups in rank order: one round trip per group of 2 (two ranks) or 4
-    // ranks, then the rank-ordered sums
+    // from their slots), groups in rank order: one round trip per group of 2 (two ranks), 4 (three
+    // or four) or 8 ranks, then the rank-ordered sums
     double sums[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) sums[i] = 0.0;
     if (nr <= 2)
         p2p_group_sums_own<kE, 2>(mine, nr, me, ne, tid, T, own, sums);
-    else
+    else if (nr <= 4)
         p2p_group_sums_own<kE, 4>(mine, nr, me, ne, tid, T, own, sums);
+    else  // 5..8 ranks: every peer's slot in flight together -- one round trip, not two groups of 4
+        p2p_group_sums_own<kE, 8>(mine, nr, me, ne, tid, T, own, sums);
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
         const int e = tid + T * i;

@@ -764,6 +764,23 @@ def test_sharded_p2p_four_ranks_match_oracle(gpu, oracle, tmp_path):
     assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
 
 
+def test_sharded_p2p_six_ranks_match_oracle(gpu, oracle, tmp_path):
+    """Six ranks (six processes on one GPU): past four ranks K5 reads every peer's slot in one
+    group of 8 (the N=8 node's path), the trial exchange spans 6 x 4 words.  2,000 landmarks per
+    rank = the oracle's 12,000-landmark solve; every rank ends with bitwise the same poses and LM
+    outcome, within the config-3 tolerances of the oracle."""
+    from rsvio import synthetic as S
+    rs = _run_p2p(6, 12000, tmp_path)
+    for r in rs[1:]:
+        assert np.array_equal(rs[0]["pose"], r["pose"]) and np.array_equal(rs[0]["res"], r["res"])
+    full = S.ba_problem(n_lm=12000)
+    po, pwo, ro = oracle.ba_solve(full)
+    assert int(rs[0]["res"][0]) == ro.status and int(rs[0]["res"][1]) == ro.iterations
+    assert abs(rs[0]["res"][2] - ro.final_cost) <= 1e-8 * ro.initial_cost
+    assert np.abs(rs[0]["pose"] - po).max() < 1e-7
+    assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
+
+
 @pytest.mark.parametrize("level,world,per_rank", [("4", 2, 2000), ("4", 4, 2000), ("3", 2, 2000), ("3", 2, 7000),
                                                   ("2", 2, 2000), ("0", 2, 2000)])
 def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level, world, per_rank):
