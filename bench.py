@@ -1181,9 +1181,9 @@ def main():
         pair lists built on the device) and starts its solve (the descriptor-mode graph: one
         launch); then the frame's features, the solve and its optimised state (48.6 KB, published
         to pinned host memory with the solve's last decision) are waited for.  Default order
-        (ba-first): the window and the solve are enqueued before the frame; --order frame-first
-        the other way round; --order split: the frame's image upload first (as soon as the frame
-        is there), then the window and the solve, then the frame's kernels and downloads."""
+        (split): the frame's image upload first (as soon as the frame is there), then the window
+        and the solve, then the frame's kernels and downloads; --order ba-first: the window and
+        the solve before the whole frame; --order frame-first the other way round."""
         if args.order == "frame-first":
             trk.step(timed, pcie=True, wait=False)
         elif args.order == "split":
