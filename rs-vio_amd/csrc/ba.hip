@@ -3256,26 +3256,37 @@ __device__ void k6_reduce_p2p(const Geometry& G, const Prob& Pr, const Work& Wk,
     bool late = false;
     if (s.solve_ok) {  // (no step: K6's waves returned early, the partials are zeros)
         for (int i0 = 0; i0 < max(G.n_wave, 64 * kU); i0 += 64 * kU) {
-            // this lane's waves i0 + lane + 64 k, polled together until every tag is this exchange's
+            // this lane's waves i0 + lane + 64 k: every pending one's 8 words loaded together, a wave
+            // whose words all carry this exchange's tag is done and not re-read (later sweeps load
+            // only the waves still missing, and lanes past the last wave load nothing)
             unsigned long long wd[kU][kPartD][2];
+            unsigned pend = 0;
+#pragma unroll
+            for (int k = 0; k < kU; ++k)
+                if (i0 + lane + 64 * k < G.n_wave) pend |= 1u << k;
             long long spins = 0;
+            const size_t nw = (size_t)G.n_wave;
             for (;;) {
-                bool ok = true;
 #pragma unroll
-                for (int k = 0; k < kU; ++k) {
-                    const int wv = i0 + lane + 64 * k;
-                    const size_t nw = (size_t)G.n_wave;
-                    const unsigned long long* a = k6tag + min(wv, max(G.n_wave - 1, 0));
+                for (int k = 0; k < kU; ++k)
+                    if (pend & (1u << k)) {
+                        const unsigned long long* a = k6tag + (i0 + lane + 64 * k);
 #pragma unroll
-                    for (int j = 0; j < kPartD; ++j) {
-                        wd[k][j][0] = __hip_atomic_load(a + (2 * j) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        wd[k][j][1] = __hip_atomic_load(a + (2 * j + 1) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        for (int j = 0; j < kPartD; ++j) {
+                            wd[k][j][0] = __hip_atomic_load(a + (2 * j) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            wd[k][j][1] = __hip_atomic_load(a + (2 * j + 1) * nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
                     }
 #pragma unroll
-                    for (int j = 0; j < kPartD; ++j)
-                        ok &= wv >= G.n_wave || ((unsigned)(wd[k][j][0] >> 32) == g32 && (unsigned)(wd[k][j][1] >> 32) == g32);
-                }
-                if (__all(ok)) break;
+                for (int k = 0; k < kU; ++k)
+                    if (pend & (1u << k)) {
+                        bool ok = true;
+#pragma unroll
+                        for (int j = 0; j < kPartD; ++j)
+                            ok &= (unsigned)(wd[k][j][0] >> 32) == g32 && (unsigned)(wd[k][j][1] >> 32) == g32;
+                        if (ok) pend &= ~(1u << k);
+                    }
+                if (__all(pend == 0)) break;
                 if (++spins > (1ll << 25)) {
                     late = true;
                     break;
