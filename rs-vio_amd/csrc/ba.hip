@@ -387,6 +387,10 @@ __device__ __forceinline__ bool ll_group_sums(const unsigned long long* mine, in
     return late;
 }
 
+// s_waitcnt immediate (gfx9 encoding) for vmcnt(0) with expcnt / lgkmcnt left at their maxima: this
+// wave's outstanding memory operations -- its stores included -- have completed
+constexpr int kWaitStores = 0x0F70;
+
 template <int SCOPE>
 __device__ __forceinline__ void ll_put_scope(unsigned long long* w, double v, unsigned g) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v), t = (unsigned long long)g << 32;
@@ -1869,7 +1873,7 @@ __device__ bool combine_p2p_ll(const Geometry& G, const Work& Wk, double* M, dou
     // poll the 6 scalar words of each rank and read the entries once (still tag-checked), instead
     // of every thread re-reading all its entries' words of every rank until they arrive -- traffic
     // that, with four ranks on one GPU, starved the last rank's own progress until the spin bound
-    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_waitcnt(kWaitStores);
     __syncthreads();
     if (tid < nr) {  // lane r pushes the scalars to rank r
         unsigned long long* d = p2p_llsys(P.peer[tid], par, me) + 2 * (size_t)ne;
@@ -3447,7 +3451,7 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p4(Geometry G, Pr
         if (s.done || !s.solve_ok) return;  // (k6_body's own early exit: no partials, no decision pending)
         // this wave's partial stores complete before its ticket (vmcnt(0): a store at device scope
         // is acknowledged once it is visible at that scope), so the last ticket sees every partial
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_s_waitcnt(kWaitStores);
         unsigned t = 0;
         if (threadIdx.x == 0) t = __hip_atomic_fetch_add(k6cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __builtin_amdgcn_readfirstlane(t);
