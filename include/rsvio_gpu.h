@@ -415,7 +415,9 @@ typedef struct {
     double translation_norm;   /* ||t_rel|| (estimator.rs:206) */
     double rotation_norm;      /* ||euler(R_rel)|| (:207-212) */
     double T_W_B[16];          /* row-major; identity on failure (frame.rs:95, state.rs:26) */
-} rsvio_motion_result;        /* 176 bytes */
+    double kernel_ms;          /* device time of the launch: its first wave's entry to the result
+                                  write (the device wall clock; no host or copy time) */
+} rsvio_motion_result;        /* 184 bytes */
 
 int rsvio_pnp_create(int32_t device, rsvio_pnp** out);
 void rsvio_pnp_destroy(rsvio_pnp* p);

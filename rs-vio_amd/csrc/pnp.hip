@@ -57,6 +57,7 @@ struct PnpArgs {
     int max_iter;
     double cost_tol, param_tol, huber_delta, lambda0, thr_t, thr_r;
     rsvio_motion_result* out;  // pinned host memory
+    double wclk_khz;           // device wall clock rate (kernel_ms)
 };
 
 struct Ctl {
@@ -330,7 +331,7 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
     C->run = 0;
 }
 
-__device__ void pnp_finish(const PnpArgs& A, const Ctl& C) {
+__device__ void pnp_finish(const PnpArgs& A, const Ctl& C, unsigned long long t_entry) {
     rsvio_motion_result r;
     r.status = C.status;
     r.iterations = C.it;
@@ -357,6 +358,7 @@ __device__ void pnp_finish(const PnpArgs& A, const Ctl& C) {
         for (int k = 0; k < 16; ++k) r.T_W_B[k] = (k % 5 == 0) ? 1.0 : 0.0;
         r.is_keyframe = 1;
     }
+    r.kernel_ms = (double)(wall_clock64() - t_entry) / A.wclk_khz;
     *A.out = r;
 }
 
@@ -375,6 +377,7 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
     __shared__ int s_nobs;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     STAMP(0);
+    const unsigned long long t_entry = wall_clock64();  // (kept by thread 0 for kernel_ms)
     const int n0 = A.dcount ? A.dcount[0] : A.n[0];
     const int n1 = A.dcount ? A.dcount[1] : A.n[1];
     const int nf = n0 + n1;
@@ -562,7 +565,7 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
         if (tid == 0) pnp_control(A, &C, s_sum, s_pose);
     }
     STAMP(28);
-    if (tid == 0) pnp_finish(A, C);
+    if (tid == 0) pnp_finish(A, C, t_entry);
     STAMP(29);
 }
 
@@ -581,6 +584,7 @@ struct Pnp {
     DevBuf<uint8_t> feat;            // [ids_l | ids_r | uv_l | uv_r]
     HostBuf<uint8_t> hfeat;
     HostBuf<rsvio_motion_result> hres;
+    double wclk_khz = 1.0e5;
     double q0_key[16] = {};              // T_W_B_last_kf of the cached initial quaternion
     double q0[4] = {1.0, 0.0, 0.0, 0.0};
 
@@ -589,6 +593,10 @@ struct Pnp {
         RSVIO_HIP(hipSetDevice(dev));
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         hres.alloc(1);
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+            wclk_khz = khz;
+        (void)hipGetLastError();
     }
     ~Pnp() {
         if (stream) (void)hipStreamDestroy(stream);
@@ -611,6 +619,7 @@ PnpArgs make_args(Pnp& p, const double* T_last, const double* TCB2, const rsvio_
     A.thr_t = rule->translation_threshold;
     A.thr_r = rule->rotation_threshold;
     A.out = p.hres.p;
+    A.wclk_khz = p.wclk_khz;
     // sliding_window.rs:506-517: F starts from the last keyframe's T_B_W = inv(T_W_B) with
     // q = UnitQuaternion::from_matrix(R_B_W); cached per keyframe pose
     if (std::memcmp(p.q0_key, T_last, sizeof p.q0_key) != 0) {

@@ -67,7 +67,8 @@ class KeyframeRule(C.Structure):
 class MotionResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("iterations", C.c_int32), ("is_keyframe", C.c_int32),
                 ("n_observations", C.c_int32), ("initial_cost", C.c_double), ("final_cost", C.c_double),
-                ("translation_norm", C.c_double), ("rotation_norm", C.c_double), ("T_W_B", C.c_double * 16)]
+                ("translation_norm", C.c_double), ("rotation_norm", C.c_double), ("T_W_B", C.c_double * 16),
+                ("kernel_ms", C.c_double)]
 
 
 class BaParams(C.Structure):

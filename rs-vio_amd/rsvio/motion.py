@@ -32,6 +32,7 @@ class MotionResult:
     translation_norm: float
     rotation_norm: float
     T_W_B: np.ndarray
+    kernel_ms: float = 0.0  # device time of the launch (wall clock; no host or copy time)
 
     @property
     def success(self) -> bool:
@@ -41,7 +42,8 @@ class MotionResult:
 
 def _result(r: _lib.MotionResult) -> MotionResult:
     return MotionResult(r.status, r.iterations, bool(r.is_keyframe), r.n_observations, r.initial_cost, r.final_cost,
-                        r.translation_norm, r.rotation_norm, np.array(r.T_W_B[:], np.float64).reshape(4, 4))
+                        r.translation_norm, r.rotation_norm, np.array(r.T_W_B[:], np.float64).reshape(4, 4),
+                        r.kernel_ms)
 
 
 class MotionTracker:
