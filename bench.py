@@ -640,7 +640,10 @@ def max_over_ranks(x: float, world: int) -> float:
 def cu_partition(device: int, frac: float, layout: str):
     """CU sets for the tracker and the BA streams (hipExtStreamCreateWithCUMask): the tracker's
     900 latency-bound one-wave workgroups otherwise share SIMDs with the BA's serial kernels.
-    layout "stride": the tracker takes every k-th CU (all XCDs); "block": a contiguous range."""
+    layout "block": mask bits 0..k-1 -- bit i is CU i // 8 of XCD i % 8, so the tracker gets k / 8 CUs
+    on every XCD; "stride": every (n / k)-th bit, which for k = n / 4 names XCDs 0 and 4 only -- a
+    mask that leaves an XCD empty is not honoured, and both streams then run on every CU
+    (tools/xcd_map.hip)."""
     import ctypes as C
 
     from rsvio import _lib
