@@ -827,6 +827,18 @@ class TrackerWorkload:
         self.slot = 1 - self.slot
         self.k += 1
 
+    def precapture(self, pcie: bool, uploaded: bool):
+        """Capture every phase's frame graph up front (a caller captures at start-up, not in its
+        first timed frames): hipGraphInstantiate costs ~1 ms of host time, which a first use
+        inside a timed repetition would add to that repetition alone."""
+        if not self.graphs:
+            return
+        s = self.stream.cuda_stream
+        for phase in range(len(self.seq)):
+            key = (phase, pcie, uploaded)
+            if key not in self._graphs:
+                self._graphs[key] = self._capture(self._plan(phase, pcie), pcie, uploaded, s)
+
     def _capture(self, plan, pcie, uploaded, s):
         """Capture the frame's enqueue sequence on the tracker stream (relaxed mode) into an
         instantiated graph executable."""
@@ -1141,8 +1153,14 @@ def main():
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
+    ap.add_argument("--precapture-graphs", type=int, default=1,
+                    help="1: capture the tracker's per-phase frame graphs before the timed region (0: on first "
+                         "use, as rounds 4-5 did -- one repetition then pays the instantiations)")
     ap.add_argument("--collective", default="auto", choices=["auto", "rccl", "p2p"],
                     help="BA exchange for N>1: P2P one-shot all-reduce (auto: if every rank attaches) or RCCL")
+    ap.add_argument("--trace-steps", default="",
+                    help="write every timed protocol step's host phase times (upload, set_problem, solve start, "
+                         "frame enqueue, frame wait, solve wait, state read-back) to this JSON file")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: all ranks on cuda:0, gloo control group, P2P exchange")
     args = ap.parse_args()
@@ -1192,18 +1210,37 @@ def main():
         (split): the frame's image upload first (as soon as the frame is there), then the window
         and the solve, then the frame's kernels and downloads; --order ba-first: the window and
         the solve before the whole frame; --order frame-first the other way round."""
+        tr = trace is not None and timed
+        if tr:
+            m = [time.perf_counter()]
         if args.order == "frame-first":
             trk.step(timed, pcie=True, wait=False)
         elif args.order == "split":
             trk.upload()
+        if tr:
+            m.append(time.perf_counter())
         ba.next_window()
+        if tr:
+            m.append(time.perf_counter())
         ba.start()
+        if tr:
+            m.append(time.perf_counter())
         if args.order != "frame-first":
             trk.step(timed, pcie=True, wait=False, uploaded=args.order == "split")
+        if tr:
+            m.append(time.perf_counter())
         trk.sync()
+        if tr:
+            m.append(time.perf_counter())
         ba.finish(timed)
+        if tr:
+            m.append(time.perf_counter())
         ba.ba.state(state_out)
+        if tr:
+            m.append(time.perf_counter())
+            trace.append(m)
 
+    trace = [] if args.trace_steps else None
     # the optimised state comes back into reused host arrays, as a Rust caller would keep them
     state_out = (np.empty((ba.prob.n_kf, 7)), np.empty((ba.prob.n_lm, 3)))
 
@@ -1221,6 +1258,8 @@ def main():
             gc.enable()
         return out
 
+    if args.precapture_graphs:
+        trk.precapture(False, False)
     for _ in range(args.warmup):
         resident_step(False)
     el_res = timed_reps(resident_step, args.reps)
@@ -1230,9 +1269,17 @@ def main():
     ba.iters.clear()
     ba.solve_ms.clear()
     trk.enable_pcie()
+    if args.precapture_graphs:
+        trk.precapture(True, args.order == "split")
     for _ in range(max(args.warmup, 2)):
         protocol_step(False)
     el_pro = timed_reps(protocol_step, args.reps)
+    if trace is not None:
+        names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
+        with open(args.trace_steps, "w") as f:
+            json.dump({"phases": names, "steps_per_rep": args.steps,
+                       "us": [[round(1e6 * (b - a), 1) for a, b in zip(m, m[1:])] for m in trace],
+                       "t0_us": [round(1e6 * (m[0] - trace[0][0]), 1) for m in trace]}, f)
     elapsed = float(np.median(el_pro))
     elapsed_res = float(np.median(el_res))
 
@@ -1264,6 +1311,8 @@ def main():
                       "uploaded (rsvio_ba_set_problem: sort, tables, pinned staging, H2D; two windows "
                       "alternate) and solved (graph re-captured), its state (48.6 KB) D2H",
         "value_reps": [round(frames / e, 3) for e in el_pro],
+        "value_reps_min": round(frames / max(el_pro), 3),
+        "value_reps_max": round(frames / min(el_pro), 3),
         "value_resident": round(value_res, 3),
         "ms_per_step_resident": round(1e3 * elapsed_res / args.steps, 4),
         "value_resident_note": "inputs resident in HBM, the same window re-solved each step (its graph "

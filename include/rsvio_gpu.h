@@ -390,6 +390,12 @@ int rsvio_ba_detach_p2p(rsvio_ba* ba);
  * doubles (1 <= n <= 8192) over reps back-to-back exchanges after one warm-up; collective --
  * every attached rank makes the same call.  Reported by bench.py at N > 1. */
 int rsvio_ba_p2p_latency(rsvio_ba* ba, int32_t reps, int32_t n, double* us_out);
+/* Diagnostics (no reference counterpart): the exchange form the current problem's LM iterations
+ * take -- -1 not P2P-sharded; 0 five launches (X1, X2); 1 four (K5 exchanges the system, X2 the
+ * trial scalars); 2, 3, 4 three (the trial exchange folded into K6 / the next decision).  Level 3
+ * (the default) needs K6's whole grid resident on the stream's CUs at once (its reducer workgroup
+ * waits inside the grid); a problem past that capacity takes level 1, bit-identically. */
+int rsvio_ba_p2p_level(rsvio_ba* ba, int32_t* level_out);
 
 /* ===== B8: motion tracking (PnP) + keyframe rule (SlidingWindow::track_motion) ===== */
 

@@ -740,7 +740,8 @@ int orc_ba_solve(int n_kf, double* pose7, const uint8_t* kf_fixed, int n_lm, dou
         double rho = dcost / pred;
         if (std::isfinite(new_cost) && std::fabs(dcost) <= cfg->cost_tolerance * cost) {
             // converged: |change| within the tolerance whatever its sign; the candidate is not
-            // applied (DESIGN.md section 5 -- a rounding-level change decides nothing)
+            // applied (DESIGN.md section 5 -- a rounding-level change decides nothing).  This
+            // build's rule, a deliberate departure: apex-solver's is absent offline (unpinned)
             status = LM_COST_TOL;
             break;
         }

@@ -388,7 +388,11 @@ __device__ __forceinline__ bool ll_group_sums(const unsigned long long* mine, in
 }
 
 // s_waitcnt immediate (gfx9 encoding) for vmcnt(0) with expcnt / lgkmcnt left at their maxima: this
-// wave's outstanding memory operations -- its stores included -- have completed
+// wave's outstanding memory operations -- its stores included -- have completed.  The encoding (and
+// stores counted by vmcnt, no separate store counter) is gfx9's: the build targets gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "kWaitStores is the gfx9 s_waitcnt encoding: build for gfx950 (ARCH=gfx950)"
+#endif
 constexpr int kWaitStores = 0x0F70;
 
 template <int SCOPE>
@@ -971,7 +975,8 @@ __device__ void lm_update(LmState& s, double cost, const double tv[4], int max_i
                 // converged: the candidate's cost change is within the
                 // tolerance, whatever its sign, and the candidate is not applied -- so a change
                 // at rounding level, whose sign two summation orders may disagree on, decides
-                // neither the outcome nor the state
+                // neither the outcome nor the state.  This build's rule, NOT apex-solver's (absent
+                // offline, parity unpinned): a deliberate departure, DESIGN.md section 5
                 s.status = RSVIO_LM_COST_TOLERANCE;
                 s.done = 1;
             } else if (isfinite(s.new_cost) && rho > 0.0) {
@@ -3231,8 +3236,15 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p(Geometry G, Pro
 // fixed-pairing wave sums, + |x|^2 of the free poses on rank 0), pushes the 4 scalars to every
 // peer flag-in-word (the X2 exchange's slots and generation), polls the peers', and writes the
 // rank-ordered sums to trial4 -- the same bits X2 wrote, read by the next K4c / K7 after the
-// boundary.  It is dispatched last, after every wave it waits for (all of K6 is co-resident), and
-// its spins are bounded like every exchange's (the error flag the host checks).
+// boundary.  Forward progress: the reducer waits inside the grid for the other n_wave workgroups,
+// so it needs them all dispatched -- HIP does not promise in-order dispatch or co-residency, it
+// relies on (a) the dispatcher handing out workgroups in index order (the reducer is the last
+// index) and (b) the whole grid fitting the stream's CUs at once.  (b) is checked on the host:
+// fold 3 is taken only while n_wave + 1 <= the resident capacity of this kernel on the stream's CU
+// mask (occupancy x CUs, divided among the ranks sharing the device), else the iteration falls back
+// to fold 1 (plain K6 + X2, the same exchange slots and generation: bit-identical, and ranks may
+// differ in the choice); see BA::k6_fits.  Its spins are bounded like every exchange's (the error
+// flag the host checks), so a broken assumption fails the solve instead of hanging it.
 // KU: waves per lane and sweep (4 when n_wave <= 256: the sums of the waves past the last are
 // zeros either way, so trial_scalars_wave's 8 give the same bits; half the uncached words per sweep)
 template <int KU>
@@ -3450,12 +3462,17 @@ __global__ __launch_bounds__(64) void ba_backsub_relinearize_p2p4(Geometry G, Pr
         const LmState s = *Wk.st;
         if (s.done || !s.solve_ok) return;  // (k6_body's own early exit: no partials, no decision pending)
         // this wave's partial stores complete before its ticket (vmcnt(0): a store at device scope
-        // is acknowledged once it is visible at that scope), so the last ticket sees every partial
+        // is acknowledged once it is visible at that scope), and the ticket is an agent-scope
+        // acquire-release: the fence releases every lane's partials with it, and the last ticket's
+        // acquire fence orders k6_last_push's loads after every other wave's release (the HIP memory
+        // model's guarantee, not only the store counter's)
         __builtin_amdgcn_s_waitcnt(kWaitStores);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         unsigned t = 0;
-        if (threadIdx.x == 0) t = __hip_atomic_fetch_add(k6cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) t = __hip_atomic_fetch_add(k6cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         t = __builtin_amdgcn_readfirstlane(t);
         if (t != (unsigned)G.n_wave - 1) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (threadIdx.x == 0) __hip_atomic_store(k6cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         k6_last_push(G, Pr, Wk, P, xgen, gen, k6part, s);
     } else {
@@ -4035,7 +4052,12 @@ struct BundleAdjuster {
     bool p2p_shared_gpu = false;  // attach_p2p found two ranks on one device (fold 2 -> 1, 4 -> 3)
     bool p2p_fold() const { return fold_lvl >= 1 && coll == 2 && k5_variant == 2 && G.n_free <= 10; }
     bool p2p_fold2() const { return fold_lvl == 2 && p2p_fold(); }
-    bool p2p_fold3() const { return fold_lvl == 3 && p2p_fold(); }
+    bool p2p_fold3() const { return fold_lvl == 3 && p2p_fold() && k6_fits(); }
+    // fold 3's reducer waits inside K6's grid for the other workgroups: only while the whole grid
+    // (n_wave + 1 one-wave workgroups) fits the stream's resident capacity at once
+    int k6_cap = 0;               // resident K6 workgroups on this stream's CUs (refresh_k6_cap)
+    bool k6_fits() const { return G.n_wave + 1 <= k6_cap; }
+    int p2p_share = 1;            // ranks on this rank's device (attach_p2p)
     bool p2p_fold4() const { return fold_lvl == 4 && p2p_fold(); }
     const WinDesc* dptr() const { return reinterpret_cast<const WinDesc*>(d_arena.p + lay.desc); }
     void fill_desc(WinDesc& d) const {
@@ -4997,11 +5019,42 @@ struct BundleAdjuster {
         // peer's K6 of CUs; they take the nearest level that waits inside K6 or K5 instead)
         fold_lvl = shared_gpu && !keep2 && (fold_req == 2 || fold_req == 4) ? fold_req - 1 : fold_req;
         p2p_shared_gpu = shared_gpu;
+        p2p_share = 0;
+        for (int a = 0; a < nr; ++a) p2p_share += out[6 + a] == out[6 + rk];
+        refresh_k6_cap();
         p2p = P;
         nranks = nr;
         rank = rk;
         coll = 2;
         drop_graph();  // the iteration's launch sequence changes with the collective
+    }
+
+    // fold 3's resident capacity: K6 workgroups per CU (occupancy of the reducer kernel, one wave
+    // each) x the CUs the stream may use (its CU mask), shared among the ranks on this device
+    void refresh_k6_cap() {
+        int per_cu = 0;
+        RSVIO_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(ba_backsub_relinearize_p2p3), 64, 0));
+        int n_cu = 0;
+        RSVIO_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, P.device));
+        uint32_t mask[32] = {};
+        if (hipExtStreamGetCUMask(stream, 32, mask) == hipSuccess) {
+            int c = 0;
+            for (uint32_t w : mask) c += __builtin_popcount(w);
+            if (c > 0) n_cu = std::min(n_cu, c);
+        } else {
+            (void)hipGetLastError();
+        }
+        const char* ov = std::getenv("RSVIO_K6_CAP");  // test hook: pretend a smaller capacity
+        k6_cap = per_cu * n_cu / std::max(p2p_share, 1);
+        if (ov && ov[0]) k6_cap = std::min(k6_cap, std::atoi(ov));
+    }
+    // the exchange level the current problem's iterations take: -1 not P2P-sharded, 0 X1 + X2
+    // launches, 1 K5 exchange + X2, 2 / 3 / 4 the folded trial exchanges
+    int p2p_level() const {
+        if (coll != 2) return -1;
+        if (!p2p_fold()) return 0;
+        return p2p_fold2() ? 2 : p2p_fold3() ? 3 : p2p_fold4() ? 4 : 1;
     }
 
     // measured exchange latency: one warm-up exchange (absorbs the ranks' start skew), then reps
@@ -5048,6 +5101,10 @@ struct BundleAdjuster {
         } else if (!own_stream) {
             RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
             own_stream = true;
+        }
+        if (coll == 2) {
+            refresh_k6_cap();
+            drop_graph();  // (fold 3 may come or go with the stream's CUs)
         }
     }
 
@@ -5571,6 +5628,14 @@ int rsvio_ba_p2p_latency(rsvio_ba* ba, int32_t reps, int32_t n, double* us_out) 
     if (!ba || !us_out) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {
         *us_out = ba->b.p2p_latency(reps, n);
+        return (int)RSVIO_OK;
+    });
+}
+
+int rsvio_ba_p2p_level(rsvio_ba* ba, int32_t* level_out) {
+    if (!ba || !level_out) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        *level_out = ba->b.p2p_level();
         return (int)RSVIO_OK;
     });
 }

@@ -269,7 +269,8 @@ __device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double*
         const double rho = dcost / C->pred;
         if (isfinite(new_cost) && fabs(dcost) <= A.cost_tol * C->cost) {
             // converged: the change is within the tolerance whatever its sign, the candidate not
-            // applied (the BA's lm_update takes the same decision)
+            // applied (the BA's lm_update takes the same decision).  This
+            // build's rule, a deliberate departure: apex-solver's is absent offline (unpinned)
             C->status = LM_COST_TOL;
             done = true;
         } else if (isfinite(new_cost) && rho > 0.0) {

@@ -150,6 +150,7 @@ SIG = {
     "rsvio_ba_attach_p2p": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
     "rsvio_ba_p2p_latency": (C.c_int, [P, C.c_int32, C.c_int32, C.POINTER(C.c_double)]),
     "rsvio_ba_detach_p2p": (C.c_int, [P]),
+    "rsvio_ba_p2p_level": (C.c_int, [P, C.POINTER(C.c_int32)]),
     "rsvio_stream_create": (C.c_int, [C.c_int32, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(P)]),
     "rsvio_stream_destroy": (C.c_int, [P]),
     "rsvio_ba_wait": (C.c_int, [P, C.POINTER(BaResult)]),

@@ -145,6 +145,13 @@ class BundleAdjuster:
         check(_lib.load().rsvio_ba_p2p_latency(self._h, reps, n, C.byref(us)))
         return us.value
 
+    def p2p_level(self) -> int:
+        """The exchange form of the current problem's iterations (rsvio_ba_p2p_level): -1 not
+        P2P-sharded, else the fold level taken (3 only while K6's grid fits the stream's CUs)."""
+        v = C.c_int32(0)
+        check(_lib.load().rsvio_ba_p2p_level(self._h, C.byref(v)))
+        return v.value
+
     def detach_p2p(self) -> None:
         check(_lib.load().rsvio_ba_detach_p2p(self._h))
 

@@ -781,7 +781,25 @@ def test_sharded_p2p_six_ranks_match_oracle(gpu, oracle, tmp_path):
     assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
 
 
-@pytest.mark.parametrize("level,world,per_rank", [("4", 2, 2000), ("4", 4, 2000), ("3", 2, 2000), ("3", 2, 7000),
+def test_sharded_p2p_eight_ranks_match_oracle(gpu, oracle, tmp_path):
+    """Eight ranks (eight processes on one GPU), the node's full group: K5 pulls the 7 peers'
+    slots in one group of 8, the exchange uses all 8 parity slots per generation and the trial
+    exchange spans 8 x 4 flag-in-word scalars.  2,000 landmarks per rank = the oracle's
+    16,000-landmark, 192,000-observation solve; every rank ends with bitwise the same poses and LM
+    outcome, within the config-3 tolerances of the oracle."""
+    from rsvio import synthetic as S
+    rs = _run_p2p(8, 16000, tmp_path)
+    for r in rs[1:]:
+        assert np.array_equal(rs[0]["pose"], r["pose"]) and np.array_equal(rs[0]["res"], r["res"])
+    full = S.ba_problem(n_lm=16000)
+    po, pwo, ro = oracle.ba_solve(full)
+    assert int(rs[0]["res"][0]) == ro.status and int(rs[0]["res"][1]) == ro.iterations
+    assert abs(rs[0]["res"][2] - ro.final_cost) <= 1e-8 * ro.initial_cost
+    assert np.abs(rs[0]["pose"] - po).max() < 1e-7
+    assert np.abs(np.concatenate([r["pw"] for r in rs]) - pwo).max() < 1e-6
+
+
+@pytest.mark.parametrize("level,world,per_rank", [("3", 8, 2000), ("4", 2, 2000), ("4", 4, 2000), ("3", 2, 2000), ("3", 2, 7000),
                                                   ("2", 2, 2000), ("0", 2, 2000)])
 def test_sharded_p2p_fold_equals_separate_exchange(gpu, tmp_path, level, world, per_rank):
     """The 4-launch iteration (RSVIO_P2P_FOLD=1: the reduced system's exchange in K5's prologue,
@@ -814,6 +832,67 @@ def test_sharded_p2p_flag_in_word_equals_flag_protocol(gpu, tmp_path, world):
     ll = _run_p2p(world, 2000 * world, tmp_path / "a", env={"RSVIO_P2P_LL": "1"})
     fl = _run_p2p(world, 2000 * world, tmp_path / "b")
     for a, b in zip(ll, fl):
+        for k in ("pose", "pw", "res"):
+            assert np.array_equal(a[k], b[k]), k
+
+
+def _cap_worker(rank, world, port, out_dir, n_cu):
+    import os
+
+    import torch.distributed as dist
+    os.environ["RSVIO_P2P_FOLD"] = "3"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rsvio import synthetic as S
+        from rsvio._lib import CuStream
+        from rsvio.ba import BundleAdjuster
+        shard = S.ba_problem(n_lm=2000 * world).shard(rank, world)
+        ba = BundleAdjuster(max_keyframes=21, max_landmarks=shard.n_lm, max_observations=shard.n_obs)
+        # n_cu CUs: mask bits 0 .. n_cu - 1 = CU i // 8 of XCD i % 8 (every XCD keeps a CU)
+        st = CuStream(0, list(range(n_cu))) if n_cu else None
+        if st:
+            ba.set_stream(st.ptr)
+        mine = ba.p2p_export(world)
+        handles = [None] * world
+        dist.all_gather_object(handles, mine)
+        ba.attach_p2p(world, rank, handles)
+        ba.set_problem_from(shard)
+        level = ba.p2p_level()
+        r = ba.run()
+        pose, pw = ba.state()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), pose=pose, pw=pw, level=level,
+                 res=np.array([r.status, r.iterations, r.final_cost, r.initial_cost]))
+        ba.close()
+        if st:
+            st.close()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fold3_refused_past_resident_capacity(gpu, tmp_path):
+    """ADVICE/verdict r05: fold 3's reducer waits inside K6's grid for the other workgroups, so the
+    handle takes fold 3 only while n_wave + 1 <= K6's resident capacity on its stream's CU mask
+    (shared among the ranks on the device).  Two ranks on an 8-CU stream (capacity far below a
+    2,000-landmark shard's waves) report level 1 and solve bit-identically to two ranks on the
+    whole GPU at level 3."""
+    import socket
+
+    import torch.multiprocessing as mp
+    outs = {}
+    for n_cu in (0, 8):
+        d = tmp_path / f"cu{n_cu}"
+        d.mkdir()
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        mp.start_processes(_cap_worker, args=(2, port, str(d), n_cu), nprocs=2, join=True, start_method="spawn")
+        outs[n_cu] = [np.load(d / f"r{r}.npz") for r in range(2)]
+    assert [int(r["level"]) for r in outs[0]] == [3, 3]
+    assert [int(r["level"]) for r in outs[8]] == [1, 1]
+    for a, b in zip(outs[0], outs[8]):
         for k in ("pose", "pw", "res"):
             assert np.array_equal(a[k], b[k]), k
 
