@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import resource
 import math
 import os
 import sys
@@ -595,6 +596,20 @@ def pmc_traffic(kernel: str, shape: str = "u8_gath"):
                           "fetch_multiplier": round(mult, 4), "multiplier_source": msrc}
 
 
+def _read_text(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _minor_faults() -> int:
+    """This process's minor page faults so far (/proc/self/stat field 10)."""
+    t = _read_text("/proc/self/stat")
+    return int(t.rsplit(")", 1)[1].split()[7]) if t else -1
+
+
 def setup_dist(same_device: bool = False):
     """One process per GPU over RCCL.  `same_device` is a rehearsal mode for a one-GPU box: every
     rank on cuda:0 with a gloo control group (RCCL refuses two ranks on one device)."""
@@ -1043,6 +1058,27 @@ class BAWorkload:
         alt = S.ba_problem(n_lm=2000 * world, seed=17, init_seed=23)
         self.windows = [self.prob, alt.shard(rank, world) if world > 1 else alt]
         self.k = 0
+        self._pinned = []
+
+    def pin_windows(self):
+        """The windows' host arrays in page-locked memory (as a caller that builds its keyframe
+        windows in a pinned arena would): set_problem's observation pass reads ~0.6 MB of them per
+        window, and on pageable memory the kernel's NUMA-balancing scan occasionally unmaps those
+        pages, so one pass in a few hundred took ~6.7 ms of hinting faults (profiles/r06b_*)."""
+        import dataclasses
+
+        import torch
+        out = []
+        for w in self.windows:
+            repl = {}
+            for f in ("pose7", "kf_fixed", "p_W", "obs_lm", "obs_kf", "obs_cam", "obs_uv", "T_C_B2"):
+                a = np.ascontiguousarray(getattr(w, f))
+                t = torch.empty(a.shape, dtype=getattr(torch, str(a.dtype)), pin_memory=True)
+                t.numpy()[...] = a
+                self._pinned.append(t)
+                repl[f] = t.numpy()
+            out.append(dataclasses.replace(w, **repl))
+        self.windows = out
 
     def next_window(self):
         """Upload the next keyframe window (rsvio_ba_set_problem through the handle's pinned
@@ -1153,6 +1189,9 @@ def main():
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
+    ap.add_argument("--pin-windows", type=int, default=1,
+                    help="1: the keyframe windows' host arrays in page-locked memory (0: pageable numpy arrays, "
+                         "where an occasional NUMA-balancing scan stalls one set_problem for ~6.7 ms)")
     ap.add_argument("--precapture-graphs", type=int, default=1,
                     help="1: capture the tracker's per-phase frame graphs before the timed region (0: on first "
                          "use, as rounds 4-5 did -- one repetition then pays the instantiations)")
@@ -1212,6 +1251,7 @@ def main():
         the solve before the whole frame; --order frame-first the other way round."""
         tr = trace is not None and timed
         if tr:
+            f0 = (resource.getrusage(resource.RUSAGE_SELF).ru_minflt, resource.getrusage(1).ru_minflt)
             m = [time.perf_counter()]
         if args.order == "frame-first":
             trk.step(timed, pcie=True, wait=False)
@@ -1239,8 +1279,11 @@ def main():
         if tr:
             m.append(time.perf_counter())
             trace.append(m)
+            trace_flt.append((resource.getrusage(resource.RUSAGE_SELF).ru_minflt - f0[0],
+                              resource.getrusage(1).ru_minflt - f0[1]))  # 1: RUSAGE_THREAD
 
     trace = [] if args.trace_steps else None
+    trace_flt = []
     # the optimised state comes back into reused host arrays, as a Rust caller would keep them
     state_out = (np.empty((ba.prob.n_kf, 7)), np.empty((ba.prob.n_lm, 3)))
 
@@ -1269,17 +1312,24 @@ def main():
     ba.iters.clear()
     ba.solve_ms.clear()
     trk.enable_pcie()
+    if args.pin_windows:
+        ba.pin_windows()
     if args.precapture_graphs:
         trk.precapture(True, args.order == "split")
     for _ in range(max(args.warmup, 2)):
         protocol_step(False)
+    minflt0 = _minor_faults()
     el_pro = timed_reps(protocol_step, args.reps)
+    minflt = _minor_faults() - minflt0
     if trace is not None:
         names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
         with open(args.trace_steps, "w") as f:
             json.dump({"phases": names, "steps_per_rep": args.steps,
                        "us": [[round(1e6 * (b - a), 1) for a, b in zip(m, m[1:])] for m in trace],
-                       "t0_us": [round(1e6 * (m[0] - trace[0][0]), 1) for m in trace]}, f)
+                       "t0_us": [round(1e6 * (m[0] - trace[0][0]), 1) for m in trace],
+                       "minor_faults_process_thread": trace_flt,
+                       "thp": _read_text("/sys/kernel/mm/transparent_hugepage/enabled"),
+                       "thp_defrag": _read_text("/sys/kernel/mm/transparent_hugepage/defrag")}, f)
     elapsed = float(np.median(el_pro))
     elapsed_res = float(np.median(el_res))
 
@@ -1312,6 +1362,8 @@ def main():
                       "alternate) and solved (graph re-captured), its state (48.6 KB) D2H",
         "value_reps": [round(frames / e, 3) for e in el_pro],
         "value_reps_min": round(frames / max(el_pro), 3),
+        "protocol_minor_faults": minflt,
+        "host_numa_balancing": _read_text("/proc/sys/kernel/numa_balancing"),
         "value_reps_max": round(frames / min(el_pro), 3),
         "value_resident": round(value_res, 3),
         "ms_per_step_resident": round(1e3 * elapsed_res / args.steps, 4),

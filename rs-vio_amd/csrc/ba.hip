@@ -181,6 +181,10 @@ struct Geometry {
     Mat4 TCB[2];
     double huber_delta;
     int chol;  // linear solver: 0 Schur (inv3 landmark blocks), 1 the SparseCholesky fallback (LL^T)
+    // the symbolic envelope of the camera system: env[k] = the last free keyframe whose rows of
+    // column block k may be nonzero in L (>= k; a window of landmarks over consecutive keyframes
+    // gives a band), set_problem from the landmarks' keyframe masks
+    unsigned char env[kMaxFree];
 };
 
 // Structure-of-arrays problem description (device pointers)
@@ -1325,6 +1329,53 @@ __global__ __launch_bounds__(256) void ba_schur_combine(Geometry G, Prob Pr, Wor
     if (threadIdx.x == 0) *Wk.singular = 0;
 }
 
+// K4d-wide (single rank, 11..20 free keyframes, round 6): the 8 partial systems summed into sys
+// by many workgroups -- one entry per thread, the partials in slot order then + lambda on the
+// diagonal, exactly combine_system's operations -- so the camera solve's one workgroup pulls one
+// system (55 KB at W=20) instead of eight (440 KB: 28k of K5's 128k cycles, one CU's bandwidth,
+// profiles/r06c_c5_k5_stamps.txt).  Block 0 also sums the initial cost (K4's wave partials, as
+// combine_system) and copies the singular flag; K5 then reads sys through the map (combine = 0).
+__global__ __launch_bounds__(256) void ba_schur_combine_wide(Geometry G, Prob Pr, Work Wk) {
+    const LmState* st = Wk.st;
+    if (st->done) return;
+    const int n_e = G.n_pb * 36 + 12 * G.n_free;
+    const size_t L = sys_len(G);
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    constexpr int kU = 16;
+    const int lane = threadIdx.x;
+    double pa[kU];
+    int sing = 0;
+    if (blockIdx.x == 0 && lane < 64) {
+#pragma unroll
+        for (int k = 0; k < kU; ++k) pa[k] = lane + 64 * k < G.n_wave ? Wk.partA[(lane + 64 * k) * kPartA] : 0.0;
+        sing = *Wk.singular;
+    }
+    const double lambda = st->lambda;
+    if (e < n_e) {
+        double v[kGrp];
+#pragma unroll
+        for (int x = 0; x < kGrp; ++x) v[x] = Wk.cpart[(size_t)x * L + e];
+        double a = v[0];
+#pragma unroll
+        for (int x = 1; x < kGrp; ++x) a += v[x];
+        // a diagonal entry (k, k) of a diagonal camera block (f, f): pb = f n - f (f - 1) / 2
+        const int pb = e / 36, k = e % 36;
+        if (pb < G.n_pb && k % 7 == 0 && Pr.pb_fa[pb] == Pr.pb_fb[pb]) a += lambda;
+        Wk.sys[e] = a;
+    }
+    if (blockIdx.x == 0 && lane < 64) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < kU; ++k) c += pa[k];
+        for (int w = lane + 64 * kU; w < G.n_wave; w += 64) c += Wk.partA[w * kPartA];
+        c = wave_sum_det(c);
+        if (lane == 0) {
+            Wk.sys[n_e] = c;  // the decision of iteration 0 reads the initial cost here
+            Wk.sys[n_e + 1] = sing ? 1.0 : 0.0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // K5: camera system solve (one workgroup of 256):
 //   n <= 60 (<= 10 free keyframes): pipelined 4-wave register LDL^T of [S; b^T] (chol_pipe)
@@ -2269,14 +2320,28 @@ struct BkDims {
 // Step K's rank-6 update of the columns >= 6 (K + 2) by update wave `wid` of `nw`.  Uk: U of
 // block K (6 columns of LD doubles, zero on the rows before block K + 1); L of block K lives in
 // M's columns 6K .. 6K + 5.
+// Round 6: only the tiles the step can change.  env = the last camera block whose rows of column
+// block K may be nonzero (the symbolic envelope, BA::set_problem: a window whose landmarks each
+// span a few consecutive keyframes gives a banded S, and LDL^T keeps the band), so the update
+// covers tile columns up to that block's and tile rows up to it plus the b row's tile; the other
+// tiles of the dense count are skipped (no loads, no MFMAs).  The same tiles get the same MFMAs
+// as before, the skipped ones would have added exact zeros: the same bits.
 template <int NF, int K, int NWU>
-__device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane, int wid) {
+__device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane, int wid, int env) {
     using D = BkDims<NF>;
     constexpr int c0 = 6 * K, cmin = c0 + 12;
     if constexpr (cmin < D::NP) {
         constexpr int TJ0 = cmin / 16;
-        constexpr int ntile = (D::NTC - TJ0) * D::NT - (D::NTC - 1 + TJ0) * (D::NTC - TJ0) / 2;
-        constexpr int Q = (ntile + NWU - 1) / NWU;  // tiles per update wave
+        constexpr int ntile_dense = (D::NTC - TJ0) * D::NT - (D::NTC - 1 + TJ0) * (D::NTC - TJ0) / 2;
+        constexpr int Q = (ntile_dense + NWU - 1) / NWU;  // tiles per update wave (at most)
+        constexpr int TIb = D::NP / 16;                   // the tile row of b (row NP)
+        const int rlast = min(6 * (env + 1), D::NP) - 1;  // the band's last row
+        const int TIe = rlast / 16;
+        const int TJe = env >= K + 2 ? min(TIe, D::NTC - 1) : TJ0 - 1;  // no column in the band: nothing
+        const int extra = TIb > TIe ? 1 : 0;              // the b row's tile below the band's
+        // tiles of tile column TJ: rows TJ .. TIe, then TIb
+        int ntile = 0;
+        for (int TJ = TJ0; TJ <= TJe; ++TJ) ntile += TIe - TJ + 1 + extra;
         const int i16 = lane & 15, k4 = lane >> 4;
         // every tile's operands and accumulator loaded first, then the MFMAs, then the stores:
         // one LDS round trip per step instead of one per tile
@@ -2288,11 +2353,11 @@ __device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane,
         for (int q = 0; q < Q; ++q) {
             const int t = wid + NWU * q;
             int TJ = TJ0, rem = t < ntile ? t : 0;
-            while (rem >= D::NT - TJ) {
-                rem -= D::NT - TJ;
+            while (rem >= TIe - TJ + 1 + extra) {
+                rem -= TIe - TJ + 1 + extra;
                 ++TJ;
             }
-            const int TI = TJ + rem;
+            const int TI = rem <= TIe - TJ ? TJ + rem : TIb;
             const int col = 16 * TJ + i16;  // this lane's column of the C tile (= a row of L)
             live[q] = t < ntile && col >= cmin && col < D::NP;
             base[q] = col * D::LD + 16 * TI + k4;
@@ -2306,9 +2371,11 @@ __device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane,
             for (int r = 0; r < 4; ++r) c[q][r] = live[q] ? M[base[q] + 4 * r] : 0.0;
         }
 #pragma unroll
-        for (int q = 0; q < Q; ++q) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][0], bv[q][0], c[q], 0, 0, 0);
+        for (int q = 0; q < Q; ++q)
+            if (wid + NWU * q < ntile) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][0], bv[q][0], c[q], 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < Q; ++q) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][1], bv[q][1], c[q], 0, 0, 0);
+        for (int q = 0; q < Q; ++q)
+            if (wid + NWU * q < ntile) c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][1], bv[q][1], c[q], 0, 0, 0);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
             if (live[q])
@@ -2322,12 +2389,15 @@ __device__ __forceinline__ void bk_update(double* M, const double* Uk, int lane,
 // runs every step (one barrier each).
 template <int NF, int K, int NW>
 __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, double* Lsc,
-                                         double (&a)[BkDims<NF>::RPL][6], int tid, bool& bad) {
+                                         double (&a)[BkDims<NF>::RPL][6], int tid, bool& bad,
+                                         const unsigned char* env) {
     using D = BkDims<NF>;
     constexpr int RPL = D::RPL, LD = D::LD, c0 = 6 * K;
     const int lane = tid & 63, wave = tid >> 6;
     double u[RPL][6];
     if constexpr (K < 9) WSTAMP(0, 8 + K);  // slots 8..16: wave 0 at the step's start
+    WSTAMP(0, 32 + K);                       // slots 32..51: the same for every step (NF <= 20)
+    WSTAMP(1, 64 + K);                       // slots 64..83: wave 1 done with step K - 1's update
     if (wave == 0) {
         // the diagonal block to every lane: its 6 rows store, every lane reads the lower 21
 #pragma unroll
@@ -2392,6 +2462,7 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
     if constexpr (K >= 1 && K <= 4) WSTAMP(1, 25 + K);  // slots 26..29: wave 1 done with step K - 1
     __syncthreads();  // L and U of block K visible; the update waves finished block K - 1's update
     if constexpr (K < 8) WSTAMP(0, 17 + K);  // slots 17..24: wave 0 released by barrier K
+    WSTAMP(0, 96 + K);                          // slots 96..115: the same for every step
     if (wave == 0) {
         if constexpr (K + 1 < NF) {
             // the look-ahead: column block K + 1 (block K - 1's update applied by the update
@@ -2415,9 +2486,9 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
                     for (int m = 0; m < 6; ++m) a[h][j] = fma(-u[h][m], Ls[j][m], a[h][j]);
         }
     } else {
-        bk_update<NF, K, NW - 1>(M, U + (K & 1) * 6 * LD, lane, wave - 1);
+        bk_update<NF, K, NW - 1>(M, U + (K & 1) * 6 * LD, lane, wave - 1, env[K]);
     }
-    if constexpr (K + 1 < NF) bk_steps<NF, K + 1, NW>(M, U, Dsc, Lsc, a, tid, bad);
+    if constexpr (K + 1 < NF) bk_steps<NF, K + 1, NW>(M, U, Dsc, Lsc, a, tid, bad, env);
 }
 
 // The whole factorisation (every wave of the block); afterwards M's columns hold L (unit lower)
@@ -2425,7 +2496,8 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
 // the steps -- one step's code reused instead of ~37 KB of straight-line code -- measured
 // slower: 17.1 vs 13.9 us per K5 launch at config 3, profiles/r05d_k5_stamps.txt.)
 template <int NF, int NW>
-__device__ __forceinline__ void bk_factor(double* M, double* U, double* S, int tid, bool& bad) {
+__device__ __forceinline__ void bk_factor(double* M, double* U, double* S, int tid, bool& bad,
+                                          const unsigned char* env) {
     using D = BkDims<NF>;
     double a[D::RPL][6];
     if ((tid >> 6) == 0) {
@@ -2437,7 +2509,7 @@ __device__ __forceinline__ void bk_factor(double* M, double* U, double* S, int t
             for (int j = 0; j < 6; ++j) a[h][j] = M[j * D::LD + r];
         }
     }
-    bk_steps<NF, 0, NW>(M, U, S, S + 36, a, tid, bad);
+    bk_steps<NF, 0, NW>(M, U, S, S + 36, a, tid, bad, env);
 }
 
 template <int NF, bool LL = false>
@@ -2522,7 +2594,7 @@ __device__ void camera_solve_mfma_body(const Geometry& G, const Prob& Pr, const 
     double* const Lres = Lf;
 #else
     static_assert(BkDims<NF>::NPP == NPP && BkDims<NF>::LD == kMfLd, "one M layout for both factorisations");
-    bk_factor<NF, kK5Threads / 64>(M, Up, Lf, tid, bad);
+    bk_factor<NF, kK5Threads / 64>(M, Up, Lf, tid, bad, G.env);
     double* const Lres = M;  // L in place in M's columns
 #endif
     if (wave != 0) return;
@@ -2587,6 +2659,7 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nF = G.n_free, n = 6 * nF;
     const int ne = G.n_pb * 36 + 12 * nF;
+    STAMP(0);
     double p7b[2][7];
     int fidx = -1;
 #pragma unroll
@@ -2650,17 +2723,37 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
                 fail = sing;
             }
         }
-    } else {  // sharded: the all-reduced system (+ lambda on the owner rank) from sys, by the map
-        if (st->done) return;
+    } else {  // sharded, or pre-summed (ba_schur_combine_wide): the system from sys, by the map
+        // every entry's map and value loads in flight together (16 per thread covers W = 20:
+        // 7,068 entries / 512 threads), then the scatter -- one round trip, not one per entry
         const double* sys = Wk.sys;
-        for (int e = tid; e < ne; e += T) {
+        constexpr int kE = 16;
+        int dst[kE];
+        double val[kE];
+#pragma unroll
+        for (int i = 0; i < kE; ++i) {
+            const int e = tid + T * i;
+            dst[i] = e < ne ? Pr.dmap[e] : -1;
+            val[i] = e < ne ? sys[e] : 0.0;
+        }
+        const double sfail = sys[ne + 1];
+        if (st->done) return;
+        for (int e = tid + T * kE; e < ne; e += T) {  // (none at W <= 20)
             const int d = Pr.dmap[e];
             if (d >= 0)
                 M[d & (kMfMapLambda - 1)] = sys[e];
             else if (d <= -2)
                 gsh[-2 - d] = sys[e];
         }
-        if (tid == 0) fail = sys[ne + 1] != 0.0;
+#pragma unroll
+        for (int i = 0; i < kE; ++i) {
+            const int d = dst[i];
+            if (d >= 0)
+                M[d & (kMfMapLambda - 1)] = val[i];
+            else if (d <= -2)
+                gsh[-2 - d] = val[i];
+        }
+        if (tid == 0) fail = sfail != 0.0;
     }
     const int cur = st->cur;
     double p7[7];
@@ -2672,17 +2765,20 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
             if (r >= c && ((r >= n && r < NP) || (c >= n && c < NP))) M[c * LD + r] = r == c ? 1.0 : 0.0;
         }
     __syncthreads();
+    STAMP(1);
     if (tid == 0) *Wk.singular = 0;
     double gcl[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) gcl[q] = (wave == 0 && lane + 64 * q < n) ? gsh[lane + 64 * q] : 0.0;
     __syncthreads();
+    STAMP(2);
     if (fail) {
         if (tid == 0) k5_result(st, 0, 0.0, 0.0);
         return;
     }
     bool bad = false;
-    bk_factor<NF, kBkWaves>(M, U, S, tid, bad);
+    bk_factor<NF, kBkWaves>(M, U, S, tid, bad, G.env);
+    STAMP(3);
     if (wave != 0) return;
     if (bad) {
         if (lane == 0) k5_result(st, 0, 0.0, 0.0);
@@ -2714,6 +2810,7 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
             }
         }
     }
+    STAMP(4);
     double x[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) x[q] = lane + 64 * q < n ? yv[q] : 0.0;
@@ -2742,6 +2839,7 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
         }
     }
     if (lane == 0) k5_result(st, 1, d2, gd);
+    STAMP(5);
 }
 
 template <int NF>
@@ -3001,6 +3099,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
             }
         }
     }
+    STAMP(4);
     double x[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) x[q] = lane + 64 * q < n ? yv[q] : 0.0;
@@ -3029,6 +3128,7 @@ __global__ __launch_bounds__(64 * kX2Waves) void ba_camera_solve_x2(Geometry G, 
         }
     }
     if (lane == 0) k5_result(st, 1, d2, gd);
+    STAMP(5);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4511,11 +4611,29 @@ struct BundleAdjuster {
         auto* wave_lm = reinterpret_cast<int*>(hb + L.wave_lm);
         int n_wave = 0, fill = 0;
         int gl[kGrp] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // the camera system's symbolic envelope (the 6x6-block solver past 10 free keyframes
+        // skips the tiles outside it): a landmark couples every free keyframe between its first
+        // and last one (a superset of its pairs); cand[a] = the last keyframe of the landmarks
+        // starting at a, env[k] = the prefix maximum (the rows of L's column block k that may be
+        // nonzero: LDL^T keeps the envelope)
+        const bool want_env = n_free > 10;
+        unsigned long long freebits = 0;
+        for (int k = 0; k < n_kf; ++k)
+            if (free_idx[k] >= 0) freebits |= 1ull << (2 * k);
+        int cand[kMaxFree];
+        for (int k = 0; k < kMaxFree; ++k) cand[k] = -1;
         for (int l = 0; l < n_lm; ++l) {
             const int ns = slot_count(m2[l]);
             if (!ns) {
                 lm_base[l] = -1;
                 continue;
+            }
+            if (want_env) {
+                const unsigned long long kb = (m2[l] | (m2[l] >> 1)) & freebits;
+                if (kb) {
+                    const int a = free_idx[__builtin_ctzll(kb) >> 1], b = free_idx[(63 - __builtin_clzll(kb)) >> 1];
+                    cand[a] = std::max(cand[a], b);
+                }
             }
             if (n_wave == 0 || fill + ns > 64) {
                 if (n_wave) wave_fill[n_wave - 1] = fill;
@@ -4558,6 +4676,10 @@ struct BundleAdjuster {
                          6 * bk_template_nf(n_free), kBkLd);
         G.n_kf = n_kf; G.n_free = n_free; G.n_lm = n_lm; G.n_obs = n_obs; G.n_slot = (int)n_pad;
         G.n_pb = n_pb; G.n_wave = n_wave; G.n_chunk = n_chunk; G.pair_stride = stride;
+        for (int k = 0, run = -1; k < kMaxFree; ++k) {
+            run = std::max(run, cand[k]);
+            G.env[k] = (unsigned char)(k >= n_free ? k : want_env ? std::max(k, run) : n_free - 1);
+        }
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
         grow_buffers();  // (before the descriptor: it holds their addresses)
@@ -4633,7 +4755,14 @@ struct BundleAdjuster {
         hipLaunchKernelGGL(ba_schur_chunks, dim3(G.n_chunk), dim3(kSchurThreads), 0, stream, G, pr, wk, la,
                            sharded() ? 1 : 0);
         RSVIO_HIP(hipGetLastError());
-        if (!sharded() && !materialise) return;  // single rank: K5 sums the partials itself
+        if (!sharded() && !materialise) {  // single rank: K5 sums the partials itself
+            if (wide_combine()) {  // ... or, past 10 free keyframes, pulls one pre-summed system
+                hipLaunchKernelGGL(ba_schur_combine_wide, dim3((36 * G.n_pb + 12 * G.n_free + 255) / 256), dim3(256),
+                                   0, stream, G, pr, wk);
+                RSVIO_HIP(hipGetLastError());
+            }
+            return;
+        }
         if (coll == 2) {  // P2P: combine + exchange in one launch (X1)
             hipLaunchKernelGGL(ba_p2p_sys, dim3(1), dim3(256), 0, stream, G, pr, wk, p2p, d_xgen.p, d_p2p_err.p);
             RSVIO_HIP(hipGetLastError());
@@ -4646,7 +4775,11 @@ struct BundleAdjuster {
 
     // register-resident factorisation for n_free <= 10, two rows per lane otherwise; combine:
     // the reduced system is summed from the chunk partials in K5's prologue (single rank)
+    // single rank past 10 free keyframes (the 6x6-block solver): the partial systems summed by
+    // ba_schur_combine_wide, so K5's one workgroup pulls one system instead of eight
+    bool wide_combine() const { return !sharded() && k5_variant == 2 && G.n_free > 10; }
     void launch_camera_solve(const Prob& pr, const Work& wk, int combine) {
+        if (combine && wide_combine()) combine = 0;
         const dim3 g(1), b(kK5Threads);
         if (k5_variant == 2 && G.n_free <= 10) {
             switch (G.n_free) {

@@ -14,15 +14,24 @@
 //     is_keyframe = true and T_W_B = I (estimator.rs:228-234, frame.rs:95, state.rs:26).
 //
 // One workgroup of 512 lanes runs the whole sequence in one launch (no host round trip, no
-// grid-wide synchronisation): the map ids are staged in LDS for the join (binary search), the
-// matched observations (<= 4096 features per frame) stay in LDS, and every pass linearises all
-// of them at one pose and reduces H (21), g (6) and the cost in a fixed order (DPP wave sums, then
-// waves in order).  Lane 0 runs the LM control (6x6 Cholesky, SE3 (+), gain ratio) between
-// passes with its state in LDS.  Each pass after the first is at a trial pose: if the step is
-// accepted its H and g are the next system, so an accepted iteration costs one pass.
+// grid-wide synchronisation).  Round 6 layout:
+//   * the join: rsvio_pnp_set_map builds a bucketed hash table of the map on the host (4 entries of
+//     {id, p_W} per 128-B bucket, load <= 1/4) and uploads it once per map; a feature's id is looked
+//     up with ONE bucket load (its map point inside the entry), so a frame pays two dependent round
+//     trips (feature, bucket) instead of staging the map in LDS and an 11-step binary search
+//     (10.1k of the kernel's 53.8k cycles, profiles/r05pnp_stamps.txt);
+//   * the LM control runs on all of wave 0 at once, its state in registers (every lane the same
+//     values) instead of lane 0 against an LDS struct; T_C_W of the next pass is written by the
+//     same wave, so a pass costs two workgroup barriers instead of four.
+// Every pass linearises all matched observations at one pose and reduces H (21), g (6) and the
+// cost in a fixed order (DPP reduce-scatter per wave, then the waves in order).  Each pass after
+// the first is at a trial pose: if the step is accepted its H and g are the next system, so an
+// accepted iteration costs one pass.
 #include <cmath>
 #include <cstring>
+#include <algorithm>
 #include <stdexcept>
+#include <vector>
 
 #include "common.hpp"
 #include "rotation.hpp"
@@ -36,8 +45,22 @@ RSVIO_DBG_DECL
 constexpr int kPnpThreads = 512;
 constexpr int kPnpWaves = kPnpThreads / 64;
 constexpr int kPnpMaxFeatures = 4096; // features per frame (both cameras), observations in LDS
-constexpr int kPnpMapLds = 4096;      // map ids staged in LDS (32 KB) up to this size
 constexpr int kRed = 28;          // H upper (21), g (6), cost
+constexpr uint64_t kEmptyId = ~0ull;  // a free hash-table entry
+constexpr int kBucket = 4;            // entries per 128-B bucket
+
+// One hash-table entry: the map id and its point (sliding_window.rs:466-475 keeps map_points as
+// [f32; 3]); 32 B, 4 per 128-B line
+struct alignas(32) PnpEntry {
+    uint64_t id;
+    float pw[3];
+    uint32_t pad;
+};
+static_assert(sizeof(PnpEntry) == 32, "4 entries per 128-B bucket");
+
+__host__ __device__ __forceinline__ uint32_t map_bucket(uint64_t id, int mask) {
+    return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 40) & (uint32_t)mask;  // Fibonacci hashing
+}
 
 enum { LM_COST_TOL = 1, LM_PARAM_TOL = 2, LM_MAX_ITERS = 3, LM_TRUST_REGION = 4, LM_NUMFAIL = -1, LM_SKIPPED = -2,
        LM_LINSOLVE = -3 };
@@ -48,8 +71,11 @@ struct PnpArgs {
     const float2* uv[2];     // undistorted coordinates (frame.rs:118-119,131-132)
     const int* dcount;       // device (n_l, n_r), or null: n[] below
     int n[2];
-    const uint64_t* map_ids; // strictly ascending
-    const float* map_pw;     // [f32; 3] per map point (sliding_window.rs:466-475)
+    const PnpEntry* table;   // the map as a bucketed hash table (MapTable)
+    int bucket_mask;         // buckets - 1 (a power of two)
+    int max_probe;           // the longest bucket run an insertion took (lookups stop there)
+    int has_top;             // a map point has the id kEmptyId (not representable in the table)
+    float top_pw[3];         // ... its p_W
     int n_map;
     double T_last[16];
     double q0[4];            // from_matrix(R_B_W) of the last keyframe (host, rotation.hpp)
@@ -60,6 +86,7 @@ struct PnpArgs {
     double wclk_khz;           // device wall clock rate (kernel_ms)
 };
 
+// LM control state: wave 0's registers, every lane holding the same values
 struct Ctl {
     double x[7], xt[7], H[21], g[6];
     double R[9], Rt[9];       // R_BW of x and of xt (pose_from7), cached for SE3 (+) and the pass
@@ -120,13 +147,14 @@ __device__ __forceinline__ double wave_reduce_scatter32(double (&v)[32], int lan
 // PnPFactor::linearize restated in T_C_W = T_C_B T_B_W (computed once per pass): p_C = R p_W + t,
 // r = (x/z, y/z) - obs, dr/dt = jac_proj R_CW, dr/dw = jac_proj R_CB (-R_BW [p_W]x) = -(dr/dt) [p_W]x,
 // i.e. row i of dr/dw is -(row i of dr/dt) x p_W.  Same values as factors.rs:545-571 up to
-// rounding (~60 flops instead of ~180; tolerance parity with the oracle's reference order).
+// rounding (~60 flops instead of ~180; 1/z by the refined hardware reciprocal; tolerance parity
+// with the oracle's reference order).
 __device__ __forceinline__ void pnp_linearize_cw(const double pW[3], const double uv[2], const double* T,
                                                  double r[2], double J[2][6]) {
     const double pC0 = ((T[0] * pW[0] + T[1] * pW[1]) + T[2] * pW[2]) + T[9];
     const double pC1 = ((T[3] * pW[0] + T[4] * pW[1]) + T[5] * pW[2]) + T[10];
     const double pC2 = ((T[6] * pW[0] + T[7] * pW[1]) + T[8] * pW[2]) + T[11];
-    const double iz = 1.0 / pC2;
+    const double iz = rcp_f64(pC2);
     const double x = pC0 * iz, y = pC1 * iz;
     r[0] = x - uv[0];
     r[1] = y - uv[1];
@@ -143,11 +171,26 @@ __device__ __forceinline__ void pnp_linearize_cw(const double pW[3], const doubl
     }
 }
 
+// Huber(delta) (factors.rs, the Ceres-style rho and IRLS weight as se3.hpp's huber) with one
+// refined reciprocal square root instead of sqrt + a division: rho = 2 d s / sqrt(s) - d^2,
+// w = d / sqrt(s) (tolerance parity)
+__device__ __forceinline__ void pnp_huber(double s, double d, double* rho, double* w) {
+    const double d2 = d * d;
+    if (s <= d2) {
+        *rho = s;
+        *w = 1.0;
+    } else {
+        const double is = rsqrt_f64(s);
+        *rho = 2.0 * d * (s * is) - d2;
+        *w = d * is;
+    }
+}
+
 // (H + lambda I) dx = -g by LDL^T with hardware-reciprocal pivots (no square root, no IEEE
 // division on the serial chain).  Positive definiteness is tested on the pivots exactly like
 // the oracle's Cholesky (chol_solve) tests d > 0; the solution agrees to rounding (tolerance
-// parity).
-__device__ bool ldl6(const double* __restrict__ Hp, double lambda, const double* __restrict__ g, double* dx) {
+// parity).  All operands in registers (wave 0, every lane the same values).
+__device__ __forceinline__ bool ldl6(const double (&Hp)[21], double lambda, const double (&g)[6], double (&dx)[6]) {
     double A[6][6];
 #pragma unroll
     for (int a = 0; a < 6; ++a)
@@ -156,12 +199,13 @@ __device__ bool ldl6(const double* __restrict__ Hp, double lambda, const double*
 #pragma unroll
     for (int a = 0; a < 6; ++a) A[a][a] += lambda;
     double L[6][6], U[6][6], inv[6];
+    bool ok = true;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         double d = A[j][j];
 #pragma unroll
         for (int k = 0; k < j; ++k) d -= L[j][k] * U[j][k];
-        if (!(d > 0.0) || !isfinite(d)) return false;
+        ok &= (d > 0.0) && isfinite(d);
         inv[j] = rcp_f64(d);
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
@@ -187,16 +231,7 @@ __device__ bool ldl6(const double* __restrict__ Hp, double lambda, const double*
         for (int k = i + 1; k < 6; ++k) s -= L[k][i] * dx[k];
         dx[i] = s;
     }
-    return true;
-}
-
-// The pass pose: R_BW (9) and t_BW (3) into LDS; threads 0..23 expand it to T_C_W per camera
-__device__ __forceinline__ void write_pose(double* s_pose, const double* R, const double* x7) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) s_pose[k] = R[k];
-    s_pose[9] = x7[0];
-    s_pose[10] = x7[1];
-    s_pose[11] = x7[2];
+    return ok;
 }
 
 __device__ __forceinline__ void rot_from_unit_quat(const double* q, double* R) {
@@ -210,19 +245,23 @@ __device__ __forceinline__ void rot_from_unit_quat(const double* q, double* R) {
 }
 
 // se3_plus with the rotation of x7 given (cached) and the rotation of the result returned
-// (from its normalised quaternion): same operations as se3.hpp se3_plus otherwise.
-__device__ __forceinline__ void se3_plus_r(const double* p7, const double* R, const double* d, double* out,
-                                           double* Rout) {
+// (from its normalised quaternion).  The four functions of theta by se3.hpp's power series in
+// theta^2 for |theta| < 1/4 (an LM step's rotation: no square root, sincos or division on the
+// chain), one sincos of theta / 2 otherwise -- the BA's se3_plus; tolerance parity.
+__device__ __forceinline__ void se3_plus_r(const double (&p7)[7], const double (&R)[9], const double (&d)[6],
+                                           double (&out)[7], double (&Rout)[9]) {
     const double* rho = d;
     const double* om = d + 3;
     const double th2 = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
-    const double th = sqrt(th2);
     double qd[4], Ac, Bc;
-    if (th < 1e-8) {
-        qd[0] = 1.0; qd[1] = 0.5 * om[0]; qd[2] = 0.5 * om[1]; qd[3] = 0.5 * om[2];
-        Ac = 0.5 - th2 / 24.0;
-        Bc = 1.0 / 6.0 - th2 / 120.0;
+    if (th2 < 0.0625) {
+        const double s = se3_series<1>(th2);  // sin(theta/2) / theta
+        qd[0] = se3_series<0>(th2);           // cos(theta/2)
+        qd[1] = s * om[0]; qd[2] = s * om[1]; qd[3] = s * om[2];
+        Ac = se3_series<2>(th2);
+        Bc = se3_series<3>(th2);
     } else {
+        const double th = sqrt(th2);
         double sh, ch;
         sincos(0.5 * th, &sh, &ch);
         const double ith = rcp_f64(th);
@@ -250,88 +289,106 @@ __device__ __forceinline__ void se3_plus_r(const double* p7, const double* R, co
     rot_from_unit_quat(out + 3, Rout);
 }
 
-// Lane 0 between passes: consume the pass in s_sum, then either set up the next pass (run = 1)
-// or finish (run = 0).  Mirrors oracle orc_track_motion's loop step for step.
-__device__ void pnp_control(const PnpArgs& A, Ctl* __restrict__ C, const double* __restrict__ s_sum,
-                            double* __restrict__ s_pose) {
+// Lane 0 of wave 0 between passes (the state in LDS: its registers are the pass's): consume the
+// pass sums, then either set up the next pass at a trial pose (C.run = 1, its R_BW and t_BW in
+// pose[12]) or finish (run = 0).  Mirrors oracle orc_track_motion's loop step for step.
+__device__ __forceinline__ void pnp_control(const PnpArgs& A, Ctl& C, const double* __restrict__ sum,
+                                         double* __restrict__ pose) {
     bool done = false;
-    if (C->phase == 0) {
+    if (C.phase == 0) {
 #pragma unroll
-        for (int k = 0; k < 21; ++k) C->H[k] = s_sum[k];
+        for (int k = 0; k < 21; ++k) C.H[k] = sum[k];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) C->g[k] = s_sum[21 + k];
-        C->cost = s_sum[27];
-        C->initial_cost = C->cost;
-        C->phase = 1;
+        for (int k = 0; k < 6; ++k) C.g[k] = sum[21 + k];
+        C.cost = sum[27];
+        C.initial_cost = C.cost;
+        C.phase = 1;
     } else {
-        const double new_cost = s_sum[27];
-        const double dcost = C->cost - new_cost;
-        const double rho = dcost / C->pred;
-        if (isfinite(new_cost) && fabs(dcost) <= A.cost_tol * C->cost) {
+        const double new_cost = sum[27];
+        const double dcost = C.cost - new_cost;
+        const double rho = dcost / C.pred;
+        if (isfinite(new_cost) && fabs(dcost) <= A.cost_tol * C.cost) {
             // converged: the change is within the tolerance whatever its sign, the candidate not
             // applied (the BA's lm_update takes the same decision).  This
             // build's rule, a deliberate departure: apex-solver's is absent offline (unpinned)
-            C->status = LM_COST_TOL;
+            C.status = LM_COST_TOL;
             done = true;
         } else if (isfinite(new_cost) && rho > 0.0) {
 #pragma unroll
-            for (int k = 0; k < 7; ++k) C->x[k] = C->xt[k];
+            for (int k = 0; k < 7; ++k) C.x[k] = C.xt[k];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) C->R[k] = C->Rt[k];
+            for (int k = 0; k < 9; ++k) C.R[k] = C.Rt[k];
 #pragma unroll
-            for (int k = 0; k < 21; ++k) C->H[k] = s_sum[k];
+            for (int k = 0; k < 21; ++k) C.H[k] = sum[k];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) C->g[k] = s_sum[21 + k];
+            for (int k = 0; k < 6; ++k) C.g[k] = sum[21 + k];
             const double f = 2.0 * rho - 1.0;
-            C->lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
-            C->nu = 2.0;
-            C->cost = new_cost;
+            C.lambda *= fmax(1.0 / 3.0, 1.0 - f * f * f);
+            C.nu = 2.0;
+            C.cost = new_cost;
         } else {
-            C->lambda *= C->nu;
-            C->nu *= 2.0;
-            if (C->lambda > 1e32) {
-                C->status = LM_TRUST_REGION;
+            C.lambda *= C.nu;
+            C.nu *= 2.0;
+            if (C.lambda > 1e32) {
+                C.status = LM_TRUST_REGION;
                 done = true;
             }
         }
     }
-    while (!done) {
-        if (C->it >= A.max_iter) {
-            C->status = LM_MAX_ITERS;
-            break;
-        }
-        C->it += 1;
-        if (!isfinite(C->cost)) {
-            C->status = LM_NUMFAIL;
-            break;
-        }
-        double dx[6];
-        const bool solved = ldl6(C->H, C->lambda, C->g, dx);
-        STAMP(30);
-        if (!solved) {  // Err(LinearSolveFailed) -> track_motion returns Ok(None) (:554-560)
-            C->status = LM_LINSOLVE;
-            break;
-        }
-        double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
-        for (int k = 0; k < 6; ++k) {
-            dx2 += dx[k] * dx[k];
-            gdx += C->g[k] * dx[k];
-        }
-        for (int k = 0; k < 7; ++k) x2 += C->x[k] * C->x[k];
-        if (sqrt(dx2) <= A.param_tol * (sqrt(x2) + A.param_tol)) {
-            C->status = LM_PARAM_TOL;
-            break;
-        }
-        se3_plus_r(C->x, C->R, dx, C->xt, C->Rt);
-        STAMP(31);
-        C->pred = 0.5 * (C->lambda * dx2 - gdx);
-        write_pose(s_pose, C->Rt, C->xt);
-        C->run = 1;
+    C.run = 0;
+    if (done) return;
+    if (C.it >= A.max_iter) {
+        C.status = LM_MAX_ITERS;
         return;
     }
-    C->run = 0;
+    C.it += 1;
+    if (!isfinite(C.cost)) {
+        C.status = LM_NUMFAIL;
+        return;
+    }
+    double dx[6], H[21], g[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) H[k] = C.H[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g[k] = C.g[k];
+    const bool solved = ldl6(H, C.lambda, g, dx);
+    STAMP(30);
+    if (!solved) {  // Err(LinearSolveFailed) -> track_motion returns Ok(None) (:554-560)
+        C.status = LM_LINSOLVE;
+        return;
+    }
+    double dx2 = 0.0, gdx = 0.0, x2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        dx2 += dx[k] * dx[k];
+        gdx += g[k] * dx[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) x2 += C.x[k] * C.x[k];
+    if (sqrt(dx2) <= A.param_tol * (sqrt(x2) + A.param_tol)) {
+        C.status = LM_PARAM_TOL;
+        return;
+    }
+    double x[7], R[9], xt[7], Rt[9];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) x[k] = C.x[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = C.R[k];
+    se3_plus_r(x, R, dx, xt, Rt);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) C.xt[k] = xt[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) C.Rt[k] = Rt[k];
+    STAMP(31);
+    C.pred = 0.5 * (C.lambda * dx2 - gdx);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) pose[k] = Rt[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pose[9 + k] = xt[k];
+    C.run = 1;
 }
 
+// lane 0 of wave 0
 __device__ void pnp_finish(const PnpArgs& A, const Ctl& C, unsigned long long t_entry) {
     rsvio_motion_result r;
     r.status = C.status;
@@ -363,50 +420,105 @@ __device__ void pnp_finish(const PnpArgs& A, const Ctl& C, unsigned long long t_
     *A.out = r;
 }
 
+// The map point of `id` (map_points.get, sliding_window.rs:526-545): the bucket of its hash, then
+// the following ones up to the longest run an insertion took; a bucket with a free entry ends a
+// miss.  One 128-B load per bucket visited (almost always one).
+__device__ __forceinline__ bool map_lookup(const PnpArgs& A, uint64_t id, float (&pw)[3]) {
+    if (id == kEmptyId) {
+        pw[0] = A.top_pw[0]; pw[1] = A.top_pw[1]; pw[2] = A.top_pw[2];
+        return A.has_top != 0;
+    }
+    uint32_t b = map_bucket(id, A.bucket_mask);
+    for (int p = 0; p <= A.max_probe; ++p) {
+        // the bucket's 4 entries as 8 16-B loads, all in flight; the match picked by selects (no
+        // runtime-indexed local array: that would go through scratch)
+        const uint4* e = reinterpret_cast<const uint4*>(A.table + (size_t)b * kBucket);
+        uint4 v[2 * kBucket];
+#pragma unroll
+        for (int k = 0; k < 2 * kBucket; ++k) v[k] = e[k];
+        bool hit = false, free_slot = false;
+        uint32_t x = 0, y = 0, z = 0;
+#pragma unroll
+        for (int k = 0; k < kBucket; ++k) {
+            const uint64_t key = (uint64_t)v[2 * k].x | ((uint64_t)v[2 * k].y << 32);
+            const bool m = key == id;
+            x = m ? v[2 * k].z : x;
+            y = m ? v[2 * k].w : y;
+            z = m ? v[2 * k + 1].x : z;
+            hit |= m;
+            free_slot |= key == kEmptyId;
+        }
+        if (hit) {
+            pw[0] = __uint_as_float(x); pw[1] = __uint_as_float(y); pw[2] = __uint_as_float(z);
+            return true;
+        }
+        if (free_slot) return false;
+        b = (b + 1) & (uint32_t)A.bucket_mask;
+    }
+    return false;
+}
+
 __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A) {
-    __shared__ uint64_t s_ids[kPnpMapLds];       // map ids (small maps)
-    __shared__ float s_mpw[3][kPnpMapLds];       // small maps: map p_W by map index; large: by feature
+    __shared__ float s_mpw[3][kPnpMaxFeatures];  // the matched map point per feature
     __shared__ float s_uv[2][kPnpMaxFeatures];   // undistorted coordinates per feature
-    __shared__ int16_t s_idx[kPnpMaxFeatures];   // feature -> s_mpw column
     __shared__ int8_t s_cam[kPnpMaxFeatures];    // feature -> camera, -1: no map point
     __shared__ double s_red[kPnpWaves][kRed];
     __shared__ double s_sum[kRed];
-    __shared__ double s_pose[12];                // R_BW, t_BW of the pass pose
+    __shared__ double s_pose[12];                // R_BW, t_BW of the pass pose (wave 0's)
     __shared__ double s_tcb[2][16];
     __shared__ double s_tcw[2][12];              // T_C_W = T_C_B T_B_W per camera at the pass pose
-    __shared__ Ctl C;
     __shared__ int s_nobs;
+    __shared__ int s_run;
+    __shared__ Ctl s_ctl;                        // the LM state between controls (wave 0's)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     STAMP(0);
     const unsigned long long t_entry = wall_clock64();  // (kept by thread 0 for kernel_ms)
     const int n0 = A.dcount ? A.dcount[0] : A.n[0];
     const int n1 = A.dcount ? A.dcount[1] : A.n[1];
     const int nf = n0 + n1;
-    const bool lds_map = A.n_map <= kPnpMapLds;
-    // this lane's first two features: their loads are issued before the map staging so the two
-    // memory latencies overlap
-    auto feat = [&](int j, int& c, int& i, uint64_t& id, float2& q) {
-        c = j < n0 ? 0 : 1;
-        i = c == 0 ? j : j - n0;
-        id = *reinterpret_cast<const uint64_t*>(A.ids[c] + (size_t)i * A.id_stride);
-        q = A.uv[c][i];
-    };
     const bool fits = nf <= kPnpMaxFeatures;
-    int pc0 = 0, pi0 = 0, pc1 = 0, pi1 = 0;
-    uint64_t pid0 = 0, pid1 = 0;
-    float2 pq0 = make_float2(0.0f, 0.0f), pq1 = pq0;
-    if (fits && tid < nf) feat(tid, pc0, pi0, pid0, pq0);
-    if (fits && tid + kPnpThreads < nf) feat(tid + kPnpThreads, pc1, pi1, pid1, pq1);
+    // the factor list: features with a map point, left then right (sliding_window.rs:519-547);
+    // feature j's observation goes to LDS entry j (cam -1: no map point).  Two features per lane
+    // per round: both id / uv loads, then both bucket loads in flight together.
+    int mine = 0;
+    if (tid == 0) s_nobs = 0;
     if (tid < 32) s_tcb[tid >> 4][tid & 15] = A.TCB[tid >> 4][tid & 15];
-    if (lds_map)
-        for (int i = tid; i < A.n_map; i += kPnpThreads) {
-            s_ids[i] = A.map_ids[i];
-            s_mpw[0][i] = A.map_pw[3 * i];
-            s_mpw[1][i] = A.map_pw[3 * i + 1];
-            s_mpw[2][i] = A.map_pw[3 * i + 2];
+    for (int j0 = tid; j0 < nf && fits; j0 += 2 * kPnpThreads) {
+        uint64_t id[2];
+        float2 q[2];
+        int cam[2];
+        bool v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = j0 + h * kPnpThreads;
+            v[h] = j < nf;
+            const int jj = v[h] ? j : j0;
+            cam[h] = jj < n0 ? 0 : 1;
+            const int i = cam[h] == 0 ? jj : jj - n0;
+            id[h] = *reinterpret_cast<const uint64_t*>(A.ids[cam[h]] + (size_t)i * A.id_stride);
+            q[h] = A.uv[cam[h]][i];
         }
-    if (tid == 0) {
-        s_nobs = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!v[h]) continue;
+            const int j = j0 + h * kPnpThreads;
+            float pw[3];
+            const bool hit = A.n_map > 0 && map_lookup(A, id[h], pw);
+            s_cam[j] = hit ? (int8_t)cam[h] : (int8_t)-1;
+            if (hit) {
+                s_uv[0][j] = q[h].x;
+                s_uv[1][j] = q[h].y;
+                s_mpw[0][j] = pw[0];
+                s_mpw[1][j] = pw[1];
+                s_mpw[2][j] = pw[2];
+                ++mine;
+            }
+        }
+    }
+    // wave 0: the LM state (LDS between controls, registers during one); F starts from the last
+    // keyframe (sliding_window.rs:506-517)
+    if (wv == 0) {
+        Ctl C;
         C.it = 0;
         C.status = LM_MAX_ITERS;
         C.phase = 0;
@@ -414,7 +526,7 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
         C.nu = 2.0;
         C.cost = 0.0;
         C.initial_cost = 0.0;
-        // sliding_window.rs:506-517: F = (t_B_W, from_matrix(R_B_W)) of the last keyframe
+        C.pred = 0.0;
         double TBW[16];
         rigid_inverse(A.T_last, TBW);
         C.x[0] = TBW[3];
@@ -425,94 +537,21 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
         const Pose P0 = pose_from7(C.x);  // SE3::from (apex) of the initial 7-vector
 #pragma unroll
         for (int k = 0; k < 9; ++k) C.R[k] = P0.R[k / 3][k % 3];
-        write_pose(s_pose, C.R, C.x);
-    }
-    __syncthreads();
-    STAMP(1);
-
-    // the factor list: features with a map point, left then right (sliding_window.rs:519-547);
-    // feature j's observation goes to LDS entry j (cam -1: no map point)
-    // two features per lane per round: ids and uv loads issued together, then both
-    // branchless lower_bound searches (fixed trip count) interleaved, then the p_W loads
-    int mine = 0;
-    const int nm = A.n_map;
-    auto map_at = [&](int k) -> uint64_t { return lds_map ? s_ids[k] : A.map_ids[k]; };
-    for (int j0 = tid; j0 < nf && fits; j0 += 2 * kPnpThreads) {
-        const int j1 = j0 + kPnpThreads;
-        const bool v1 = j1 < nf;
-        int c0 = pc0, i0 = pi0, c1 = pc1, i1 = pi1;
-        uint64_t id0 = pid0, id1 = pid1;
-        float2 q0 = pq0, q1 = pq1;
-        if (j0 != tid) {  // rounds after the first (more than 1024 features)
-            feat(j0, c0, i0, id0, q0);
-            if (v1) feat(j1, c1, i1, id1, q1);
-        }
-        int b0 = 0, b1 = 0;
-        for (int len = nm; len > 1;) {
-            const int half = len >> 1;
-            const uint64_t m0 = map_at(b0 + half), m1 = map_at(b1 + half);
-            b0 = m0 < id0 ? b0 + half : b0;
-            b1 = m1 < id1 ? b1 + half : b1;
-            len -= half;
-        }
-        bool hit0 = false, hit1 = false;
-        if (nm > 0) {
-            const uint64_t m0 = map_at(b0), m1 = map_at(b1);
-            b0 += m0 < id0 ? 1 : 0;
-            b1 += m1 < id1 ? 1 : 0;
-            hit0 = b0 < nm && map_at(b0) == id0;
-            hit1 = v1 && b1 < nm && map_at(b1) == id1;
-        }
-        s_cam[j0] = hit0 ? (int8_t)c0 : (int8_t)-1;
-        if (v1) s_cam[j1] = hit1 ? (int8_t)c1 : (int8_t)-1;
-        if (hit0) {
-            s_uv[0][j0] = q0.x;
-            s_uv[1][j0] = q0.y;
-            s_idx[j0] = (int16_t)(lds_map ? b0 : j0);
-            if (!lds_map) {
-                s_mpw[0][j0] = A.map_pw[3 * b0];
-                s_mpw[1][j0] = A.map_pw[3 * b0 + 1];
-                s_mpw[2][j0] = A.map_pw[3 * b0 + 2];
-            }
-            ++mine;
-        }
-        if (hit1) {
-            s_uv[0][j1] = q1.x;
-            s_uv[1][j1] = q1.y;
-            s_idx[j1] = (int16_t)(lds_map ? b1 : j1);
-            if (!lds_map) {
-                s_mpw[0][j1] = A.map_pw[3 * b1];
-                s_mpw[1][j1] = A.map_pw[3 * b1 + 1];
-                s_mpw[2][j1] = A.map_pw[3 * b1 + 2];
-            }
-            ++mine;
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) s_pose[k] = C.R[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s_pose[9 + k] = C.x[k];
+            s_ctl = C;
         }
     }
     // per-wave total (one LDS atomic per wave instead of one per lane)
     for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off);
+    __syncthreads();  // s_nobs = 0, s_tcb and s_pose (wave 0) before their uses
     if (lane == 0 && mine) atomicAdd(&s_nobs, mine);
-    __syncthreads();
-    STAMP(2);
-    int pass = 0;
-    if (tid == 0) {
-        C.n_obs = s_nobs;
-        C.run = 1;
-        if (nf > kPnpMaxFeatures) {
-            C.n_obs = -1;
-            C.status = LM_SKIPPED;
-            C.run = 0;
-        } else if (s_nobs == 0) {
-            C.status = LM_SKIPPED;  // no factor: treated as a failed optimisation
-            C.run = 0;
-        }
-    }
-
-    while (true) {
-        __syncthreads();
-        if (!C.run) break;
-        if (pass < 12) STAMP(3 + 2 * pass);
-        if (tid < 24) {  // T_C_W = T_C_B T_B_W, one entry per thread
-            const int c = tid / 12, e = tid % 12;
+    if (wv == 0) {
+        if (lane < 24) {  // T_C_W = T_C_B T_B_W, one entry per lane
+            const int c = lane / 12, e = lane % 12;
             const double* T = s_tcb[c];
             if (e < 9) {
                 const int i = e / 3, j = e % 3;
@@ -523,7 +562,19 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
                               T[4 * i + 3];
             }
         }
-        __syncthreads();
+    }
+    STAMP(1);
+    __syncthreads();  // the factor list, s_nobs and the first T_C_W
+    STAMP(2);
+    const int nobs = s_nobs;
+    int run = (fits && nobs > 0) ? 1 : 0;
+    if (tid == 0) {
+        s_ctl.n_obs = fits ? nobs : -1;
+        if (!run) s_ctl.status = LM_SKIPPED;  // no factor: treated as a failed optimisation
+    }
+    int pass = 0;
+    while (run) {
+        if (pass < 12) STAMP(3 + 2 * pass);
         // one pass at the pose in s_tcw: H, g, cost over this lane's observations (j order)
         double acc[32];
 #pragma unroll
@@ -532,14 +583,13 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
         for (int j = tid; j < nf; j += kPnpThreads) {
             const int cam = s_cam[j];
             if (cam < 0) continue;
-            const int m = s_idx[j];
-            const double pW[3] = {(double)s_mpw[0][m], (double)s_mpw[1][m], (double)s_mpw[2][m]};
+            const double pW[3] = {(double)s_mpw[0][j], (double)s_mpw[1][j], (double)s_mpw[2][j]};
             const double uv[2] = {(double)s_uv[0][j], (double)s_uv[1][j]};
             double r[2], J[2][6];
             pnp_linearize_cw(pW, uv, s_tcw[cam], r, J);
             const double s2 = r[0] * r[0] + r[1] * r[1];
             double rho, w;
-            huber(s2, A.huber_delta, &rho, &w);
+            pnp_huber(s2, A.huber_delta, &rho, &w);
             acc[27] += 0.5 * rho;
             const double wr0 = w * r[0], wr1 = w * r[1];
 #pragma unroll
@@ -554,19 +604,43 @@ __global__ __launch_bounds__(kPnpThreads) void pnp_track_motion_kernel(PnpArgs A
             const double v = wave_reduce_scatter32(acc, lane);
             if ((lane & 1) == 0 && (lane >> 1) < kRed) s_red[wv][lane >> 1] = v;
         }
-        __syncthreads();
-        if (tid < kRed) {
-            double v = s_red[0][tid];
-            for (int w = 1; w < kPnpWaves; ++w) v += s_red[w][tid];
-            s_sum[tid] = v;
-        }
-        __syncthreads();
+        __syncthreads();  // every wave's partials
         if (pass < 12) STAMP(4 + 2 * pass);
         ++pass;
-        if (tid == 0) pnp_control(A, &C, s_sum, s_pose);
+        if (wv == 0) {
+            // the waves in order (lane k sums value k), then lane 0's control
+            if (lane < kRed) {
+                double v = s_red[0][lane];
+#pragma unroll
+                for (int w = 1; w < kPnpWaves; ++w) v += s_red[w][lane];
+                s_sum[lane] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                pnp_control(A, s_ctl, s_sum, s_pose);
+                s_run = s_ctl.run;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (s_run && lane < 24) {
+                const int c = lane / 12, e = lane % 12;
+                const double* T = s_tcb[c];
+                if (e < 9) {
+                    const int i = e / 3, j = e % 3;
+                    s_tcw[c][e] = (T[4 * i] * s_pose[j] + T[4 * i + 1] * s_pose[3 + j]) + T[4 * i + 2] * s_pose[6 + j];
+                } else {
+                    const int i = e - 9;
+                    s_tcw[c][e] = ((T[4 * i] * s_pose[9] + T[4 * i + 1] * s_pose[10]) + T[4 * i + 2] * s_pose[11]) +
+                                  T[4 * i + 3];
+                }
+            }
+        }
+        __syncthreads();  // s_run and the next pass's T_C_W
+        run = s_run;
     }
     STAMP(28);
-    if (tid == 0) pnp_finish(A, C, t_entry);
+    if (tid == 0) pnp_finish(A, s_ctl, t_entry);
     STAMP(29);
 }
 
@@ -579,8 +653,12 @@ struct Pnp {
     hipStream_t stream = nullptr;      // the handle's own
     hipStream_t user = nullptr;        // rsvio_pnp_set_stream
     hipStream_t active() const { return user ? user : stream; }
-    DevBuf<uint64_t> map_ids;
-    DevBuf<float> map_pw;
+    // the map as a bucketed hash table (set_map): kBucket entries per bucket, a power of two of
+    // buckets with at most one entry per kBucket slots used (load <= 1/4)
+    DevBuf<PnpEntry> table;
+    std::vector<PnpEntry> htable;
+    int bucket_mask = 0, max_probe = 0, has_top = 0;
+    float top_pw[3] = {0.f, 0.f, 0.f};
     int n_map = 0;
     DevBuf<uint8_t> feat;            // [ids_l | ids_r | uv_l | uv_r]
     HostBuf<uint8_t> hfeat;
@@ -607,8 +685,11 @@ struct Pnp {
 PnpArgs make_args(Pnp& p, const double* T_last, const double* TCB2, const rsvio_lm_cfg* cfg,
                   const rsvio_keyframe_rule* rule) {
     PnpArgs A{};
-    A.map_ids = p.map_ids.p;
-    A.map_pw = p.map_pw.p;
+    A.table = p.table.p;
+    A.bucket_mask = p.bucket_mask;
+    A.max_probe = p.max_probe;
+    A.has_top = p.has_top;
+    for (int k = 0; k < 3; ++k) A.top_pw[k] = p.top_pw[k];
     A.n_map = p.n_map;
     std::memcpy(A.T_last, T_last, sizeof(A.T_last));
     std::memcpy(A.TCB, TCB2, sizeof(A.TCB));
@@ -721,14 +802,37 @@ int rsvio_pnp_set_map(rsvio_pnp* h, const uint64_t* ids, const float* p_W, int32
     return guarded([&] {
         auto& P = h->p;
         RSVIO_HIP(hipSetDevice(P.device));
-        if (P.map_ids.n < (size_t)n) {
-            P.map_ids.alloc((size_t)n);
-            P.map_pw.alloc((size_t)3 * n);
+        // the hash table: >= 4 n entries (load <= 1/4: a bucket overflows into the next one for
+        // well under 1 % of the ids), linear probing over buckets
+        int nb = 16;
+        while ((size_t)nb * rsvio::kBucket < (size_t)4 * n) nb *= 2;
+        P.htable.assign((size_t)nb * rsvio::kBucket, rsvio::PnpEntry{rsvio::kEmptyId, {0.f, 0.f, 0.f}, 0u});
+        P.bucket_mask = nb - 1;
+        P.max_probe = 0;
+        P.has_top = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            if (ids[i] == rsvio::kEmptyId) {  // the one id the table cannot hold (the largest: last)
+                P.has_top = 1;
+                for (int k = 0; k < 3; ++k) P.top_pw[k] = p_W[3 * i + k];
+                continue;
+            }
+            uint32_t b = rsvio::map_bucket(ids[i], P.bucket_mask);
+            for (int probe = 0;; ++probe) {
+                rsvio::PnpEntry* e = &P.htable[(size_t)b * rsvio::kBucket];
+                int k = 0;
+                while (k < rsvio::kBucket && e[k].id != rsvio::kEmptyId) ++k;
+                if (k < rsvio::kBucket) {
+                    e[k].id = ids[i];
+                    for (int c = 0; c < 3; ++c) e[k].pw[c] = p_W[3 * i + c];
+                    P.max_probe = std::max(P.max_probe, probe);
+                    break;
+                }
+                b = (b + 1) & (uint32_t)P.bucket_mask;
+            }
         }
-        if (n) {
-            RSVIO_HIP(hipMemcpyAsync(P.map_ids.p, ids, sizeof(uint64_t) * n, hipMemcpyHostToDevice, P.active()));
-            RSVIO_HIP(hipMemcpyAsync(P.map_pw.p, p_W, sizeof(float) * 3 * n, hipMemcpyHostToDevice, P.active()));
-        }
+        if (P.table.n < P.htable.size()) P.table.alloc(P.htable.size());
+        RSVIO_HIP(hipMemcpyAsync(P.table.p, P.htable.data(), sizeof(rsvio::PnpEntry) * P.htable.size(),
+                                 hipMemcpyHostToDevice, P.active()));
         RSVIO_HIP(hipStreamSynchronize(P.active()));
         P.n_map = n;
         return (int)RSVIO_OK;
