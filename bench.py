@@ -610,6 +610,18 @@ def _minor_faults() -> int:
     return int(t.rsplit(")", 1)[1].split()[7]) if t else -1
 
 
+def tame_malloc():
+    """glibc malloc without trimming and with a fixed 32 MB mmap threshold (mallopt): freed heap
+    memory stays mapped, so a later allocation of it does not page-fault again.  Diagnostic A/B
+    for the one-rep stall (a ~16 MB burst of the main thread's minor faults inside one
+    set_problem, profiles/r06e_*)."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    m_trim_threshold, m_mmap_threshold = -1, -3
+    ok = libc.mallopt(m_mmap_threshold, 32 << 20) == 1 and libc.mallopt(m_trim_threshold, 1 << 30) == 1
+    log(f"[bench] malloc: no trimming, mmap threshold 32 MB ({'ok' if ok else 'mallopt refused'})")
+
+
 def setup_dist(same_device: bool = False):
     """One process per GPU over RCCL.  `same_device` is a rehearsal mode for a one-GPU box: every
     rank on cuda:0 with a gloo control group (RCCL refuses two ranks on one device)."""
@@ -1189,6 +1201,8 @@ def main():
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
+    ap.add_argument("--tame-malloc", type=int, default=0,
+                    help="1: glibc malloc without trimming (mallopt), the stall A/B")
     ap.add_argument("--pin-windows", type=int, default=1,
                     help="1: the keyframe windows' host arrays in page-locked memory (0: pageable numpy arrays, "
                          "where an occasional NUMA-balancing scan stalls one set_problem for ~6.7 ms)")
@@ -1209,6 +1223,8 @@ def main():
         # RSVIO_P2P_FOLD=2 and 4: attach_p2p sees the shared device and lowers them to 1 and 3,
         # DESIGN.md section 8)
 
+    if args.tame_malloc:
+        tame_malloc()
     world, rank, local = setup_dist(args.same_device)
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")

@@ -185,6 +185,7 @@ struct Geometry {
     // column block k may be nonzero in L (>= k; a window of landmarks over consecutive keyframes
     // gives a band), set_problem from the landmarks' keyframe masks
     unsigned char env[kMaxFree];
+    int env_on;  // env is the landmarks' (past 10 free keyframes); else env[k] = n_free - 1, unused
 };
 
 // Structure-of-arrays problem description (device pointers)
@@ -1195,6 +1196,21 @@ __device__ void schur_chunks_body(const Geometry& G, const Prob& Pr, const Work&
     const int pb = c / kGrp, x = c % kGrp;
     RTSTAMP(0);
     STAMP(26);
+    if (G.env_on) {
+        // a camera block outside the system's envelope (no landmark sees both keyframes: a window
+        // of landmarks over consecutive keyframes, config 5) has no pair: its partial is zero and
+        // needs no decision -- a third of config 5's 1,520 chunks.  (fa, fb) from pb by the host's
+        // enumeration (pb_fa / pb_fb: a-major, b >= a), without a load
+        int a = 0, r = pb;
+        while (a < G.n_free && r >= G.n_free - a) {
+            r -= G.n_free - a;
+            ++a;
+        }
+        if (a < G.n_free && a + r > (int)G.env[a]) {
+            if (tid < 36) Wk.cpart[(size_t)x * sys_len(G) + pb * 36 + tid] = 0.0;
+            return;
+        }
+    }
     // this chunk's pairs sit at a fixed stride: the first pair of every thread is one load,
     // issued together with the decision's loads
     const int4* pr = Pr.pairs + (size_t)c * G.pair_stride;
@@ -2186,8 +2202,15 @@ __device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMf
     if constexpr (J + 2 < PW) a[J + 2] = fma(-l, rl64(u, K + 2), a[J + 2]);
     Lf[K * kMfLd + lane] = l;  // column K of L (rows > K; row NP: z_K); the upper part is never read
     Up[J * kMfLd + lane] = u;  // column J of the panel's U = D L
+#ifdef RSVIO_K5_RLQ
+    // A/B (round 6): the later columns' multipliers by readlane -- no LDS read and no wait on it
+    // between this pivot's chain and the next
+#pragma unroll
+    for (int jj = J + 3; jj < PW; ++jj) uq[jj] = rl64(u, kMfPanel * H + jj);
+#else
 #pragma unroll
     for (int jj = J + 3; jj < PW; ++jj) uq[jj] = Up[J * kMfLd + kMfPanel * H + jj];  // broadcasts
+#endif
     if constexpr (J + 1 < PW) mf_pivot<H, J + 1, PW>(a, uq, l, inv_next, Lf, Up, lane, bad);
 }
 
@@ -2759,11 +2782,20 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
     double p7[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) p7[i] = cur ? p7b[1][i] : p7b[0][i];
-    if (n < NP)  // identity padding: rows / columns [n, NP), the b row zero there
-        for (int e = tid; e < NP * (NP + 1); e += T) {
-            const int c = e / (NP + 1), r = e - c * (NP + 1);
-            if (r >= c && ((r >= n && r < NP) || (c >= n && c < NP))) M[c * LD + r] = r == c ? 1.0 : 0.0;
+    if (n < NP) {  // identity padding: rows / columns [n, NP), the b row zero there
+        // only the padded entries (round 6: the loop over every NP x (NP + 1) entry with a
+        // division each was ~4k cycles at config 5): the padded columns' lower part (b row
+        // included), then the real columns' padded rows
+        const int np = NP - n;
+        for (int e = tid; e < np * (np + 1); e += T) {
+            const int c = n + e / (np + 1), r = n + e % (np + 1);
+            if (r >= c) M[c * LD + r] = r == c ? 1.0 : 0.0;
         }
+        for (int e = tid; e < n * np; e += T) {
+            const int c = e / np, r = n + e % np;
+            M[c * LD + r] = 0.0;
+        }
+    }
     __syncthreads();
     STAMP(1);
     if (tid == 0) *Wk.singular = 0;
@@ -2786,27 +2818,42 @@ __device__ __forceinline__ void camera_solve_blk_body(const Geometry& G, const P
     }
     // L^T x = z (unit diagonal), z = row NP: lane holds the unknowns i = lane, lane + 64, L[j][i] =
     // M[i LD + j] (zero for j <= i by the select); the padded unknowns have z = 0: start at n - 1
+    // Unrolled over the template's NP unknowns (round 6): every readlane's lane and half are
+    // compile-time constants (no runtime select of the half, no loop), the next 8 columns' L
+    // entries are loaded while the current 8 steps run, and the padded unknowns (j >= n: z = 0,
+    // no coupling) are skipped by a uniform test.  The same fmas in the same order as the
+    // runtime loop it replaces (22k cycles at config 5, profiles/r06e_c5_k5_stamps.txt).
     double yv[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) yv[q] = M[min(lane + 64 * q, NP - 1) * LD + NP];
-    constexpr int kBs = 8;
-    for (int j0 = n - 1; j0 >= 0; j0 -= kBs) {
-        double lt[kBs][2];
+    {
+        constexpr int kBs = 8, NB = (NP + kBs - 1) / kBs;
+        double lt[2][kBs][2];
 #pragma unroll
-        for (int t = 0; t < kBs; ++t) {
-            const int j = max(j0 - t, 0);
+        for (int t = 0; t < kBs; ++t)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) lt[t][q] = M[min(lane + 64 * q, NP - 1) * LD + j];
-        }
+            for (int q = 0; q < 2; ++q) lt[0][t][q] = M[min(lane + 64 * q, NP - 1) * LD + (NP - 1 - t)];
 #pragma unroll
-        for (int t = 0; t < kBs; ++t) {
-            const int j = j0 - t;
-            if (j < 0) break;
-            const double xj = j >= 64 ? rl64(yv[1], j - 64) : rl64(yv[0], j);
+        for (int b = 0; b < NB; ++b) {
+            if (b + 1 < NB)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const double upd = fma(-lt[t][q], xj, yv[q]);
-                yv[q] = lane + 64 * q < j ? upd : yv[q];
+                for (int t = 0; t < kBs; ++t) {
+                    const int j = NP - 1 - (b + 1) * kBs - t;
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        lt[(b + 1) & 1][t][q] = M[min(lane + 64 * q, NP - 1) * LD + (j > 0 ? j : 0)];
+                }
+#pragma unroll
+            for (int t = 0; t < kBs; ++t) {
+                const int j = NP - 1 - b * kBs - t;
+                if (j >= 0 && j < n) {
+                    const double xj = rl64(yv[j >> 6], j & 63);
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const double upd = fma(-lt[b & 1][t][q], xj, yv[q]);
+                        yv[q] = lane + 64 * q < j ? upd : yv[q];
+                    }
+                }
             }
         }
     }
@@ -4301,6 +4348,7 @@ struct BundleAdjuster {
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
     bool uv_env = true;         // RSVIO_BA_UV32=0: always upload (u, v) as f64 (A/B)
+    bool early_env = true;      // RSVIO_BA_EARLY_COPY=0: the observation section goes up with the rest (A/B)
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
     // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
@@ -4377,6 +4425,8 @@ struct BundleAdjuster {
         prof_env = std::getenv("RSVIO_BA_PROFILE") != nullptr;
         const char* u32v = std::getenv("RSVIO_BA_UV32");
         uv_env = !(u32v && u32v[0] == '0');
+        const char* ecv = std::getenv("RSVIO_BA_EARLY_COPY");
+        early_env = !(ecv && ecv[0] == '0');
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
@@ -4599,7 +4649,8 @@ struct BundleAdjuster {
             d_arena.alloc(2 * L.upload);
         }
         settled = false;  // (the upload, grow_buffers' memset and ba_build_layout go on the stream)
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice, stream));
+        if (early_env)
+            RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice, stream));
         mark();
         // waves: whole landmarks, <= 64 slots each (greedy, in landmark order); the Schur pair
         // stride is the largest XCD group's landmark count (at most one pair per landmark and
@@ -4680,13 +4731,14 @@ struct BundleAdjuster {
             run = std::max(run, cand[k]);
             G.env[k] = (unsigned char)(k >= n_free ? k : want_env ? std::max(k, run) : n_free - 1);
         }
+        G.env_on = want_env ? 1 : 0;
         for (int c = 0; c < 2; ++c)
             for (int i = 0; i < 16; ++i) G.TCB[c].m[i] = TCB2[16 * c + i];
         grow_buffers();  // (before the descriptor: it holds their addresses)
         fill_desc(hdesc);
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, L.mask, hipMemcpyHostToDevice, stream));
+        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
         {
