@@ -1073,10 +1073,9 @@ class BAWorkload:
         self._pinned = []
 
     def pin_windows(self):
-        """The windows' host arrays in page-locked memory (as a caller that builds its keyframe
-        windows in a pinned arena would): set_problem's observation pass reads ~0.6 MB of them per
-        window, and on pageable memory the kernel's NUMA-balancing scan occasionally unmaps those
-        pages, so one pass in a few hundred took ~6.7 ms of hinting faults (profiles/r06b_*)."""
+        """The windows' host arrays in page-locked memory (diagnostic, --pin-windows 1): the stall
+        it was meant to remove turned out to be trimmed heap memory re-faulted inside one
+        set_problem (--tame-malloc), not the caller's arrays (profiles/r06c_*, r06i_*)."""
         import dataclasses
 
         import torch
@@ -1201,11 +1200,14 @@ def main():
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
-    ap.add_argument("--tame-malloc", type=int, default=0,
-                    help="1: glibc malloc without trimming (mallopt), the stall A/B")
-    ap.add_argument("--pin-windows", type=int, default=1,
-                    help="1: the keyframe windows' host arrays in page-locked memory (0: pageable numpy arrays, "
-                         "where an occasional NUMA-balancing scan stalls one set_problem for ~6.7 ms)")
+    ap.add_argument("--tame-malloc", type=int, default=1,
+                    help="1 (default): glibc malloc without trimming and with a fixed mmap threshold (mallopt, as "
+                         "a real-time caller configures its process): otherwise about every other run one "
+                         "set_problem re-faults ~14-16 MB of trimmed heap (3.5-4.1k minor faults, 6-10 ms) -- "
+                         "the one slow repetition of rounds 4-5 (profiles/r06i_malloc_ab.txt); 0: glibc defaults")
+    ap.add_argument("--pin-windows", type=int, default=0,
+                    help="1: the keyframe windows' host arrays in page-locked memory (diagnostic of the stall; it "
+                         "did not remove it); 0 (default): ordinary numpy arrays, as a caller's Vecs")
     ap.add_argument("--precapture-graphs", type=int, default=1,
                     help="1: capture the tracker's per-phase frame graphs before the timed region (0: on first "
                          "use, as rounds 4-5 did -- one repetition then pays the instantiations)")

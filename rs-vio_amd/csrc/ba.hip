@@ -2174,9 +2174,9 @@ __device__ bool combine_p2p(const Geometry& G, const Prob& Pr, const Work& Wk, d
 }
 
 // pivot J of panel H (width PW) by wave 0: inv = 1 / d_K ready.  Column J+1 (the next pivot's)
-// and column J+2 are updated from readlanes of the unscaled column u; columns >= J+3 from LDS
-// broadcasts of u issued this step and consumed one step later (uq, with the pivot's l as lp), so
-// neither the readlane issue cost nor the LDS latency sits on the 1/d chain.
+// and column J+2 are updated from readlanes of the unscaled column u; columns >= J+3 from values
+// of u read this step and consumed one step later (uq, with the pivot's l as lp) -- by readlane
+// since round 6 (LDS broadcasts before: their wait sat between two pivots' chains).
 template <int H, int J, int PW>
 __device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMfPanel], double lp, double inv,
                                          double* Lf, double* Up, int lane, bool& bad) {
@@ -2191,7 +2191,20 @@ __device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMf
         uk1 = rl64(u, K + 1);
         const double piv = fma(-(uk1 * uk1), inv, rl64(a[J + 1], K + 1));
         bad |= !(piv > 0.0) || !isfinite(piv);
+#ifndef RSVIO_K5_RCP_LATE
+        // the hardware reciprocal issued here, before the barrier (round 6): left to the
+        // compiler, IR code sinking moved it past this pivot's other updates, so ~12 issue slots
+        // sat between the pivot and its reciprocal on the 1/d chain; the Newton steps follow where
+        // the next pivot needs them (rcp_f64's operations, the same bits).  Measured neutral
+        // (0.0302-0.0304 ms per LM iteration either way, profiles/r06i_rcp_ab.txt): the chain's
+        // issue slots, not this placement, bound it
+        double y0 = __builtin_amdgcn_rcp(piv);
+        __asm__ volatile("" : "+v"(y0));
+        const double e = fma(-piv, y0, 1.0);
+        inv_next = fma(y0, fma(e, e, e), y0);
+#else
         inv_next = rcp_f64(piv);
+#endif
     }
     const double l = u * inv;
     if constexpr (J + 1 < PW) a[J + 1] = fma(-l, uk1, a[J + 1]);
@@ -2202,9 +2215,10 @@ __device__ __forceinline__ void mf_pivot(double (&a)[kMfPanel], double (&uq)[kMf
     if constexpr (J + 2 < PW) a[J + 2] = fma(-l, rl64(u, K + 2), a[J + 2]);
     Lf[K * kMfLd + lane] = l;  // column K of L (rows > K; row NP: z_K); the upper part is never read
     Up[J * kMfLd + lane] = u;  // column J of the panel's U = D L
-#ifdef RSVIO_K5_RLQ
-    // A/B (round 6): the later columns' multipliers by readlane -- no LDS read and no wait on it
-    // between this pivot's chain and the next
+#ifndef RSVIO_K5_LDSQ
+    // round 6: the later columns' multipliers by readlane too -- no LDS read and no wait on it
+    // between this pivot's chain and the next (0.0305 -> 0.0302 ms per LM iteration, 3 of 3 A/B
+    // pairs, profiles/r06h_rlq_ab.txt); -DRSVIO_K5_LDSQ: LDS broadcasts (round 3-5)
 #pragma unroll
     for (int jj = J + 3; jj < PW; ++jj) uq[jj] = rl64(u, kMfPanel * H + jj);
 #else
@@ -4348,7 +4362,10 @@ struct BundleAdjuster {
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
     bool uv_env = true;         // RSVIO_BA_UV32=0: always upload (u, v) as f64 (A/B)
-    bool early_env = true;      // RSVIO_BA_EARLY_COPY=0: the observation section goes up with the rest (A/B)
+    // RSVIO_BA_EARLY_COPY=1: the observation section's copy issued as soon as the pass fills it
+    // (rounds 3-5); default one copy at the end: set_problem 61 -> 56 us of host time alone
+    // (profiles/r06g_setprob.txt), the step no slower (profiles/r06h_early_copy_ab.txt)
+    bool early_env = false;
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
     // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
@@ -4426,7 +4443,7 @@ struct BundleAdjuster {
         const char* u32v = std::getenv("RSVIO_BA_UV32");
         uv_env = !(u32v && u32v[0] == '0');
         const char* ecv = std::getenv("RSVIO_BA_EARLY_COPY");
-        early_env = !(ecv && ecv[0] == '0');
+        early_env = ecv && ecv[0] == '1';
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
