@@ -24,10 +24,11 @@ Also reported: BA ms per LM iteration, tracker ms per frame, the dominant kernel
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
-import resource
 import math
 import os
+import resource
 import sys
 import time
 from pathlib import Path
@@ -384,7 +385,8 @@ class _StageTimer:
         return self.be.set_map(*a)
 
 
-def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_seconds: float = 40.0):
+def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_seconds: float = 40.0,
+                         native: bool = True):
     """BASELINE config 4 on one GPU: the Estimator (estimator.rs:101-262) over the device backend
     on a rendered stereo stream of textured planes (synthetic.euroc_scene_stream_device, frames
     resident in HBM): per frame the tracker (6 levels, grid 50, fused radtan unprojection), PnP +
@@ -401,7 +403,7 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
 
     from rsvio import synthetic as S
     from rsvio.camera import Camera
-    from rsvio.estimator import DeviceBackend, Estimator
+    from rsvio.estimator import DeviceBackend, Estimator, NativeEstimator
     dev = f"cuda:{device}"
     s = S.euroc_scene_stream_device(n_frames, dev)
     torch.cuda.synchronize()
@@ -409,11 +411,20 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
 
     def run(frames):
         be = _StageTimer(DeviceBackend(W, H, cams, 6, 50, MAX_IT, THRESH, 10, 0.05, 0.05, device))
-        est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=be, pipelined=True)
-        t0 = time.perf_counter()
-        out = list(est.run(frames))
-        est.flush()
-        el = time.perf_counter() - t0
+        if native:  # the host logic in C++ (rsvio.estimator.NativeEstimator): the same calls
+            est = NativeEstimator(be.be, s.T_B_Cl, s.T_B_Cr, window=10)
+            t0 = time.perf_counter()
+            out = est.run(frames)
+            el = time.perf_counter() - t0
+            st = est.stats
+            be.t = {"track": st.track, "track_motion": st.track_motion, "ba": st.ba, "ba_wait": st.ba_wait}
+            be.n_solves, be.ba_iters = st.n_solves, st.ba_iterations
+        else:
+            est = Estimator(W, H, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=be, pipelined=True)
+            t0 = time.perf_counter()
+            out = list(est.run(frames))
+            est.flush()
+            el = time.perf_counter() - t0
         be.be.close()
         return out, el, be
 
@@ -432,6 +443,8 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
            "stage_ms_per_frame": {k: round(1e3 * v / n_frames, 4) for k, v in be.t.items()},
            "host_ms_per_frame": round(1e3 * (el - sum(be.t.values())) / n_frames, 4),
            "max_position_error_m": round(err, 5),
+           "host_logic": "C++ (rsvio.estimator.NativeEstimator, lib/librsvio_host.so)" if native
+                         else "Python (rsvio.estimator.Estimator)",
            "note": "frames already in HBM; stage times are host wall time around each device call "
                    "(each returns its results to the host, as the reference API does)"}
     if cpu:
@@ -1115,6 +1128,123 @@ class BAWorkload:
         return r
 
 
+class NativeProtocol:
+    """bench.py's protocol step driven from C++ (lib/librsvio_host.so, rs-vio_amd/driver/
+    protocol.cpp): the same calls on the same buffers as protocol_step's split order -- image
+    upload, rsvio_ba_set_problem of the next window, rsvio_ba_run_async, the frame's captured
+    tracker graph (every 4th frame enqueued directly with LK timing events, as trk.step does),
+    the frame's event polled, rsvio_ba_wait, rsvio_ba_get_state -- without Python between them,
+    as the reference's Rust caller runs them.  The library's entry points are passed as the
+    function pointers of the library rsvio already loaded."""
+
+    class Window(ctypes.Structure):
+        _fields_ = [("n_kf", ctypes.c_int32), ("pose7", ctypes.c_void_p), ("kf_fixed", ctypes.c_void_p),
+                    ("n_lm", ctypes.c_int32), ("p_W", ctypes.c_void_p), ("n_obs", ctypes.c_int32),
+                    ("obs_lm", ctypes.c_void_p), ("obs_kf", ctypes.c_void_p), ("obs_cam", ctypes.c_void_p),
+                    ("obs_uv", ctypes.c_void_p), ("T_C_B2", ctypes.c_void_p)]
+
+    class Frame(ctypes.Structure):
+        _fields_ = [("upload_dst", ctypes.c_void_p), ("upload_src", ctypes.c_void_p), ("upload_bytes", ctypes.c_size_t),
+                    ("graph_exec", ctypes.c_void_p), ("pyr_dst", ctypes.c_void_p), ("batches", ctypes.c_void_p)]
+
+    class Api(ctypes.Structure):
+        _fields_ = [(n, ctypes.c_void_p) for n in ("set_problem", "run_async", "wait", "get_state",
+                                                   "build_pyramids_d", "track_points_d")]
+
+    class Setup(ctypes.Structure):
+        _fields_ = [("api", ctypes.c_void_p), ("ba", ctypes.c_void_p), ("cfg", ctypes.c_void_p),
+                    ("trk_stream", ctypes.c_void_p), ("done_event", ctypes.c_void_p),
+                    ("n_windows", ctypes.c_int32), ("windows", ctypes.c_void_p),
+                    ("n_phases", ctypes.c_int32), ("frames", ctypes.c_void_p),
+                    ("pose_out", ctypes.c_void_p), ("pw_out", ctypes.c_void_p),
+                    ("first_phase", ctypes.c_int32), ("first_window", ctypes.c_int32),
+                    ("track_ctx", ctypes.c_void_p), ("max_iterations", ctypes.c_int32), ("thresh", ctypes.c_float),
+                    ("d_out", ctypes.c_void_p), ("h_out", ctypes.c_void_p), ("out_bytes", ctypes.c_size_t),
+                    ("d_valid", ctypes.c_void_p), ("h_valid", ctypes.c_void_p), ("valid_bytes", ctypes.c_size_t),
+                    ("first_step", ctypes.c_int32), ("lk_events", ctypes.c_void_p), ("n_lk_events", ctypes.c_int32)]
+
+    def __init__(self, trk: "TrackerWorkload", ba: "BAWorkload", state_out, max_steps: int):
+        from rsvio import _lib
+        from rsvio.ba import BundleAdjuster, _DEFAULT_CFG
+        lib = _lib.load()
+        path = _lib.LIB_PATH.parent / "librsvio_host.so"
+        self.drv = ctypes.CDLL(str(path))
+        self.drv.rsvio_protocol_run.restype = ctypes.c_int
+        self.drv.rsvio_protocol_run.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p]
+        fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+        self.api = self.Api(fp(lib.rsvio_ba_set_problem), fp(lib.rsvio_ba_run_async), fp(lib.rsvio_ba_wait),
+                            fp(lib.rsvio_ba_get_state), fp(lib.rsvio_build_pyramids_d), fp(lib.rsvio_track_points_d))
+        self.keep = []
+        wins = (self.Window * len(ba.windows))()
+        for i, w in enumerate(ba.windows):
+            keep, args = BundleAdjuster._marshal(*(getattr(w, f) for f in BundleAdjuster._FIELDS))
+            self.keep.append(keep)
+            wins[i] = self.Window(*args)
+        nph = len(trk.seq)
+        frames = (self.Frame * nph)()
+        for ph in range(nph):
+            plan = trk._plan(ph, True)
+            ex = trk._graphs.get((ph, True, True))
+            if ex is None:
+                ex = trk._capture(plan, True, True, trk.stream.cuda_stream)
+                trk._graphs[(ph, True, True)] = ex
+            frames[ph] = self.Frame(plan["src"], plan["h_img"], plan["img_bytes"], ex, plan["dst"],
+                                    ctypes.addressof(plan["batches"]))
+        self.wins, self.frames = wins, frames
+        n_ev = max_steps // 4 + 2
+        create = lib.hipEventCreateWithFlags
+        create.restype, create.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint]
+        self._elapsed = lib.hipEventElapsedTime
+        self._elapsed.restype = ctypes.c_int
+        self._elapsed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        self._destroy = lib.hipEventDestroy
+        self._destroy.restype, self._destroy.argtypes = ctypes.c_int, [ctypes.c_void_p]
+        self.ev_ptrs = (ctypes.c_void_p * (2 * n_ev))()
+        for i in range(2 * n_ev):
+            e = ctypes.c_void_p()
+            _lib.check(create(ctypes.byref(e), 0))  # hipEventDefault: timing
+            self.ev_ptrs[i] = e.value
+        self.cfg = _DEFAULT_CFG
+        self.trk, self.ba, self.state_out = trk, ba, state_out
+        self.n_ev = n_ev
+
+    def run(self, steps: int):
+        """`steps` protocol steps from the workloads' current phase and window; advances them."""
+        trk, ba = self.trk, self.ba
+        setup = self.Setup(ctypes.addressof(self.api), ba.ba._h.value, ctypes.addressof(self.cfg),
+                           trk.stream.cuda_stream, trk._done_ev, len(ba.windows), ctypes.addressof(self.wins),
+                           len(trk.seq), ctypes.addressof(self.frames),
+                           self.state_out[0].ctypes.data, self.state_out[1].ctypes.data,
+                           trk.k % len(trk.seq), (ba.k + 1) % len(ba.windows),
+                           trk.ctx.value, MAX_IT, THRESH,
+                           trk.out.data_ptr(), trk.h_out.data_ptr(), trk.out.numel() * 4,
+                           trk.valid.data_ptr(), trk.h_valid.data_ptr(), trk.valid.numel(),
+                           trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev)
+        iters = (ctypes.c_int32 * steps)()
+        sms = (ctypes.c_double * steps)()
+        sec, npair = ctypes.c_double(0.0), ctypes.c_int32(0)
+        rc = self.drv.rsvio_protocol_run(ctypes.addressof(setup), steps, iters, sms, ctypes.byref(sec),
+                                         ctypes.byref(npair))
+        if rc:
+            raise RuntimeError(f"rsvio_protocol_run failed: {rc}")
+        trk.k += steps
+        trk.slot ^= steps & 1
+        ba.k += steps
+        lk = []
+        for i in range(npair.value):
+            ms = ctypes.c_float(0.0)
+            _ = self._elapsed(ctypes.byref(ms), self.ev_ptrs[2 * i], self.ev_ptrs[2 * i + 1])
+            lk.append(ms.value)
+        return list(iters), list(sms), lk
+
+    def close(self):
+        for e in self.ev_ptrs:
+            if e:
+                self._destroy(e)
+        self.ev_ptrs = (ctypes.c_void_p * 0)()
+
+
 def host_cores() -> int:
     """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS, set per GPU on
     the pool) or the affinity mask."""
@@ -1200,6 +1330,10 @@ def main():
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
+    ap.add_argument("--driver", default="native", choices=["native", "python"],
+                    help="who runs the protocol step's calls: native (default) -- lib/librsvio_host.so, the same "
+                         "C ABI calls from C++ as the reference's Rust caller makes them; python -- this loop "
+                         "(ctypes; ~1-5 us of interpreter per call; --trace-steps uses it)")
     ap.add_argument("--tame-malloc", type=int, default=1,
                     help="1 (default): glibc malloc without trimming and with a fixed mmap threshold (mallopt, as "
                          "a real-time caller configures its process): otherwise about every other run one "
@@ -1334,10 +1468,31 @@ def main():
         ba.pin_windows()
     if args.precapture_graphs:
         trk.precapture(True, args.order == "split")
-    for _ in range(max(args.warmup, 2)):
-        protocol_step(False)
+    native = None
+    if args.driver == "native" and args.order == "split" and not args.trace_steps:
+        native = NativeProtocol(trk, ba, state_out, max(args.steps, args.warmup, 2))
+        native.run(max(args.warmup, 2))
+    else:
+        for _ in range(max(args.warmup, 2)):
+            protocol_step(False)
     minflt0 = _minor_faults()
-    el_pro = timed_reps(protocol_step, args.reps)
+    if native is None:
+        el_pro = timed_reps(protocol_step, args.reps)
+        lk_pro = None
+    else:
+        import gc
+        el_pro, lk_pro = [], []
+        for _ in range(args.reps):
+            barrier(world)
+            gc.disable()
+            t0 = time.perf_counter()
+            its, sms, lk = native.run(args.steps)
+            barrier(world)
+            el_pro.append(max_over_ranks(time.perf_counter() - t0, world))
+            gc.enable()
+            ba.iters += its
+            ba.solve_ms += sms
+            lk_pro += lk
     minflt = _minor_faults() - minflt0
     if trace is not None:
         names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
@@ -1354,7 +1509,7 @@ def main():
     frames = world * args.steps
     value = frames / elapsed
     value_res = frames / elapsed_res
-    lk_ms = trk.lk_ms()
+    lk_ms = trk.lk_ms() if lk_pro is None else (float(np.mean(lk_pro)) if lk_pro else float("nan"))
     ba_iters = float(np.mean(ba.iters))
     ba_solve_ms = float(np.mean(ba.solve_ms))
     ba_ms_iter = ba_solve_ms / ba_iters
@@ -1379,6 +1534,8 @@ def main():
                       "uploaded (rsvio_ba_set_problem: sort, tables, pinned staging, H2D; two windows "
                       "alternate) and solved (graph re-captured), its state (48.6 KB) D2H",
         "value_reps": [round(frames / e, 3) for e in el_pro],
+        "driver": "native (lib/librsvio_host.so: the step's C ABI calls from C++)" if native is not None
+                  else "python (ctypes)",
         "value_reps_min": round(frames / max(el_pro), 3),
         "protocol_minor_faults": minflt,
         "host_numa_balancing": _read_text("/proc/sys/kernel/numa_balancing"),
@@ -1439,7 +1596,8 @@ def main():
         out.setdefault("rows", {})["tracker_batched"] = measure_tracker_batched_row(trk, local, args.batch_streams)
     if rank == 0 and not args.no_rows and args.pipeline_frames > 0:
         out.setdefault("rows", {})["pipeline_config4"] = measure_pipeline_row(
-            local, cpu=(world == 1 and not args.no_cpu), n_frames=args.pipeline_frames)
+            local, cpu=(world == 1 and not args.no_cpu), n_frames=args.pipeline_frames,
+            native=args.driver == "native")
     if rank == 0 and world == 1 and not args.no_cpu:
         # two legs -- all host cores (the reported baseline, rayon's parallelism) and
         # one thread -- each a bounded sample of the same per-frame work
@@ -1461,6 +1619,8 @@ def main():
         dist.destroy_process_group()
     # release device objects before interpreter teardown (the CU-mask streams last)
     torch.cuda.synchronize()
+    if native is not None:
+        native.close()
     ba.ba.close()
     trk.close()
     for st in streams:

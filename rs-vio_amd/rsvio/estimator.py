@@ -21,6 +21,7 @@ upload and start) run while frame t + 1 tracks.  Results equal process_frame's f
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass
 
 import numpy as np
@@ -213,3 +214,87 @@ class Estimator:
         self.flush()
         if hasattr(self.backend, "close"):
             self.backend.close()
+
+
+class NativeEstimator:
+    """Estimator.run (pipelined, the tracker one frame ahead) with its host logic in C++
+    (lib/librsvio_host.so, rs-vio_amd/driver/estimator.cpp): the same steps over the same
+    DeviceBackend handles, as the reference's compiled Rust estimator runs them -- no interpreter
+    between the device calls.  Frame for frame the same outputs as Estimator(pipelined=True).run
+    (tests/test_estimator_gpu.py); `stats` holds the host wall time per stage."""
+
+    _INT_NONE = -(2 ** 31)
+
+    class Api(C.Structure):
+        _fields_ = [(n, C.c_void_p) for n in ("submit_device", "collect", "undistorted", "set_map", "track_motion",
+                                              "window_problem", "window_apply", "set_problem", "run_async", "wait",
+                                              "run", "get_state")]
+
+    class Setup(C.Structure):
+        pass
+
+    class FrameOut(C.Structure):
+        _fields_ = [("frame_id", C.c_int32), ("is_keyframe", C.c_int32), ("n_left", C.c_int32),
+                    ("n_right", C.c_int32), ("pnp_status", C.c_int32), ("pnp_iterations", C.c_int32),
+                    ("ba_status", C.c_int32), ("ba_iterations", C.c_int32), ("pnp_cost", C.c_double),
+                    ("T_W_B", C.c_double * 16)]
+
+    class Stats(C.Structure):
+        _fields_ = [("track", C.c_double), ("track_motion", C.c_double), ("ba", C.c_double),
+                    ("ba_wait", C.c_double), ("total", C.c_double), ("n_solves", C.c_int32),
+                    ("ba_iterations", C.c_int32), ("fallbacks", C.c_int32), ("reserved", C.c_int32)]
+
+    def __init__(self, backend: DeviceBackend, T_B_Cl, T_B_Cr, window: int = 10):
+        from . import _lib
+        from .ba import fallback_cfg, lm_cfg
+        from .motion import pnp_cfg
+        lib = _lib.load()
+        self.drv = C.CDLL(str(_lib.LIB_PATH.parent / "librsvio_host.so"))
+        self.drv.rsvio_est_run.restype = C.c_int
+        self.drv.rsvio_est_run.argtypes = [C.c_void_p] * 6
+        fp = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+        self.api = self.Api(*[fp(getattr(lib, "rsvio_" + n)) for n in (
+            "tracker_submit_device", "tracker_collect", "tracker_undistorted", "pnp_set_map", "track_motion_tracker",
+            "window_problem", "window_apply", "ba_set_problem", "ba_run_async", "ba_wait", "ba_run", "ba_get_state")])
+        T_B_Cl = np.ascontiguousarray(T_B_Cl, np.float64).reshape(16)
+        T_B_Cr = np.ascontiguousarray(T_B_Cr, np.float64).reshape(16)
+        # the rig's inverse as the Python Estimator computes it (Estimator._T_C_B2: np.linalg.inv)
+        tcb = np.linalg.inv(np.stack([T_B_Cl.reshape(4, 4), T_B_Cr.reshape(4, 4)])).reshape(32)
+        self.setup = self.Setup(C.addressof(self.api), backend.tracker._h.value,
+                                backend.motion._h.value, backend.solver._h.value, window, backend.tracker.cap,
+                                (C.c_double * 16)(*T_B_Cl), (C.c_double * 16)(*T_B_Cr), (C.c_double * 32)(*tcb),
+                                lm_cfg(), fallback_cfg(), pnp_cfg(), backend.motion.rule)
+        self.stats = None
+
+    def run(self, frames):
+        """frames: (left, right) device-resident u8 tensors (data_ptr); returns the FrameResults."""
+        n = len(frames)
+        dl = (C.c_void_p * max(n, 1))(*[l.data_ptr() for l, _ in frames])
+        dr = (C.c_void_p * max(n, 1))(*[r.data_ptr() for _, r in frames])
+        out = (self.FrameOut * max(n, 1))()
+        st = self.Stats()
+        rc = self.drv.rsvio_est_run(C.addressof(self.setup), C.addressof(dl), C.addressof(dr), n, C.addressof(out),
+                                    C.addressof(st))
+        if rc:
+            raise RuntimeError(f"rsvio_est_run failed: {rc}")
+        self.stats = st
+        none = lambda v: None if v == self._INT_NONE else int(v)  # noqa: E731
+        res = []
+        for o in out[:n]:
+            res.append(FrameResult(o.frame_id, bool(o.is_keyframe), np.array(o.T_W_B[:], np.float64).reshape(4, 4),
+                                   o.n_left, o.n_right, none(o.pnp_status), none(o.ba_status),
+                                   pnp_iterations=none(o.pnp_iterations),
+                                   pnp_cost=None if o.pnp_status == self._INT_NONE else float(o.pnp_cost),
+                                   ba_iterations=none(o.ba_iterations)))
+        return res
+
+
+def _native_setup_fields():
+    from . import _lib
+    return [("api", C.c_void_p), ("tracker", C.c_void_p), ("pnp", C.c_void_p), ("ba", C.c_void_p),
+            ("window", C.c_int32), ("max_features", C.c_int32), ("T_B_Cl", C.c_double * 16),
+            ("T_B_Cr", C.c_double * 16), ("T_C_B2", C.c_double * 32), ("ba_cfg", _lib.LmCfg),
+            ("ba_fallback", _lib.LmCfg), ("pnp_cfg", _lib.LmCfg), ("rule", _lib.KeyframeRule)]
+
+
+NativeEstimator.Setup._fields_ = _native_setup_fields()

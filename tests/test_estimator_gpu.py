@@ -160,3 +160,37 @@ def test_estimator_pipelined_matches_sequential(gpu, scene_stream):
         assert sorted(ma) == sorted(mb) and all(np.array_equal(ma[i], mb[i]) for i in ma)
     for e in ests:
         e.close()
+
+
+def test_native_estimator_equals_python_estimator(gpu):
+    """The Estimator's host logic in C++ (rsvio.estimator.NativeEstimator over lib/librsvio_host.so,
+    the loop a compiled caller runs) against the Python Estimator in the same mode (pipelined, the
+    tracker one frame ahead) on the bench's config-4 stream, 200 frames resident on the device:
+    the same device calls in the same order, so every frame's keyframe flag, feature counts, PnP
+    and BA status / iterations / cost and pose are bit-identical."""
+    import torch
+
+    from rsvio import synthetic as S
+    from rsvio.camera import Camera
+    from rsvio.estimator import DeviceBackend, Estimator, NativeEstimator
+    s = S.euroc_scene_stream_device(200, torch.device("cuda", 0))
+    h, w = s.frames[0][0].shape
+    cams = [Camera.opencv5(*p) for p in s.intrinsics]
+    be_p = DeviceBackend(w, h, cams, 6, 50, 20, 0.01, 10, 0.05, 0.05, 0)
+    est = Estimator(w, h, cams, s.T_B_Cl, s.T_B_Cr, window=10, backend=be_p, pipelined=True)
+    rp = list(est.run(s.frames))
+    est.flush()
+    be_n = DeviceBackend(w, h, cams, 6, 50, 20, 0.01, 10, 0.05, 0.05, 0)
+    nat = NativeEstimator(be_n, s.T_B_Cl, s.T_B_Cr, window=10)
+    rn = nat.run(s.frames)
+    assert len(rp) == len(rn) == 200
+    n_kf = n_ba = 0
+    for k, (a, b) in enumerate(zip(rp, rn)):
+        assert (a.frame_id, a.is_keyframe, a.n_left, a.n_right) == (b.frame_id, b.is_keyframe, b.n_left, b.n_right), k
+        assert _outcome(a) == _outcome(b), k
+        assert np.array_equal(a.T_W_B, b.T_W_B), k
+        n_kf += a.is_keyframe
+        n_ba += a.ba_status is not None
+    assert n_kf >= 50 and n_ba >= 40 and nat.stats.n_solves == n_ba
+    est.close()
+    be_n.close()
