@@ -635,6 +635,28 @@ def tame_malloc():
     log(f"[bench] malloc: no trimming, mmap threshold 32 MB ({'ok' if ok else 'mallopt refused'})")
 
 
+def lock_code() -> str:
+    """mlock the executable mappings of the HIP / HSA runtimes and the product library (diagnostic
+    of the one-rep stall: if host memory pressure drops their code pages from this process, the
+    next call through a cold path re-faults them).  Only when RLIMIT_MEMLOCK covers them."""
+    libc = ctypes.CDLL("libc.so.6", use_errno=True)
+    libc.mlock.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    names = ("libamdhip64", "libhsa-runtime64", "librsvio", "libhsakmt", "libc.so", "libstdc++")
+    spans = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and parts[1].startswith("r") and any(n in parts[5] for n in names):
+                a, b = (int(x, 16) for x in parts[0].split("-"))
+                spans.append((a, b - a))
+    total = sum(n for _, n in spans)
+    soft, _ = resource.getrlimit(resource.RLIMIT_MEMLOCK)
+    if soft != resource.RLIM_INFINITY and total > soft:
+        return f"skipped: {total >> 20} MB of mappings > RLIMIT_MEMLOCK {soft >> 10} KB"
+    bad = sum(1 for a, n in spans if libc.mlock(a, n) != 0)
+    return f"locked {len(spans) - bad}/{len(spans)} mappings, {total >> 20} MB"
+
+
 def setup_dist(same_device: bool = False):
     """One process per GPU over RCCL.  `same_device` is a rehearsal mode for a one-GPU box: every
     rank on cuda:0 with a gloo control group (RCCL refuses two ranks on one device)."""
@@ -1334,6 +1356,8 @@ def main():
                     help="who runs the protocol step's calls: native (default) -- lib/librsvio_host.so, the same "
                          "C ABI calls from C++ as the reference's Rust caller makes them; python -- this loop "
                          "(ctypes; ~1-5 us of interpreter per call; --trace-steps uses it)")
+    ap.add_argument("--lock-code", type=int, default=0,
+                    help="1: mlock the runtimes' and the library's mapped pages (stall diagnostic)")
     ap.add_argument("--tame-malloc", type=int, default=1,
                     help="1 (default): glibc malloc without trimming and with a fixed mmap threshold (mallopt, as "
                          "a real-time caller configures its process): otherwise about every other run one "
@@ -1368,6 +1392,8 @@ def main():
 
     import rsvio
     arch = rsvio.require_device(local)
+    if args.lock_code:
+        log(f"[bench] lock-code: {lock_code()}")
     log(f"[bench] rank {rank}/{world} on cuda:{local} ({arch})")
     streams = []
     if args.cu_split > 0:
