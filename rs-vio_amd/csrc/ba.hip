@@ -41,7 +41,7 @@
 
 #include "common.hpp"
 
-#include <immintrin.h>  // host: set_problem's vectorised observation pass
+#include "obs_pass.hpp"  // host: set_problem's observation pass
 #include "se3.hpp"
 #include "wave.hpp"
 
@@ -3989,120 +3989,9 @@ __global__ __launch_bounds__(256) void ba_p2p_trial(Geometry G, Prob Pr, Work Wk
 RSVIO_DBG_READER(rsvio_dbg_ba_stamps)
 RSVIO_RT_READER(rsvio_dbg_ba_rt)
 
-// ======================================================================================
-// The observations' (u, v) into the staging image as f32 when every value is exactly an f32 (the
-// estimator's are: normalised coordinates unprojected from f32 pixels and stored as f32 features,
-// frame.rs:107-134 -> sliding_window.rs:274-300), halving the largest part of the window's PCIe
-// upload; false (nothing usable written) if one is not, and the caller copies the f64 values.
-__attribute__((target("avx2"))) static bool uv_narrow_avx2(size_t n2, const double* uv, float* out) {
-    size_t i = 0;
-    __m256d bad = _mm256_setzero_pd();
-    for (; i + 4 <= n2; i += 4) {
-        const __m256d d = _mm256_loadu_pd(uv + i);
-        const __m128 f = _mm256_cvtpd_ps(d);
-        bad = _mm256_or_pd(bad, _mm256_cmp_pd(_mm256_cvtps_pd(f), d, _CMP_NEQ_UQ));
-        _mm_storeu_ps(out + i, f);
-    }
-    bool ok = _mm256_movemask_pd(bad) == 0;
-    for (; i < n2; ++i) {
-        out[i] = (float)uv[i];
-        ok &= (double)out[i] == uv[i];
-    }
-    return ok;
-}
-static bool uv_narrow(size_t n2, const double* uv, float* out) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2) return uv_narrow_avx2(n2, uv, out);
-    bool ok = true;
-    for (size_t i = 0; i < n2; ++i) {
-        out[i] = (float)uv[i];
-        ok &= (double)out[i] == uv[i];
-    }
-    return ok;
-}
-
-// ======================================================================================
-// set_problem's observation pass, fast path (host).  Keys l << 6 | k << 1 | c with the index
-// validation, 8 observations per AVX2 step (when the host has it); false if an index is out of
-// range (the exact pass then reports which).
-__attribute__((target("avx2"))) static bool obs_keys_avx2(int n_obs, const int32_t* lm, const int32_t* kf,
-                                                        const uint8_t* cam, int n_lm, int n_kf, unsigned* key) {
-    const __m256i nl1 = _mm256_set1_epi32(n_lm - 1), nk1 = _mm256_set1_epi32(n_kf - 1), one = _mm256_set1_epi32(1);
-    __m256i bad = _mm256_setzero_si256();
-    int i = 0;
-    for (; i + 8 <= n_obs; i += 8) {
-        const __m256i l = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(lm + i));
-        const __m256i k = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(kf + i));
-        const __m256i c = _mm256_cvtepu8_epi32(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(cam + i)));
-        // x > n - 1 (unsigned; negative indices are huge)  <=>  max(x, n - 1) != n - 1
-        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(l, nl1), nl1));
-        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(k, nk1), nk1));
-        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu32(c, one), one));
-        const __m256i kk = _mm256_or_si256(_mm256_or_si256(_mm256_slli_epi32(l, 6), _mm256_slli_epi32(k, 1)), c);
-        _mm256_storeu_si256(reinterpret_cast<__m256i*>(key + i), kk);
-    }
-    unsigned bad_t = 0;
-    for (; i < n_obs; ++i) {
-        const unsigned l = (unsigned)lm[i], k = (unsigned)kf[i], c = cam[i];
-        bad_t |= (unsigned)(l >= (unsigned)n_lm) | (unsigned)(k >= (unsigned)n_kf) | (unsigned)(c > 1);
-        key[i] = l << 6 | k << 1 | c;
-    }
-    return _mm256_testz_si256(bad, bad) && !bad_t;
-}
-
-static bool obs_keys(int n_obs, const int32_t* lm, const int32_t* kf, const uint8_t* cam, int n_lm, int n_kf,
-                     unsigned* key) {
-    if (n_lm <= 0 || n_kf <= 0) return false;
-    static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2) return obs_keys_avx2(n_obs, lm, kf, cam, n_lm, n_kf, key);
-    unsigned bad = 0;
-    for (int i = 0; i < n_obs; ++i) {
-        const unsigned l = (unsigned)lm[i], k = (unsigned)kf[i], c = cam[i];
-        bad |= (unsigned)(l >= (unsigned)n_lm) | (unsigned)(k >= (unsigned)n_kf) | (unsigned)(c > 1);
-        key[i] = l << 6 | k << 1 | c;
-    }
-    return !bad;
-}
-
-// Per-landmark (keyframe, camera) masks from the keys when each landmark's observations are
-// contiguous (a landmark-major list, as SlidingWindow builds it): four independent chains over
-// run-aligned quarters, each keeping its current run's mask in a register and storing it (no
-// load on the chain).  True iff the masks hold n_obs bits in total -- no duplicate observation and
-// no landmark in two runs; otherwise the exact pass rebuilds them (and reports a duplicate).
-__attribute__((target("popcnt"))) static bool obs_masks_runs(int n_obs, const unsigned* key, int n_lm,
-                                                            unsigned long long* m2) {
-    std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
-    int cut[5];
-    cut[0] = 0;
-    cut[4] = n_obs;
-    for (int q = 1; q < 4; ++q) {
-        int c = std::max((int)((long long)q * n_obs / 4), cut[q - 1]);
-        while (c > 0 && c < n_obs && (key[c] >> 6) == (key[c - 1] >> 6)) ++c;
-        cut[q] = c;
-    }
-    int len = n_obs;
-    for (int q = 0; q < 4; ++q) len = std::min(len, cut[q + 1] - cut[q]);
-    unsigned cl[4] = {~0u, ~0u, ~0u, ~0u};
-    unsigned long long cm[4] = {0, 0, 0, 0};
-    auto step = [&](int q, int i) {
-        const unsigned kj = key[i], l = kj >> 6;
-        const unsigned long long b = 1ull << (kj & 63);
-        cm[q] = l == cl[q] ? (cm[q] | b) : b;
-        cl[q] = l;
-        m2[l] = cm[q];
-    };
-    for (int j = 0; j < len; ++j) {
-        step(0, cut[0] + j);
-        step(1, cut[1] + j);
-        step(2, cut[2] + j);
-        step(3, cut[3] + j);
-    }
-    for (int q = 0; q < 4; ++q)
-        for (int i = cut[q] + len; i < cut[q + 1]; ++i) step(q, i);
-    long long bits = 0;
-    for (int l = 0; l < n_lm; ++l) bits += __builtin_popcountll(m2[l]);
-    return bits == n_obs;
-}
+// set_problem's observation pass (keys, masks, (u, v) narrowed) lives in obs_pass.hpp: chunked
+// over the calling thread and a few helper threads.
+using rsvio_obs::observation_pass;
 
 // slots of a landmark = keyframes with any of its observations (bits 2 kf, 2 kf + 1 of its mask)
 __attribute__((target("popcnt"))) static inline int slot_count(unsigned long long m) {
@@ -4631,10 +4520,14 @@ struct BundleAdjuster {
         // observations: validated, a (keyframe, camera) bit per landmark, packed keys
         auto* m2 = reinterpret_cast<unsigned long long*>(hb + L.mask);
         auto* key = reinterpret_cast<unsigned*>(hb + L.key);
-        // fast path: vectorised keys + validation, masks by run-aligned chains (obs_masks_runs);
-        // anything else (an index out of range, a duplicate, a landmark in two runs) takes the
-        // exact pass below, which reports the error or builds the masks of any order
-        if (!(obs_keys(n_obs, obs_lm, obs_kf, obs_cam, n_lm, n_kf, key) && obs_masks_runs(n_obs, key, n_lm, m2))) {
+        // fast path: vectorised keys + validation, masks by run-aligned chains and the (u, v) as f32
+        // when exact (half the bytes to copy and to upload), in landmark-run-aligned chunks over the
+        // helper threads (obs_pass.hpp); anything else (an index out of range, a duplicate, a
+        // landmark in two runs) takes the exact pass below, which reports the error or builds the
+        // masks of any order
+        bool uv32 = false;
+        if (!observation_pass(n_obs, obs_lm, obs_kf, obs_cam, obs_uv, n_lm, n_kf, key, m2,
+                              uv_env ? reinterpret_cast<float*>(hb + L.ouv) : nullptr, &uv32)) {
             std::memset(m2, 0, sizeof(unsigned long long) * (size_t)n_lm);
             // the mask of the current run of one landmark's observations stays in a register (a
             // landmark-major list would otherwise chain every read-modify-write of m2[l] through
@@ -4657,9 +4550,8 @@ struct BundleAdjuster {
                 key[i] = (unsigned)l << 6 | (unsigned)k << 1 | (unsigned)c;
             }
             if (cl >= 0) m2[cl] = cm;
+            uv32 = uv_env && rsvio_obs::uv_narrow(2 * (size_t)n_obs, obs_uv, reinterpret_cast<float*>(hb + L.ouv));
         }
-        // (u, v) as f32 when exact (half the bytes to copy and to upload), else as given
-        const bool uv32 = uv_env && uv_narrow(2 * (size_t)n_obs, obs_uv, reinterpret_cast<float*>(hb + L.ouv));
         if (!uv32) std::memcpy(hb + L.ouv, obs_uv, sizeof(double2) * (size_t)n_obs);
         L.upload = L.ouv + al((uv32 ? sizeof(float2) : sizeof(double2)) * std::max(n_obs, 1));
         if (d_arena.n < L.upload) {  // (grown for the whole arena below once its size is known)
