@@ -1183,9 +1183,10 @@ class NativeProtocol:
                     ("track_ctx", ctypes.c_void_p), ("max_iterations", ctypes.c_int32), ("thresh", ctypes.c_float),
                     ("d_out", ctypes.c_void_p), ("h_out", ctypes.c_void_p), ("out_bytes", ctypes.c_size_t),
                     ("d_valid", ctypes.c_void_p), ("h_valid", ctypes.c_void_p), ("valid_bytes", ctypes.c_size_t),
-                    ("first_step", ctypes.c_int32), ("lk_events", ctypes.c_void_p), ("n_lk_events", ctypes.c_int32)]
+                    ("first_step", ctypes.c_int32), ("lk_events", ctypes.c_void_p), ("n_lk_events", ctypes.c_int32),
+                    ("order", ctypes.c_int32)]
 
-    def __init__(self, trk: "TrackerWorkload", ba: "BAWorkload", state_out, max_steps: int):
+    def __init__(self, trk: "TrackerWorkload", ba: "BAWorkload", state_out, max_steps: int, order: int = 0):
         from rsvio import _lib
         from rsvio.ba import BundleAdjuster, _DEFAULT_CFG
         lib = _lib.load()
@@ -1230,6 +1231,7 @@ class NativeProtocol:
         self.cfg = _DEFAULT_CFG
         self.trk, self.ba, self.state_out = trk, ba, state_out
         self.n_ev = n_ev
+        self.order = order
 
     def run(self, steps: int):
         """`steps` protocol steps from the workloads' current phase and window; advances them."""
@@ -1242,7 +1244,7 @@ class NativeProtocol:
                            trk.ctx.value, MAX_IT, THRESH,
                            trk.out.data_ptr(), trk.h_out.data_ptr(), trk.out.numel() * 4,
                            trk.valid.data_ptr(), trk.h_valid.data_ptr(), trk.valid.numel(),
-                           trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev)
+                           trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev, self.order)
         iters = (ctypes.c_int32 * steps)()
         sms = (ctypes.c_double * steps)()
         sec, npair = ctypes.c_double(0.0), ctypes.c_int32(0)
@@ -1342,13 +1344,15 @@ def main():
                          "best (round 2 sweep: K4c's 360 two-wave-per-SIMD workgroups fit the BA's 192 CUs "
                          "in one round)")
     ap.add_argument("--cu-layout", default="block", choices=["stride", "block"])
-    ap.add_argument("--order", default="split", choices=["frame-first", "ba-first", "split"],
+    ap.add_argument("--order", default="split", choices=["frame-first", "ba-first", "split", "window-first"],
                     help="protocol step: the frame's image upload first, then the keyframe window's upload + "
                          "solve start, then the frame's kernels and downloads (split, the default: 4.16-4.35k vs "
                          "3.98-4.08k frames/s for ba-first and 3.74-3.96k for frame-first on one box, "
                          "profiles/r05h_order_ab.txt -- the image and window uploads share the copy engine, and "
                          "the image then lands first without holding the window back behind the frame's kernels "
-                         "enqueue); both paths run concurrently either way (the tracker does not depend on the solve)")
+                         "enqueue); both paths run concurrently either way (the tracker does not depend on the solve); "
+                         "window-first: the window's upload, then the image upload, then the solve start and the "
+                         "frame (the window's copy ahead of the image's)")
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
@@ -1438,13 +1442,15 @@ def main():
         if tr:
             m.append(time.perf_counter())
         ba.next_window()
+        if args.order == "window-first":
+            trk.upload()
         if tr:
             m.append(time.perf_counter())
         ba.start()
         if tr:
             m.append(time.perf_counter())
         if args.order != "frame-first":
-            trk.step(timed, pcie=True, wait=False, uploaded=args.order == "split")
+            trk.step(timed, pcie=True, wait=False, uploaded=args.order in ("split", "window-first"))
         if tr:
             m.append(time.perf_counter())
         trk.sync()
@@ -1493,10 +1499,11 @@ def main():
     if args.pin_windows:
         ba.pin_windows()
     if args.precapture_graphs:
-        trk.precapture(True, args.order == "split")
+        trk.precapture(True, args.order in ("split", "window-first"))
     native = None
-    if args.driver == "native" and args.order == "split" and not args.trace_steps:
-        native = NativeProtocol(trk, ba, state_out, max(args.steps, args.warmup, 2))
+    if args.driver == "native" and args.order in ("split", "window-first") and not args.trace_steps:
+        native = NativeProtocol(trk, ba, state_out, max(args.steps, args.warmup, 2),
+                                order=1 if args.order == "window-first" else 0)
         native.run(max(args.warmup, 2))
     else:
         for _ in range(max(args.warmup, 2)):
@@ -1584,6 +1591,7 @@ def main():
                    "landmarks_per_gpu": prob.n_lm, "observations_per_gpu": prob.n_obs,
                    "parallelism": f"tracker replicas x{world}, BA landmark-sharded over {world} GPU(s)"
                                    + (f" ({ba.collective} all-reduce)" if world > 1 else ""),
+                   "order": args.order,
                    "cu_partition": (f"{args.cu_layout} {args.cu_split:g} of CUs to the tracker stream"
                                     if args.cu_split > 0 else "none")},
         "ba_ms_per_iter": round(ba_ms_iter, 4),

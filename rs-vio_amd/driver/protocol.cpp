@@ -8,7 +8,7 @@
 // driver runs the same calls, in the same order, on the same buffers, from C++ -- nothing in it
 // is device work of its own, and nothing of the step is skipped:
 //
-//   per step k (split order, bench.py protocol_step):
+//   per step k (split order, bench.py protocol_step; order 1 swaps steps 1 and 2):
 //     1. the next frame's two images up from pinned host memory (hipMemcpyAsync, tracker stream);
 //     2. a NEW keyframe window: rsvio_ba_set_problem (two pre-built windows alternate);
 //     3. rsvio_ba_run_async (the solve's captured graph);
@@ -91,6 +91,9 @@ struct rsvio_protocol {
     int32_t first_step;
     void** lk_events;          // 2 hipEvent_t (timing) per sampled step, in order; null: no sampling
     int32_t n_lk_events;       // pairs available
+    int32_t order;             // 0: split (image upload, window, solve start, frame); 1: window first
+                               // (window, image upload, solve start, frame: the window's copy ahead of
+                               // the image's on the copy engine)
 };
 
 // Runs `steps` protocol steps; per step the solve's LM iterations and device solve time into
@@ -110,11 +113,15 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
     for (int32_t k = 0; k < steps; ++k) {
         const rsvio_protocol_frame& f = P->frames[(P->first_phase + k) % P->n_phases];
         const rsvio_protocol_window& w = P->windows[(P->first_window + k) % P->n_windows];
-        if (hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
+        if (P->order == 0 &&
+            hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
             return RSVIO_ERR_HIP;
         int rc = A.set_problem(P->ba, w.n_kf, w.pose7, w.kf_fixed, w.n_lm, w.p_W, w.n_obs, w.obs_lm, w.obs_kf,
                                w.obs_cam, w.obs_uv, w.T_C_B2);
         if (rc) return rc;
+        if (P->order == 1 &&
+            hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
+            return RSVIO_ERR_HIP;
         if ((rc = A.run_async(P->ba, P->cfg))) return rc;
         if (P->lk_events && (P->first_step + k) % 4 == 0 && n_lk < P->n_lk_events) {
             // the frame enqueued directly, the LK launch between two timing events
@@ -157,7 +164,7 @@ int rsvio_protocol_layout(int64_t* out, int32_t n) {
                          (int64_t)offsetof(rsvio_protocol_window, T_C_B2), (int64_t)offsetof(rsvio_protocol_frame, batches),
                          (int64_t)offsetof(rsvio_protocol, first_step), (int64_t)offsetof(rsvio_protocol, lk_events),
                          (int64_t)offsetof(rsvio_protocol, n_lk_events), (int64_t)offsetof(rsvio_protocol, thresh),
-                         (int64_t)offsetof(rsvio_protocol, valid_bytes)};
+                         (int64_t)offsetof(rsvio_protocol, valid_bytes), (int64_t)offsetof(rsvio_protocol, order)};
     const int32_t m = (int32_t)(sizeof v / sizeof v[0]);
     for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
     return m;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6, call 13: (a) the observation pass over helper threads, A/B (RSVIO_BA_HOST_THREADS 0 / 3);
 # (b) set_problem's host phases both ways; (c) the CU split with the native driver (56 vs 64 tracker
-# CUs); (d) a host + device timeline of the protocol step (rocprofv3 hip + kernel + copy traces)
+# CUs); (e) window-first order vs split; (d) a host + device timeline of the protocol step (rocprofv3 hip + kernel + copy traces)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -20,6 +20,12 @@ for rep in 1 2; do
   for cs in 0.25 0.21875; do
     timeout -k 10 240 $B --cu-split $cs > gpurun_out/r06m_cs${cs}_$rep.json 2> gpurun_out/r06m_cs${cs}_$rep.err || { tail -20 gpurun_out/r06m_cs${cs}_$rep.err; exit 1; }
     show gpurun_out/r06m_cs${cs}_$rep.json "split $cs"
+  done
+done
+for rep in 1 2; do
+  for o in split window-first; do
+    timeout -k 10 240 $B --order $o > gpurun_out/r06n_o${o}_$rep.json 2> gpurun_out/r06n_o${o}_$rep.err || { tail -20 gpurun_out/r06n_o${o}_$rep.err; exit 1; }
+    show gpurun_out/r06n_o${o}_$rep.json "order $o"
   done
 done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
