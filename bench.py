@@ -1184,7 +1184,7 @@ class NativeProtocol:
                     ("d_out", ctypes.c_void_p), ("h_out", ctypes.c_void_p), ("out_bytes", ctypes.c_size_t),
                     ("d_valid", ctypes.c_void_p), ("h_valid", ctypes.c_void_p), ("valid_bytes", ctypes.c_size_t),
                     ("first_step", ctypes.c_int32), ("lk_events", ctypes.c_void_p), ("n_lk_events", ctypes.c_int32),
-                    ("order", ctypes.c_int32)]
+                    ("order", ctypes.c_int32), ("phase_us", ctypes.c_void_p)]
 
     def __init__(self, trk: "TrackerWorkload", ba: "BAWorkload", state_out, max_steps: int, order: int = 0):
         from rsvio import _lib
@@ -1232,6 +1232,7 @@ class NativeProtocol:
         self.trk, self.ba, self.state_out = trk, ba, state_out
         self.n_ev = n_ev
         self.order = order
+        self.phases = None  # a list: each run appends its steps' 7 host phase times (us)
 
     def run(self, steps: int):
         """`steps` protocol steps from the workloads' current phase and window; advances them."""
@@ -1244,7 +1245,9 @@ class NativeProtocol:
                            trk.ctx.value, MAX_IT, THRESH,
                            trk.out.data_ptr(), trk.h_out.data_ptr(), trk.out.numel() * 4,
                            trk.valid.data_ptr(), trk.h_valid.data_ptr(), trk.valid.numel(),
-                           trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev, self.order)
+                           trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev, self.order, None)
+        ph = (ctypes.c_double * (7 * steps))() if self.phases is not None else None
+        setup.phase_us = ctypes.addressof(ph) if ph is not None else None
         iters = (ctypes.c_int32 * steps)()
         sms = (ctypes.c_double * steps)()
         sec, npair = ctypes.c_double(0.0), ctypes.c_int32(0)
@@ -1252,6 +1255,8 @@ class NativeProtocol:
                                          ctypes.byref(npair))
         if rc:
             raise RuntimeError(f"rsvio_protocol_run failed: {rc}")
+        if ph is not None:
+            self.phases += [list(ph[7 * i:7 * i + 7]) for i in range(steps)]
         trk.k += steps
         trk.slot ^= steps & 1
         ba.k += steps
@@ -1501,10 +1506,12 @@ def main():
     if args.precapture_graphs:
         trk.precapture(True, args.order in ("split", "window-first"))
     native = None
-    if args.driver == "native" and args.order in ("split", "window-first") and not args.trace_steps:
+    if args.driver == "native" and args.order in ("split", "window-first"):
         native = NativeProtocol(trk, ba, state_out, max(args.steps, args.warmup, 2),
                                 order=1 if args.order == "window-first" else 0)
         native.run(max(args.warmup, 2))
+        if trace is not None:
+            native.phases = []
     else:
         for _ in range(max(args.warmup, 2)):
             protocol_step(False)
@@ -1527,7 +1534,15 @@ def main():
             ba.solve_ms += sms
             lk_pro += lk
     minflt = _minor_faults() - minflt0
-    if trace is not None:
+    if native is not None and native.phases is not None:  # the native driver's own host phase times
+        names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
+        ph = np.array(native.phases)
+        with open(args.trace_steps, "w") as f:
+            json.dump({"driver": "native", "phases": names, "steps_per_rep": args.steps,
+                       "median_us": [round(float(x), 2) for x in np.median(ph, axis=0)],
+                       "p90_us": [round(float(x), 2) for x in np.percentile(ph, 90, axis=0)],
+                       "us": [[round(float(x), 1) for x in r] for r in ph]}, f)
+    elif trace is not None:
         names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
         with open(args.trace_steps, "w") as f:
             json.dump({"phases": names, "steps_per_rep": args.steps,

@@ -94,6 +94,9 @@ struct rsvio_protocol {
     int32_t order;             // 0: split (image upload, window, solve start, frame); 1: window first
                                // (window, image upload, solve start, frame: the window's copy ahead of
                                // the image's on the copy engine)
+    double* phase_us;          // null, or 7 host phase times per step (us): image upload, set_problem,
+                               // run_async, frame enqueue, frame wait, rsvio_ba_wait, get_state (order
+                               // 1 counts the image upload after set_problem into its first entry)
 };
 
 // Runs `steps` protocol steps; per step the solve's LM iterations and device solve time into
@@ -109,20 +112,36 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
     const hipStream_t ts = static_cast<hipStream_t>(P->trk_stream);
     const hipEvent_t done = static_cast<hipEvent_t>(P->done_event);
     int32_t n_lk = 0;
-    const auto t0 = std::chrono::steady_clock::now();
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    clk::time_point tp[8];
+    double* ph = P->phase_us;
+    auto mark = [&](int i) {
+        if (ph) tp[i] = clk::now();
+    };
     for (int32_t k = 0; k < steps; ++k) {
+        mark(0);
         const rsvio_protocol_frame& f = P->frames[(P->first_phase + k) % P->n_phases];
         const rsvio_protocol_window& w = P->windows[(P->first_window + k) % P->n_windows];
         if (P->order == 0 &&
             hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
             return RSVIO_ERR_HIP;
+        mark(1);
         int rc = A.set_problem(P->ba, w.n_kf, w.pose7, w.kf_fixed, w.n_lm, w.p_W, w.n_obs, w.obs_lm, w.obs_kf,
                                w.obs_cam, w.obs_uv, w.T_C_B2);
         if (rc) return rc;
-        if (P->order == 1 &&
-            hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
-            return RSVIO_ERR_HIP;
+        mark(2);
+        if (P->order == 1) {
+            if (hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
+                return RSVIO_ERR_HIP;
+            if (ph) {  // (the image upload's time goes to the first phase)
+                const auto t = clk::now();
+                tp[1] += t - tp[2];
+                tp[2] = t;
+            }
+        }
         if ((rc = A.run_async(P->ba, P->cfg))) return rc;
+        mark(3);
         if (P->lk_events && (P->first_step + k) % 4 == 0 && n_lk < P->n_lk_events) {
             // the frame enqueued directly, the LK launch between two timing events
             if ((rc = A.build_pyramids_d(P->track_ctx, static_cast<const uint8_t*>(f.upload_dst), 2, f.pyr_dst, ts)))
@@ -139,16 +158,24 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
             return RSVIO_ERR_HIP;
         }
         if (hipEventRecord(done, ts) != hipSuccess) return RSVIO_ERR_HIP;
+        mark(4);
         hipError_t q;
         while ((q = hipEventQuery(done)) == hipErrorNotReady) {
         }
         if (q != hipSuccess) return RSVIO_ERR_HIP;
+        mark(5);
         rsvio_ba_result r{};
         if ((rc = A.wait(P->ba, &r))) return rc;
+        mark(6);
         if (r.status <= 0) return -100 - r.status;
         if (iters_out) iters_out[k] = r.iterations;
         if (solve_ms_out) solve_ms_out[k] = r.solve_ms;
         if ((rc = A.get_state(P->ba, P->pose_out, P->pw_out))) return rc;
+        if (ph) {
+            tp[7] = clk::now();
+            for (int i = 0; i < 7; ++i)
+                ph[7 * k + i] = std::chrono::duration<double, std::micro>(tp[i + 1] - tp[i]).count();
+        }
     }
     if (seconds_out)
         *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -164,7 +191,7 @@ int rsvio_protocol_layout(int64_t* out, int32_t n) {
                          (int64_t)offsetof(rsvio_protocol_window, T_C_B2), (int64_t)offsetof(rsvio_protocol_frame, batches),
                          (int64_t)offsetof(rsvio_protocol, first_step), (int64_t)offsetof(rsvio_protocol, lk_events),
                          (int64_t)offsetof(rsvio_protocol, n_lk_events), (int64_t)offsetof(rsvio_protocol, thresh),
-                         (int64_t)offsetof(rsvio_protocol, valid_bytes), (int64_t)offsetof(rsvio_protocol, order)};
+                         (int64_t)offsetof(rsvio_protocol, valid_bytes), (int64_t)offsetof(rsvio_protocol, order), (int64_t)offsetof(rsvio_protocol, phase_us)};
     const int32_t m = (int32_t)(sizeof v / sizeof v[0]);
     for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
     return m;
