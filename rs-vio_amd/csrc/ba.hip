@@ -35,6 +35,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <sys/resource.h>
 #include <numeric>
 #include <stdexcept>
 #include <vector>
@@ -745,6 +747,28 @@ __device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSr
 
 // set_problem's device part in one launch: blocks [0, nb_slots) build the slot layout, the next
 // n_chunk blocks the Schur pair lists
+// set_problem's staging image into the device arena, on the BA's own stream: this kernel reads the
+// pinned image over PCIe (8-B system-scope loads: each goes to host memory, nothing stale from an
+// earlier window can be served by a cache) instead of an SDMA copy, so ba_build_layout follows it
+// in the same queue without the copy engine -> compute queue hand-off (≈ 12 µs between the copy's
+// end and the next kernel's start in the traced step, profiles/r06n_traced_step_timeline.txt).
+constexpr int kStageWords = 2;  // 8-B words per thread (all loads in flight before the stores)
+__global__ __launch_bounds__(256) void ba_stage_in(const unsigned long long* src, unsigned long long* __restrict__ dst,
+                                                   int n_words) {
+    const int t = (int)(blockIdx.x * 256 + threadIdx.x), st = (int)(gridDim.x * 256);
+    unsigned long long v[kStageWords];
+#pragma unroll
+    for (int k = 0; k < kStageWords; ++k) {
+        const int i = t + k * st;
+        v[k] = i < n_words ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kStageWords; ++k) {
+        const int i = t + k * st;
+        if (i < n_words) dst[i] = v[k];
+    }
+}
+
 __global__ __launch_bounds__(256) void ba_build_layout(Geometry G, Prob Pr, SlotSrc S, int nb_slots, int4* hdr,
                                                        double2* huv, int4* pairs) {
     const int b = blockIdx.x;
@@ -4250,11 +4274,15 @@ struct BundleAdjuster {
         size_t hdr, uv, pairs, total;  // built on the device
     } lay{};
     bool prof_env = false;      // RSVIO_BA_PROFILE: host phase times of set_problem on stderr
+    bool prof_slow = false;     // RSVIO_BA_PROFILE=slow: only the slow calls, with the mappings added since
+    std::string prof_maps;      // (the last /proc/self/maps of a slow-call report)
     bool uv_env = true;         // RSVIO_BA_UV32=0: always upload (u, v) as f64 (A/B)
     // RSVIO_BA_EARLY_COPY=1: the observation section's copy issued as soon as the pass fills it
     // (rounds 3-5); default one copy at the end: set_problem 61 -> 56 us of host time alone
     // (profiles/r06g_setprob.txt), the step no slower (profiles/r06h_early_copy_ab.txt)
     bool early_env = false;
+    bool stage_kernel = true;   // RSVIO_BA_STAGE=sdma: the staging image by hipMemcpyAsync (A/B)
+    const unsigned long long* h_arena_dev = nullptr;  // the staging image's device address
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
     // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
@@ -4328,11 +4356,16 @@ struct BundleAdjuster {
         tick_wait = !(wv && std::strcmp(wv, "sync") == 0);
         const char* ge = std::getenv("RSVIO_BA_GRAPHS");  // "0": direct launches (A/B switch)
         graphs_ok = !(ge && ge[0] == '0');
-        prof_env = std::getenv("RSVIO_BA_PROFILE") != nullptr;
+        const char* pv = std::getenv("RSVIO_BA_PROFILE");
+        prof_env = pv != nullptr;
+        prof_slow = pv && std::strcmp(pv, "slow") == 0;
         const char* u32v = std::getenv("RSVIO_BA_UV32");
         uv_env = !(u32v && u32v[0] == '0');
         const char* ecv = std::getenv("RSVIO_BA_EARLY_COPY");
         early_env = ecv && ecv[0] == '1';
+        const char* stv = std::getenv("RSVIO_BA_STAGE");
+        stage_kernel = !(stv && std::strcmp(stv, "sdma") == 0);
+        if (stage_kernel) early_env = false;
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
@@ -4445,12 +4478,22 @@ struct BundleAdjuster {
         const bool prof = prof_env;
         auto tp0 = std::chrono::steady_clock::now();
         double tms[12];
+        long flt[12];
         int ntm = 0;
+        auto faults = [] {
+            struct rusage ru;
+            getrusage(RUSAGE_THREAD, &ru);
+            return (long)ru.ru_minflt;
+        };
+        long f0 = prof ? faults() : 0;
         auto mark = [&] {
             if (!prof) return;
             const auto t = std::chrono::steady_clock::now();
-            tms[ntm++] = std::chrono::duration<double, std::micro>(t - tp0).count();
+            const long f = faults();
+            tms[ntm] = std::chrono::duration<double, std::micro>(t - tp0).count();
+            flt[ntm++] = f - f0;
             tp0 = t;
+            f0 = f;
         };
         // no stream synchronisation: the staging image is guarded by ev_up, the device buffers by
         // stream order (a buffer that grows is freed by hipFree, which waits for the device), and
@@ -4514,7 +4557,12 @@ struct BundleAdjuster {
             }
             up_pending = false;
         }
-        if (h_arena.n < L.upload) h_arena.alloc(L.upload + L.upload / 4);
+        if (h_arena.n < L.upload) {
+            h_arena.alloc(L.upload + L.upload / 4, hipHostMallocCoherent);
+            void* dp = nullptr;
+            RSVIO_HIP(hipHostGetDevicePointer(&dp, h_arena.p, 0));
+            h_arena_dev = static_cast<const unsigned long long*>(dp);
+        }
         uint8_t* hb = h_arena.p;
         mark();
         // observations: validated, a (keyframe, camera) bit per landmark, packed keys
@@ -4620,8 +4668,9 @@ struct BundleAdjuster {
         L.total = off;
         if (d_arena.n < L.total) {  // the observation copy above went to the old arena: redo it
             d_arena.alloc(L.total + L.total / 4);
-            RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice,
-                                     stream));
+            if (early_env)
+                RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice,
+                                         stream));
         }
         lay = L;
         std::memcpy(hb + L.pose_init, pose7, sizeof(double) * 7 * (size_t)n_kf);
@@ -4647,7 +4696,14 @@ struct BundleAdjuster {
         fill_desc(hdesc);
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
-        RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));
+        if (stage_kernel) {
+            const int nw = (int)(L.upload / 8);  // (L.upload is a multiple of 256)
+            hipLaunchKernelGGL(ba_stage_in, dim3((nw + 256 * kStageWords - 1) / (256 * kStageWords)), dim3(256), 0,
+                               stream, h_arena_dev, reinterpret_cast<unsigned long long*>(d_arena.p), nw);
+            RSVIO_HIP(hipGetLastError());
+        } else {
+            RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));
+        }
         RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
         {
@@ -4672,10 +4728,42 @@ struct BundleAdjuster {
         state_fresh = true;
         has_problem = true;
         mark();
-        if (prof)
-            fprintf(stderr, "[rsvio] set_problem us: checks+layout %.1f upload wait %.1f observations %.1f waves %.1f "
-                    "tables %.1f enqueue %.1f grow %.1f (upload %zu B, arena %zu B)\n",
-                    tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], tms[6], L.upload, L.total);
+        if (prof) {
+            double tot = 0.0;
+            long ftot = 0;
+            for (int i = 0; i < ntm; ++i) tot += tms[i], ftot += flt[i];
+            if (!prof_slow || tot > 1000.0 || ftot > 100)
+                fprintf(stderr, "[rsvio] set_problem us: checks+layout %.1f upload wait %.1f observations %.1f waves %.1f "
+                        "tables %.1f enqueue %.1f grow %.1f (upload %zu B, arena %zu B); minor faults %ld %ld %ld %ld "
+                        "%ld %ld %ld\n",
+                        tms[0], tms[1], tms[2], tms[3], tms[4], tms[5], tms[6], L.upload, L.total, flt[0], flt[1],
+                        flt[2], flt[3], flt[4], flt[5], flt[6]);
+            if (prof_slow && (tot > 1000.0 || ftot > 100)) {  // what the process mapped since the last report
+                std::string maps;
+                if (FILE* fm = std::fopen("/proc/self/maps", "r")) {
+                    char buf[4096];
+                    size_t n;
+                    while ((n = std::fread(buf, 1, sizeof buf, fm)) > 0) maps.append(buf, n);
+                    std::fclose(fm);
+                }
+                std::vector<std::string> now, was;
+                auto split = [](const std::string& t, std::vector<std::string>& out) {
+                    size_t a = 0;
+                    while (a < t.size()) {
+                        size_t b = t.find('\n', a);
+                        if (b == std::string::npos) b = t.size();
+                        out.emplace_back(t, a, b - a);
+                        a = b + 1;
+                    }
+                };
+                split(maps, now);
+                split(prof_maps, was);
+                std::sort(was.begin(), was.end());
+                for (const auto& l : now)
+                    if (!std::binary_search(was.begin(), was.end(), l)) fprintf(stderr, "[rsvio]   new map: %s\n", l.c_str());
+                prof_maps.swap(maps);
+            }
+        }
     }
 
     void allreduce(double* buf, size_t n) {

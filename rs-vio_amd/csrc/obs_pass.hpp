@@ -288,12 +288,15 @@ struct ObsJob {
 };
 
 // The pool shared by every handle of the process (created on first use): RSVIO_BA_HOST_THREADS
-// helpers (default 3; 0 disables), spinning RSVIO_BA_HOST_SPIN_US (default 2000) before parking.
+// helpers (default 0: off -- on the MI355X box's host the pass did not get shorter with 3 helpers,
+// 17.5 vs 14.7-20.7 us, the window's arrays being in the calling core's cache and the helpers'
+// spinning costing CPU time, profiles/r06n_host_pool_cu_order_ab.txt), spinning
+// RSVIO_BA_HOST_SPIN_US (default 2000) before parking.
 static HostPool* shared_pool() {
     static HostPool* pool = [] {
         const char* tv = std::getenv("RSVIO_BA_HOST_THREADS");
         const char* sv = std::getenv("RSVIO_BA_HOST_SPIN_US");
-        const int nt = tv ? std::max(0, std::min(15, std::atoi(tv))) : 3;
+        const int nt = tv ? std::max(0, std::min(15, std::atoi(tv))) : 0;
         const int sp = sv ? std::max(0, std::atoi(sv)) : 2000;
         return nt > 0 ? new HostPool(nt, sp) : nullptr;  // (lives to the process's end)
     }();

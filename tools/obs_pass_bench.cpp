@@ -1,5 +1,5 @@
 // CPU micro-benchmark + equality check of set_problem's observation pass (obs_pass.hpp): the
-// single-threaded pass vs the chunked one over the helper pool, on a config-3-shaped window
+// single-threaded pass vs the chunked one over the helper pool (RSVIO_BA_HOST_THREADS, default 0: set it), on a config-3-shaped window
 // (2,000 landmarks x 12 observations, landmark-major, (u, v) exact f32 values).
 //   g++ -O2 -std=c++17 -pthread -I rs-vio_amd/csrc tools/obs_pass_bench.cpp -o /tmp/obs_pass_bench
 #include <chrono>

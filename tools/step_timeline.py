@@ -21,9 +21,11 @@ import sys
 
 
 def rows(d, suffix):
+    import gzip
     out = []
-    for p in glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True):
-        out += list(csv.DictReader(open(p)))
+    for p in glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True) + \
+            glob.glob(os.path.join(d, "**", f"*{suffix}.gz"), recursive=True):
+        out += list(csv.DictReader(gzip.open(p, "rt") if p.endswith(".gz") else open(p)))
     return out
 
 
@@ -58,8 +60,15 @@ def main(d):
         a, b = t0s[i], t0s[i + 1]
         if b - a > 2_000_000:  # a rep boundary (host work between reps), not one step
             continue
-        h = [(r["Function"], int(r["Start_Timestamp"]) - a, int(r["End_Timestamp"]) - a)
-             for r in main_api if a <= int(r["Start_Timestamp"]) < b]
+        h = []
+        for r in main_api:  # (a run of one call -- the event polls -- is one entry: first start, last end)
+            if not a <= int(r["Start_Timestamp"]) < b:
+                continue
+            s0, e0 = int(r["Start_Timestamp"]) - a, int(r["End_Timestamp"]) - a
+            if h and h[-1][0] == r["Function"] and r["Function"] in ("hipEventQuery", "hipStreamQuery"):
+                h[-1] = (h[-1][0], h[-1][1], e0)
+            else:
+                h.append((r["Function"], s0, e0))
         dv = [(n, s - a, e - a) for n, s, e in dev if a <= s < b]
         steps.append((tuple(x[0] for x in h), h, dv, b - a))
     sig = collections.Counter(s[0] for s in steps).most_common(1)[0][0]
