@@ -725,6 +725,8 @@ def cu_partition(device: int, frac: float, layout: str):
 class TrackerWorkload:
     """Config 2 on device: per-frame pyramids (left, right) + 3 track_points batches."""
 
+    upload_kernel = False  # bench.py --upload: the pcie image upload by rsvio_upload_async
+
     def __init__(self, device: int, stream_ptr=None):
         import ctypes as C
 
@@ -838,7 +840,11 @@ class TrackerWorkload:
         """The next frame's two images up from pinned host memory (the first part of a pcie step:
         issued as soon as the frame is there; step(..., uploaded=True) enqueues the rest)."""
         plan = self._plan(self.k % len(self.seq), True)
-        self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, self.stream.cuda_stream))
+        if self.upload_kernel:  # a kernel on the tracker stream reads the pinned images (no copy engine)
+            self.L.check(self.lib.rsvio_upload_async(plan["src"], plan["h_img"], plan["img_bytes"],
+                                                     self.stream.cuda_stream))
+        else:
+            self.L.check(self._memcpy(plan["src"], plan["h_img"], plan["img_bytes"], 1, self.stream.cuda_stream))
 
     def step(self, timed: bool, pcie: bool = False, wait: bool = True, uploaded: bool = False):
         """Frame t -> t': 2 pyramids of t', then cam0 / cam1 temporal + stereo batches.  pcie:
@@ -1171,7 +1177,7 @@ class NativeProtocol:
 
     class Api(ctypes.Structure):
         _fields_ = [(n, ctypes.c_void_p) for n in ("set_problem", "run_async", "wait", "get_state",
-                                                   "build_pyramids_d", "track_points_d")]
+                                                   "build_pyramids_d", "track_points_d", "upload")]
 
     class Setup(ctypes.Structure):
         _fields_ = [("api", ctypes.c_void_p), ("ba", ctypes.c_void_p), ("cfg", ctypes.c_void_p),
@@ -1197,7 +1203,8 @@ class NativeProtocol:
                                                 ctypes.c_void_p, ctypes.c_void_p]
         fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
         self.api = self.Api(fp(lib.rsvio_ba_set_problem), fp(lib.rsvio_ba_run_async), fp(lib.rsvio_ba_wait),
-                            fp(lib.rsvio_ba_get_state), fp(lib.rsvio_build_pyramids_d), fp(lib.rsvio_track_points_d))
+                            fp(lib.rsvio_ba_get_state), fp(lib.rsvio_build_pyramids_d), fp(lib.rsvio_track_points_d),
+                            fp(lib.rsvio_upload_async) if trk.upload_kernel else None)
         self.keep = []
         wins = (self.Window * len(ba.windows))()
         for i, w in enumerate(ba.windows):
@@ -1358,6 +1365,10 @@ def main():
                          "enqueue); both paths run concurrently either way (the tracker does not depend on the solve); "
                          "window-first: the window's upload, then the image upload, then the solve start and the "
                          "frame (the window's copy ahead of the image's)")
+    ap.add_argument("--upload", default="kernel", choices=["kernel", "sdma"],
+                    help="the protocol step's image upload: kernel (default, rsvio_upload_async: a kernel on the "
+                         "tracker stream reads the pinned images, so the pyramids follow it without a copy-engine "
+                         "hand-off) or sdma (hipMemcpyAsync)")
     ap.add_argument("--tracker-graphs", type=int, default=1,
                     help="1: the frame's copies + pyramid + LK launches replayed as one captured HIP graph per "
                          "frame phase (one hipGraphLaunch instead of up to five enqueue calls); 0: direct enqueue")
@@ -1412,6 +1423,7 @@ def main():
         log(f"[bench] CU partition ({args.cu_layout}): tracker {len(cu_trk)} CUs, BA {len(cu_ba)} CUs")
     trk = TrackerWorkload(local, streams[0].ptr if streams else None)
     trk.graphs = bool(args.tracker_graphs)
+    trk.upload_kernel = args.upload == "kernel"
     ba = BAWorkload(local, world, rank, streams[1].ptr if streams else None, args.collective,
                     rccl_ok=not args.same_device)
 

@@ -50,6 +50,11 @@ int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus);
  * CUs (hipExtStreamCreateWithCUMask).  No reference counterpart (the reference is CPU-only). */
 int rsvio_stream_create(int32_t device, const uint32_t* cu_mask, uint32_t mask_words, void** out);
 int rsvio_stream_destroy(void* stream);
+/* Host-to-device copy of page-locked host memory (hipHostMalloc / hipHostRegister) by a kernel on
+ * `stream` instead of a copy engine: the next kernel on the stream starts without the copy-engine ->
+ * compute-queue hand-off (how bench.py's protocol step uploads the frame's images).  A pageable or
+ * non-8-byte-aligned source or destination takes hipMemcpyAsync.  No reference counterpart. */
+int rsvio_upload_async(void* d_dst, const void* h_src, size_t bytes, void* stream);
 
 /* =============================== HP-T: patch tracker =============================== */
 

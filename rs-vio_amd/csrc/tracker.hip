@@ -526,6 +526,59 @@ int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus) {
     });
 }
 
+namespace {
+// rsvio_upload_async's copy: 8-B system-scope loads of the page-locked source (each one a PCIe read
+// of host memory, nothing served stale from a cache), all of a thread's loads in flight before its
+// stores; the tail bytes by the first thread
+constexpr int kUpWords = 2;
+__global__ __launch_bounds__(256) void upload_words_kernel(const unsigned long long* src,
+                                                           unsigned long long* __restrict__ dst, long long n_words,
+                                                           const unsigned char* src_tail,
+                                                           unsigned char* __restrict__ dst_tail, int n_tail) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x, st = (long long)gridDim.x * 256;
+    unsigned long long v[kUpWords];
+#pragma unroll
+    for (int k = 0; k < kUpWords; ++k) {
+        const long long i = t + k * st;
+        v[k] = i < n_words ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kUpWords; ++k) {
+        const long long i = t + k * st;
+        if (i < n_words) dst[i] = v[k];
+    }
+    if (t == 0)
+        for (int i = 0; i < n_tail; ++i)
+            dst_tail[i] = __hip_atomic_load(src_tail + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+int rsvio_upload_async(void* d_dst, const void* h_src, size_t bytes, void* stream) {
+    if ((!d_dst || !h_src) && bytes) return RSVIO_ERR_INVALID_ARG;
+    return guarded([&] {
+        if (!bytes) return (int)RSVIO_OK;
+        const hipStream_t s = static_cast<hipStream_t>(stream);
+        void* dp = nullptr;
+        const bool pinned = hipHostGetDevicePointer(&dp, const_cast<void*>(h_src), 0) == hipSuccess && dp;
+        if (!pinned || ((reinterpret_cast<uintptr_t>(dp) | reinterpret_cast<uintptr_t>(d_dst)) & 7)) {
+            (void)hipGetLastError();  // (not page-locked, or unaligned: the runtime's copy)
+            RSVIO_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, s));
+            return (int)RSVIO_OK;
+        }
+        const long long nw = (long long)(bytes / 8);
+        const int tail = (int)(bytes % 8);
+        const long long per = 256LL * kUpWords;
+        const unsigned grid = (unsigned)std::max<long long>(1, (nw + per - 1) / per);
+        auto* src8 = static_cast<const unsigned long long*>(dp);
+        auto* dst8 = static_cast<unsigned long long*>(d_dst);
+        hipLaunchKernelGGL(upload_words_kernel, dim3(grid), dim3(256), 0, s, src8, dst8, nw,
+                           reinterpret_cast<const unsigned char*>(src8 + nw), reinterpret_cast<unsigned char*>(dst8 + nw),
+                           tail);
+        RSVIO_HIP(hipGetLastError());
+        return (int)RSVIO_OK;
+    });
+}
+
 int rsvio_stream_create(int32_t device, const uint32_t* cu_mask, uint32_t mask_words, void** out) {
     if (!out || (cu_mask && mask_words == 0)) return RSVIO_ERR_INVALID_ARG;
     return guarded([&] {

@@ -9,7 +9,8 @@
 // is device work of its own, and nothing of the step is skipped:
 //
 //   per step k (split order, bench.py protocol_step; order 1 swaps steps 1 and 2):
-//     1. the next frame's two images up from pinned host memory (hipMemcpyAsync, tracker stream);
+//     1. the next frame's two images up from pinned host memory (rsvio_upload_async: a kernel on the
+//        tracker stream reads them over PCIe; or hipMemcpyAsync when the api's upload is null);
 //     2. a NEW keyframe window: rsvio_ba_set_problem (two pre-built windows alternate);
 //     3. rsvio_ba_run_async (the solve's captured graph);
 //     4. the frame's captured tracker graph (pyramids, LK, the feature lists down) + an event --
@@ -62,6 +63,7 @@ struct rsvio_protocol_api {  // the product library's entry points (its C ABI)
     decltype(&rsvio_ba_get_state) get_state;
     decltype(&rsvio_build_pyramids_d) build_pyramids_d;
     decltype(&rsvio_track_points_d) track_points_d;
+    decltype(&rsvio_upload_async) upload;  // null: the image upload by hipMemcpyAsync (copy engine)
 };
 
 struct rsvio_protocol {
@@ -123,17 +125,20 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
         mark(0);
         const rsvio_protocol_frame& f = P->frames[(P->first_phase + k) % P->n_phases];
         const rsvio_protocol_window& w = P->windows[(P->first_window + k) % P->n_windows];
-        if (P->order == 0 &&
-            hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
-            return RSVIO_ERR_HIP;
+        auto up = [&]() -> int {
+            if (A.upload) return A.upload(f.upload_dst, f.upload_src, f.upload_bytes, P->trk_stream);
+            return hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) == hipSuccess
+                       ? 0
+                       : RSVIO_ERR_HIP;
+        };
+        if (P->order == 0 && up()) return RSVIO_ERR_HIP;
         mark(1);
         int rc = A.set_problem(P->ba, w.n_kf, w.pose7, w.kf_fixed, w.n_lm, w.p_W, w.n_obs, w.obs_lm, w.obs_kf,
                                w.obs_cam, w.obs_uv, w.T_C_B2);
         if (rc) return rc;
         mark(2);
         if (P->order == 1) {
-            if (hipMemcpyAsync(f.upload_dst, f.upload_src, f.upload_bytes, hipMemcpyHostToDevice, ts) != hipSuccess)
-                return RSVIO_ERR_HIP;
+            if (up()) return RSVIO_ERR_HIP;
             if (ph) {  // (the image upload's time goes to the first phase)
                 const auto t = clk::now();
                 tp[1] += t - tp[2];

@@ -153,6 +153,7 @@ SIG = {
     "rsvio_ba_p2p_level": (C.c_int, [P, C.POINTER(C.c_int32)]),
     "rsvio_stream_create": (C.c_int, [C.c_int32, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(P)]),
     "rsvio_stream_destroy": (C.c_int, [P]),
+    "rsvio_upload_async": (C.c_int, [P, P, C.c_size_t, P]),
     "rsvio_ba_wait": (C.c_int, [P, C.POINTER(BaResult)]),
     "rsvio_ba_get_state": (C.c_int, [P, P, P]),
     "rsvio_ba_build_system": (C.c_int, [P, C.c_double, C.c_double, P, P, C.POINTER(C.c_double)]),
