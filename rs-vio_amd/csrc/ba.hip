@@ -745,8 +745,6 @@ __device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSr
     for (int i = total + tid; i < G.pair_stride; i += 256) out[i] = make_int4(-1, 0, 0, 0);
 }
 
-// set_problem's device part in one launch: blocks [0, nb_slots) build the slot layout, the next
-// n_chunk blocks the Schur pair lists
 // set_problem's staging image into the device arena, on the BA's own stream: this kernel reads the
 // pinned image over PCIe (8-B system-scope loads: each goes to host memory, nothing stale from an
 // earlier window can be served by a cache) instead of an SDMA copy, so ba_build_layout follows it
@@ -769,6 +767,8 @@ __global__ __launch_bounds__(256) void ba_stage_in(const unsigned long long* src
     }
 }
 
+// set_problem's device part in one launch: blocks [0, nb_slots) build the slot layout, the next
+// n_chunk blocks the Schur pair lists
 __global__ __launch_bounds__(256) void ba_build_layout(Geometry G, Prob Pr, SlotSrc S, int nb_slots, int4* hdr,
                                                        double2* huv, int4* pairs) {
     const int b = blockIdx.x;
