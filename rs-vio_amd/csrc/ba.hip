@@ -4263,11 +4263,13 @@ struct BundleAdjuster {
     DevBuf<double> d_pose2, d_pw2;
     // The static problem (initial state, keyframe map, slot headers + observations, Schur pair
     // lists, camera-block table) lives in one device arena, filled in one pinned staging image
-    // and uploaded by ONE asynchronous copy (ev_up marks its completion before the staging
-    // image is refilled).  Offsets in bytes, 256-B aligned.
+    // and uploaded by ONE asynchronous copy (ba_stage_in, or hipMemcpyAsync under
+    // RSVIO_BA_STAGE=sdma).  The staging image may be refilled once the copy has read it: a solve
+    // waited for since (its ticket comes after the copy in stream order) or a settled stream
+    // proves that; otherwise the next set_problem synchronises the stream (up_pending) -- no event
+    // per upload on the step's critical path.  Offsets in bytes, 256-B aligned.
     DevBuf<uint8_t> d_arena;
     HostBuf<uint8_t> h_arena;
-    hipEvent_t ev_up = nullptr;
     bool up_pending = false;
     struct ArenaLayout {
         size_t desc, pose_init, pw_init, free_idx, pb_fa, pb_fb, dmap, mask, lm_base, wave_fill, wave_lm, key, ouv, upload;
@@ -4328,7 +4330,6 @@ struct BundleAdjuster {
         RSVIO_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         RSVIO_HIP(hipEventCreate(&ev0));
         RSVIO_HIP(hipEventCreate(&ev1));
-        RSVIO_HIP(hipEventCreateWithFlags(&ev_up, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&gv.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&gd.ev_launch, hipEventDisableTiming));
         RSVIO_HIP(hipEventCreateWithFlags(&ev_desc, hipEventDisableTiming));
@@ -4383,7 +4384,6 @@ struct BundleAdjuster {
         if (xbuf) (void)hipFree(xbuf);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
-        if (ev_up) (void)hipEventDestroy(ev_up);
         if (gv.ev_launch) (void)hipEventDestroy(gv.ev_launch);
         if (gd.ev_launch) (void)hipEventDestroy(gd.ev_launch);
         if (ev_desc) (void)hipEventDestroy(ev_desc);
@@ -4495,7 +4495,7 @@ struct BundleAdjuster {
             tp0 = t;
             f0 = f;
         };
-        // no stream synchronisation: the staging image is guarded by ev_up, the device buffers by
+        // no stream synchronisation: the staging image is guarded by up_pending, the device buffers by
         // stream order (a buffer that grows is freed by hipFree, which waits for the device), and
         // the previous solve's graph is retired until the stream is next settled
         if (pend.active) throw CallOrderError("set_problem: a solve is in flight (call rsvio_ba_wait first)");
@@ -4550,13 +4550,7 @@ struct BundleAdjuster {
         L.ouv = off;       off += al(sizeof(double2) * std::max(n_obs, 1));
         L.upload = off;
         mark();
-        if (up_pending) {  // the previous upload may still read the staging image
-            if (hipEventQuery(ev_up) != hipSuccess) {  // (a query costs less than a completed sync)
-                (void)hipGetLastError();
-                RSVIO_HIP(hipEventSynchronize(ev_up));
-            }
-            up_pending = false;
-        }
+        if (up_pending) settle();  // the previous upload may still read the staging image
         if (h_arena.n < L.upload) {
             h_arena.alloc(L.upload + L.upload / 4, hipHostMallocCoherent);
             void* dp = nullptr;
@@ -4704,7 +4698,6 @@ struct BundleAdjuster {
         } else {
             RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));
         }
-        RSVIO_HIP(hipEventRecord(ev_up, stream));
         up_pending = true;
         {
             SlotSrc S;
@@ -5087,6 +5080,7 @@ struct BundleAdjuster {
             if (h_state.p->done || pend.enq >= pend.max_it) break;
             enqueue_chunk(std::min(iter_chunk, pend.max_it - pend.enq));
         }
+        up_pending = false;  // (the ticket comes after the window's upload in stream order)
         last_iterations = h_state.p->iter;
         if (coll == 2) {  // the exchange error flag came with the ticket (K7); the sync path reads it
             if (by_tick) {
@@ -5316,6 +5310,7 @@ struct BundleAdjuster {
             RSVIO_HIP(hipStreamSynchronize(stream));
             settled = true;
         }
+        up_pending = false;
         destroy_retired();
     }
 
