@@ -750,21 +750,15 @@ __device__ void build_pairs_body(const Geometry& G, const Prob& Pr, const SlotSr
 // earlier window can be served by a cache) instead of an SDMA copy, so ba_build_layout follows it
 // in the same queue without the copy engine -> compute queue hand-off (≈ 12 µs between the copy's
 // end and the next kernel's start in the traced step, profiles/r06n_traced_step_timeline.txt).
-constexpr int kStageWords = 2;  // 8-B words per thread (all loads in flight before the stores)
-__global__ __launch_bounds__(256) void ba_stage_in(const unsigned long long* src, unsigned long long* __restrict__ dst,
-                                                   int n_words) {
+// 16-B words, two per thread (both loads in flight before the stores); the image is a multiple of
+// 256 B.  (8-B atomic loads: 10.5 us for the 386 KB window, profiles/r06r_headline_kstats.txt.)
+__global__ __launch_bounds__(256) void ba_stage_in(const uint4* src, uint4* __restrict__ dst, int n_words) {
     const int t = (int)(blockIdx.x * 256 + threadIdx.x), st = (int)(gridDim.x * 256);
-    unsigned long long v[kStageWords];
-#pragma unroll
-    for (int k = 0; k < kStageWords; ++k) {
-        const int i = t + k * st;
-        v[k] = i < n_words ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
-    }
-#pragma unroll
-    for (int k = 0; k < kStageWords; ++k) {
-        const int i = t + k * st;
-        if (i < n_words) dst[i] = v[k];
-    }
+    const int i0 = t, i1 = t + st;
+    uint4 a, b;
+    host_load2x16(src + min(i0, n_words - 1), src + min(i1, n_words - 1), a, b);
+    if (i0 < n_words) dst[i0] = a;
+    if (i1 < n_words) dst[i1] = b;
 }
 
 // set_problem's device part in one launch: blocks [0, nb_slots) build the slot layout, the next
@@ -4284,7 +4278,7 @@ struct BundleAdjuster {
     // (profiles/r06g_setprob.txt), the step no slower (profiles/r06h_early_copy_ab.txt)
     bool early_env = false;
     bool stage_kernel = true;   // RSVIO_BA_STAGE=sdma: the staging image by hipMemcpyAsync (A/B)
-    const unsigned long long* h_arena_dev = nullptr;  // the staging image's device address
+    const void* h_arena_dev = nullptr;  // the staging image's device address
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
     // export_on: the final decisions export it -- turned on by the first rsvio_ba_get_state, so a
@@ -4555,7 +4549,7 @@ struct BundleAdjuster {
             h_arena.alloc(L.upload + L.upload / 4, hipHostMallocCoherent);
             void* dp = nullptr;
             RSVIO_HIP(hipHostGetDevicePointer(&dp, h_arena.p, 0));
-            h_arena_dev = static_cast<const unsigned long long*>(dp);
+            h_arena_dev = dp;
         }
         uint8_t* hb = h_arena.p;
         mark();
@@ -4691,9 +4685,9 @@ struct BundleAdjuster {
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
         if (stage_kernel) {
-            const int nw = (int)(L.upload / 8);  // (L.upload is a multiple of 256)
-            hipLaunchKernelGGL(ba_stage_in, dim3((nw + 256 * kStageWords - 1) / (256 * kStageWords)), dim3(256), 0,
-                               stream, h_arena_dev, reinterpret_cast<unsigned long long*>(d_arena.p), nw);
+            const int nw = (int)(L.upload / 16);  // (L.upload is a multiple of 256)
+            hipLaunchKernelGGL(ba_stage_in, dim3((nw + 511) / 512), dim3(256), 0, stream,
+                               reinterpret_cast<const uint4*>(h_arena_dev), reinterpret_cast<uint4*>(d_arena.p), nw);
             RSVIO_HIP(hipGetLastError());
         } else {
             RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));

@@ -118,6 +118,19 @@ __device__ __forceinline__ uint32_t sat_u32(float v) {
 
 // Pyramid level geometry: level i = (w / 2^i) x (h / 2^i), packed back to back
 // (feature_tracker.rs:215-216).
+// Two 16-B loads of page-locked host memory at system scope (sc0 sc1: each request goes over PCIe
+// to host memory, nothing served from a GPU cache), both in flight, complete on return -- the
+// staging kernels' reads (ba_stage_in, rsvio_upload_async).  a and b must be 16-B aligned.
+__device__ __forceinline__ void host_load2x16(const void* a, const void* b, uint4& va, uint4& vb) {
+    __asm__ volatile(
+        "global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+        "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(va), "=&v"(vb)
+        : "v"(a), "v"(b)
+        : "memory");
+}
+
 __host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }
 __host__ __device__ inline uint32_t level_h(uint32_t h, int i) { return h / (1u << i); }
 __host__ __device__ inline size_t level_offset(uint32_t w, uint32_t h, int level) {

@@ -527,25 +527,19 @@ int rsvio_device_info(int device, char* name_out, size_t cap, int* n_cus) {
 }
 
 namespace {
-// rsvio_upload_async's copy: 8-B system-scope loads of the page-locked source (each one a PCIe read
-// of host memory, nothing served stale from a cache), all of a thread's loads in flight before its
-// stores; the tail bytes by the first thread
-constexpr int kUpWords = 2;
-__global__ __launch_bounds__(256) void upload_words_kernel(const unsigned long long* src,
-                                                           unsigned long long* __restrict__ dst, long long n_words,
+// rsvio_upload_async's copy: 16-B system-scope loads of the page-locked source (host_load2x16:
+// each a PCIe read of host memory, nothing served stale from a cache), two per thread in flight
+// before the stores; the tail bytes (< 16) by the first thread
+__global__ __launch_bounds__(256) void upload_words_kernel(const uint4* src, uint4* __restrict__ dst, long long n_words,
                                                            const unsigned char* src_tail,
                                                            unsigned char* __restrict__ dst_tail, int n_tail) {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x, st = (long long)gridDim.x * 256;
-    unsigned long long v[kUpWords];
-#pragma unroll
-    for (int k = 0; k < kUpWords; ++k) {
-        const long long i = t + k * st;
-        v[k] = i < n_words ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
-    }
-#pragma unroll
-    for (int k = 0; k < kUpWords; ++k) {
-        const long long i = t + k * st;
-        if (i < n_words) dst[i] = v[k];
+    const long long i0 = t, i1 = t + st;
+    if (n_words > 0) {
+        uint4 a, b;
+        rsvio::host_load2x16(src + min(i0, n_words - 1), src + min(i1, n_words - 1), a, b);
+        if (i0 < n_words) dst[i0] = a;
+        if (i1 < n_words) dst[i1] = b;
     }
     if (t == 0)
         for (int i = 0; i < n_tail; ++i)
@@ -560,20 +554,19 @@ int rsvio_upload_async(void* d_dst, const void* h_src, size_t bytes, void* strea
         const hipStream_t s = static_cast<hipStream_t>(stream);
         void* dp = nullptr;
         const bool pinned = hipHostGetDevicePointer(&dp, const_cast<void*>(h_src), 0) == hipSuccess && dp;
-        if (!pinned || ((reinterpret_cast<uintptr_t>(dp) | reinterpret_cast<uintptr_t>(d_dst)) & 7)) {
-            (void)hipGetLastError();  // (not page-locked, or unaligned: the runtime's copy)
+        if (!pinned || ((reinterpret_cast<uintptr_t>(dp) | reinterpret_cast<uintptr_t>(d_dst)) & 15)) {
+            (void)hipGetLastError();  // (not page-locked, or not 16-B aligned: the runtime's copy)
             RSVIO_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, s));
             return (int)RSVIO_OK;
         }
-        const long long nw = (long long)(bytes / 8);
-        const int tail = (int)(bytes % 8);
-        const long long per = 256LL * kUpWords;
-        const unsigned grid = (unsigned)std::max<long long>(1, (nw + per - 1) / per);
-        auto* src8 = static_cast<const unsigned long long*>(dp);
-        auto* dst8 = static_cast<unsigned long long*>(d_dst);
-        hipLaunchKernelGGL(upload_words_kernel, dim3(grid), dim3(256), 0, s, src8, dst8, nw,
-                           reinterpret_cast<const unsigned char*>(src8 + nw), reinterpret_cast<unsigned char*>(dst8 + nw),
-                           tail);
+        const long long nw = (long long)(bytes / 16);
+        const int tail = (int)(bytes % 16);
+        const unsigned grid = (unsigned)std::max<long long>(1, (nw + 511) / 512);
+        auto* src16 = static_cast<const uint4*>(dp);
+        auto* dst16 = static_cast<uint4*>(d_dst);
+        hipLaunchKernelGGL(upload_words_kernel, dim3(grid), dim3(256), 0, s, src16, dst16, nw,
+                           reinterpret_cast<const unsigned char*>(src16 + nw),
+                           reinterpret_cast<unsigned char*>(dst16 + nw), tail);
         RSVIO_HIP(hipGetLastError());
         return (int)RSVIO_OK;
     });
