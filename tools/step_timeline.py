@@ -5,8 +5,8 @@
   python tools/step_timeline.py DIR
 
 A step is anchored on its ba_build_layout dispatch (one per rsvio_ba_set_problem).  Its host start
-T0 is the image upload: the hipMemcpyAsync on the launching thread just before set_problem's own
-window upload (the last hipMemcpyAsync before the anchor's launch).  Every main-thread HIP call and
+T0 is the image upload: the launch of the step's upload_words_kernel (rsvio_upload_async), or else
+the hipMemcpyAsync on the launching thread just before set_problem's own window copy.  Every main-thread HIP call and
 every device kernel / copy from T0 to the next step's T0 is labelled (name, occurrence in the step);
 the medians over the steps whose host call sequence has the most common signature are printed in
 microseconds from T0.
@@ -47,9 +47,17 @@ def main(d):
     tid = corr_api[anchors[0]["Correlation_Id"]]["Thread_Id"]
     main_api = sorted((r for r in api if r["Thread_Id"] == tid), key=lambda r: int(r["Start_Timestamp"]))
     starts = [int(r["Start_Timestamp"]) for r in main_api]
+    # the image upload's launch: an upload_words_kernel dispatch (rsvio_upload_async) if the step
+    # has one, else the hipMemcpyAsync before set_problem's own window copy
+    up_launch = sorted(int(corr_api[r["Correlation_Id"]]["Start_Timestamp"]) for r in kern
+                       if "upload_words_kernel" in r["Kernel_Name"] and r["Correlation_Id"] in corr_api)
     t0s = []
     for a in anchors:
         la = int(corr_api[a["Correlation_Id"]]["Start_Timestamp"])
+        ups = [u for u in up_launch if u < la]
+        if ups and (not t0s or ups[-1] > t0s[-1]):
+            t0s.append(ups[-1])
+            continue
         cp = [i for i, r in enumerate(main_api) if int(r["Start_Timestamp"]) < la and r["Function"] == "hipMemcpyAsync"]
         t0s.append(int(main_api[cp[-2]]["Start_Timestamp"]) if len(cp) >= 2 else la)
     dev = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kern]
