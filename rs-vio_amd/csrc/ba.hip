@@ -605,6 +605,8 @@ struct SlotSrc {
     const double2* uv;               // n_obs, f64 -- or, when uv32 is set, the same values as f32 pairs
     int nb_lm, nb_pad;               // blocks of the landmark and padding parts of the grid
     int uv32;                        // the upload holds (u, v) as float2 (every value exact in f32)
+    int obs_host;                    // key and uv point into the pinned staging image (read once
+                                     // each, at system scope, instead of staged into the arena)
 };
 constexpr unsigned long long kEvenBits = 0x5555555555555555ull;
 
@@ -643,18 +645,38 @@ __device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSr
     } else {
         const int i = 256 * (b - S.nb_lm - S.nb_pad) + t;
         if (i >= G.n_obs) return;
-        const unsigned key = S.key[i];
+        // (from the pinned image: each observation's key and (u, v) are read once, here, so the
+        // stage-in copy leaves them out; both loads in flight before the mask's)
+        unsigned key;
+        double2 ouv;
+        if (S.obs_host) {
+            key = __hip_atomic_load(S.key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (S.uv32) {
+                const unsigned long long w = __hip_atomic_load(
+                    reinterpret_cast<const unsigned long long*>(S.uv) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                ouv = make_double2((double)__uint_as_float((unsigned)w), (double)__uint_as_float((unsigned)(w >> 32)));
+            } else {
+                const unsigned long long* p = reinterpret_cast<const unsigned long long*>(S.uv + i);
+                ouv = make_double2(
+                    __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)),
+                    __longlong_as_double(
+                        (long long)__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+            }
+        } else {
+            key = S.key[i];
+            if (S.uv32) {  // widened exactly: the same f64 values as the caller's
+                const float2 f = reinterpret_cast<const float2*>(S.uv)[i];
+                ouv = make_double2((double)f.x, (double)f.y);
+            } else {
+                ouv = S.uv[i];
+            }
+        }
         const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
         const unsigned long long m = S.mask[l];
         const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
         const size_t q = (size_t)S.lm_base[l] + __popcll(below);
         const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
-        if (S.uv32) {  // widened exactly: the same f64 values as the caller's
-            const float2 f = reinterpret_cast<const float2*>(S.uv)[i];
-            huv[2 * q + sub] = make_double2((double)f.x, (double)f.y);
-        } else {
-            huv[2 * q + sub] = S.uv[i];
-        }
+        huv[2 * q + sub] = ouv;
     }
 }
 
@@ -4685,7 +4707,9 @@ struct BundleAdjuster {
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
         if (stage_kernel) {
-            const int nw = (int)(L.upload / 16);  // (L.upload is a multiple of 256)
+            // the arena's part before the observations (descriptor, state, tables, masks); the
+            // layout kernel reads the keys and (u, v) from the pinned image itself
+            const int nw = (int)(L.key / 16);  // (L.key is a multiple of 256)
             hipLaunchKernelGGL(ba_stage_in, dim3((nw + 511) / 512), dim3(256), 0, stream,
                                reinterpret_cast<const uint4*>(h_arena_dev), reinterpret_cast<uint4*>(d_arena.p), nw);
             RSVIO_HIP(hipGetLastError());
@@ -4698,9 +4722,11 @@ struct BundleAdjuster {
             S.mask = reinterpret_cast<const unsigned long long*>(d_arena.p + L.mask);
             S.lm_base = reinterpret_cast<const int*>(d_arena.p + L.lm_base);
             S.wave_fill = reinterpret_cast<const int*>(d_arena.p + L.wave_fill);
-            S.key = reinterpret_cast<const unsigned*>(d_arena.p + L.key);
-            S.uv = reinterpret_cast<const double2*>(d_arena.p + L.ouv);
+            const uint8_t* obs_src = stage_kernel ? static_cast<const uint8_t*>(h_arena_dev) : d_arena.p;
+            S.key = reinterpret_cast<const unsigned*>(obs_src + L.key);
+            S.uv = reinterpret_cast<const double2*>(obs_src + L.ouv);
             S.uv32 = uv32 ? 1 : 0;
+            S.obs_host = stage_kernel ? 1 : 0;
             S.wave_lm = reinterpret_cast<const int*>(d_arena.p + L.wave_lm);
             S.nb_lm = (n_lm + 255) / 256;
             S.nb_pad = (int)((n_pad + 255) / 256);
