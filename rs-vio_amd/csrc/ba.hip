@@ -643,25 +643,44 @@ __device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSr
         huv[2 * (size_t)ps] = z2;
         huv[2 * (size_t)ps + 1] = z2;
     } else {
-        const int i = 256 * (b - S.nb_lm - S.nb_pad) + t;
+        const int tt = 256 * (b - S.nb_lm - S.nb_pad) + t;
+        // one observation's (u, v) into its slot (the first = camera 0 if present, the second =
+        // camera 1)
+        auto place = [&](unsigned key, double2 ouv) {
+            const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
+            const unsigned long long m = S.mask[l];
+            const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
+            const size_t q = (size_t)S.lm_base[l] + __popcll(below);
+            const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
+            huv[2 * q + sub] = ouv;
+        };
+        if (S.obs_host && S.uv32) {
+            // from the pinned image, read once here (the stage-in copy leaves them out): 4
+            // observations per thread, their 4 keys and 4 f32 (u, v) pairs in three 16-B loads (the
+            // key and (u, v) sections are 256-B aligned and padded, so the last group stays inside)
+            const int i0 = 4 * tt;
+            if (i0 >= G.n_obs) return;
+            uint4 kv, u01, u23;
+            host_load3x16(S.key + i0, reinterpret_cast<const float*>(S.uv) + 2 * i0,
+                          reinterpret_cast<const float*>(S.uv) + 2 * i0 + 4, kv, u01, u23);
+            const unsigned keys[4] = {kv.x, kv.y, kv.z, kv.w};
+            const unsigned uvw[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)  // (widened exactly: the same f64 values as the caller's)
+                if (i0 + j < G.n_obs)
+                    place(keys[j], make_double2((double)__uint_as_float(uvw[2 * j]), (double)__uint_as_float(uvw[2 * j + 1])));
+            return;
+        }
+        const int i = tt;
         if (i >= G.n_obs) return;
-        // (from the pinned image: each observation's key and (u, v) are read once, here, so the
-        // stage-in copy leaves them out; both loads in flight before the mask's)
         unsigned key;
         double2 ouv;
-        if (S.obs_host) {
+        if (S.obs_host) {  // f64 (u, v) from the pinned image: one observation per thread
             key = __hip_atomic_load(S.key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (S.uv32) {
-                const unsigned long long w = __hip_atomic_load(
-                    reinterpret_cast<const unsigned long long*>(S.uv) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                ouv = make_double2((double)__uint_as_float((unsigned)w), (double)__uint_as_float((unsigned)(w >> 32)));
-            } else {
-                const unsigned long long* p = reinterpret_cast<const unsigned long long*>(S.uv + i);
-                ouv = make_double2(
-                    __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)),
-                    __longlong_as_double(
-                        (long long)__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
-            }
+            const unsigned long long* p = reinterpret_cast<const unsigned long long*>(S.uv + i);
+            ouv = make_double2(
+                __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)),
+                __longlong_as_double((long long)__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
         } else {
             key = S.key[i];
             if (S.uv32) {  // widened exactly: the same f64 values as the caller's
@@ -671,12 +690,7 @@ __device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSr
                 ouv = S.uv[i];
             }
         }
-        const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
-        const unsigned long long m = S.mask[l];
-        const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
-        const size_t q = (size_t)S.lm_base[l] + __popcll(below);
-        const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
-        huv[2 * q + sub] = ouv;
+        place(key, ouv);
     }
 }
 
@@ -4730,7 +4744,8 @@ struct BundleAdjuster {
             S.wave_lm = reinterpret_cast<const int*>(d_arena.p + L.wave_lm);
             S.nb_lm = (n_lm + 255) / 256;
             S.nb_pad = (int)((n_pad + 255) / 256);
-            const int nb = S.nb_lm + S.nb_pad + (n_obs + 255) / 256;
+            const int opt = S.obs_host && S.uv32 ? 4 : 1;  // observations per thread
+            const int nb = S.nb_lm + S.nb_pad + (n_obs + 256 * opt - 1) / (256 * opt);
             hipLaunchKernelGGL(ba_build_layout, dim3(nb + n_chunk), dim3(256), 0, stream, G, prob(), S, nb,
                                reinterpret_cast<int4*>(d_arena.p + L.hdr), reinterpret_cast<double2*>(d_arena.p + L.uv),
                                reinterpret_cast<int4*>(d_arena.p + L.pairs));
