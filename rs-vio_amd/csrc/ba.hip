@@ -605,8 +605,6 @@ struct SlotSrc {
     const double2* uv;               // n_obs, f64 -- or, when uv32 is set, the same values as f32 pairs
     int nb_lm, nb_pad;               // blocks of the landmark and padding parts of the grid
     int uv32;                        // the upload holds (u, v) as float2 (every value exact in f32)
-    int obs_host;                    // key and uv point into the pinned staging image (read once
-                                     // each, at system scope, instead of staged into the arena)
 };
 constexpr unsigned long long kEvenBits = 0x5555555555555555ull;
 
@@ -643,54 +641,20 @@ __device__ void build_slots_body(const Geometry& G, const Prob& Pr, const SlotSr
         huv[2 * (size_t)ps] = z2;
         huv[2 * (size_t)ps + 1] = z2;
     } else {
-        const int tt = 256 * (b - S.nb_lm - S.nb_pad) + t;
-        // one observation's (u, v) into its slot (the first = camera 0 if present, the second =
-        // camera 1)
-        auto place = [&](unsigned key, double2 ouv) {
-            const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
-            const unsigned long long m = S.mask[l];
-            const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
-            const size_t q = (size_t)S.lm_base[l] + __popcll(below);
-            const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
-            huv[2 * q + sub] = ouv;
-        };
-        if (S.obs_host && S.uv32) {
-            // from the pinned image, read once here (the stage-in copy leaves them out): 4
-            // observations per thread, their 4 keys and 4 f32 (u, v) pairs in three 16-B loads (the
-            // key and (u, v) sections are 256-B aligned and padded, so the last group stays inside)
-            const int i0 = 4 * tt;
-            if (i0 >= G.n_obs) return;
-            uint4 kv, u01, u23;
-            host_load3x16(S.key + i0, reinterpret_cast<const float*>(S.uv) + 2 * i0,
-                          reinterpret_cast<const float*>(S.uv) + 2 * i0 + 4, kv, u01, u23);
-            const unsigned keys[4] = {kv.x, kv.y, kv.z, kv.w};
-            const unsigned uvw[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j)  // (widened exactly: the same f64 values as the caller's)
-                if (i0 + j < G.n_obs)
-                    place(keys[j], make_double2((double)__uint_as_float(uvw[2 * j]), (double)__uint_as_float(uvw[2 * j + 1])));
-            return;
-        }
-        const int i = tt;
+        const int i = 256 * (b - S.nb_lm - S.nb_pad) + t;
         if (i >= G.n_obs) return;
-        unsigned key;
-        double2 ouv;
-        if (S.obs_host) {  // f64 (u, v) from the pinned image: one observation per thread
-            key = __hip_atomic_load(S.key + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const unsigned long long* p = reinterpret_cast<const unsigned long long*>(S.uv + i);
-            ouv = make_double2(
-                __longlong_as_double((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)),
-                __longlong_as_double((long long)__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+        const unsigned key = S.key[i];
+        const int l = (int)(key >> 6), k = (int)(key >> 1) & 31, c = (int)(key & 1);
+        const unsigned long long m = S.mask[l];
+        const unsigned long long below = ((m | (m >> 1)) & kEvenBits) & ((1ull << (2 * k)) - 1ull);
+        const size_t q = (size_t)S.lm_base[l] + __popcll(below);
+        const int sub = (c == 1 && ((m >> (2 * k)) & 1)) ? 1 : 0;
+        if (S.uv32) {  // widened exactly: the same f64 values as the caller's
+            const float2 f = reinterpret_cast<const float2*>(S.uv)[i];
+            huv[2 * q + sub] = make_double2((double)f.x, (double)f.y);
         } else {
-            key = S.key[i];
-            if (S.uv32) {  // widened exactly: the same f64 values as the caller's
-                const float2 f = reinterpret_cast<const float2*>(S.uv)[i];
-                ouv = make_double2((double)f.x, (double)f.y);
-            } else {
-                ouv = S.uv[i];
-            }
+            huv[2 * q + sub] = S.uv[i];
         }
-        place(key, ouv);
     }
 }
 
@@ -4721,9 +4685,7 @@ struct BundleAdjuster {
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
         if (stage_kernel) {
-            // the arena's part before the observations (descriptor, state, tables, masks); the
-            // layout kernel reads the keys and (u, v) from the pinned image itself
-            const int nw = (int)(L.key / 16);  // (L.key is a multiple of 256)
+            const int nw = (int)(L.upload / 16);  // (L.upload is a multiple of 256)
             hipLaunchKernelGGL(ba_stage_in, dim3((nw + 511) / 512), dim3(256), 0, stream,
                                reinterpret_cast<const uint4*>(h_arena_dev), reinterpret_cast<uint4*>(d_arena.p), nw);
             RSVIO_HIP(hipGetLastError());
@@ -4736,16 +4698,13 @@ struct BundleAdjuster {
             S.mask = reinterpret_cast<const unsigned long long*>(d_arena.p + L.mask);
             S.lm_base = reinterpret_cast<const int*>(d_arena.p + L.lm_base);
             S.wave_fill = reinterpret_cast<const int*>(d_arena.p + L.wave_fill);
-            const uint8_t* obs_src = stage_kernel ? static_cast<const uint8_t*>(h_arena_dev) : d_arena.p;
-            S.key = reinterpret_cast<const unsigned*>(obs_src + L.key);
-            S.uv = reinterpret_cast<const double2*>(obs_src + L.ouv);
+            S.key = reinterpret_cast<const unsigned*>(d_arena.p + L.key);
+            S.uv = reinterpret_cast<const double2*>(d_arena.p + L.ouv);
             S.uv32 = uv32 ? 1 : 0;
-            S.obs_host = stage_kernel ? 1 : 0;
             S.wave_lm = reinterpret_cast<const int*>(d_arena.p + L.wave_lm);
             S.nb_lm = (n_lm + 255) / 256;
             S.nb_pad = (int)((n_pad + 255) / 256);
-            const int opt = S.obs_host && S.uv32 ? 4 : 1;  // observations per thread
-            const int nb = S.nb_lm + S.nb_pad + (n_obs + 256 * opt - 1) / (256 * opt);
+            const int nb = S.nb_lm + S.nb_pad + (n_obs + 255) / 256;
             hipLaunchKernelGGL(ba_build_layout, dim3(nb + n_chunk), dim3(256), 0, stream, G, prob(), S, nb,
                                reinterpret_cast<int4*>(d_arena.p + L.hdr), reinterpret_cast<double2*>(d_arena.p + L.uv),
                                reinterpret_cast<int4*>(d_arena.p + L.pairs));

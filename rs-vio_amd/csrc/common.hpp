@@ -131,19 +131,6 @@ __device__ __forceinline__ void host_load2x16(const void* a, const void* b, uint
         : "memory");
 }
 
-// Three such loads (ba_build_layout's observations: 4 keys and their 4 f32 (u, v) pairs).
-__device__ __forceinline__ void host_load3x16(const void* a, const void* b, const void* c, uint4& va, uint4& vb,
-                                              uint4& vc) {
-    __asm__ volatile(
-        "global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
-        "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
-        "global_load_dwordx4 %2, %5, off sc0 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(va), "=&v"(vb), "=&v"(vc)
-        : "v"(a), "v"(b), "v"(c)
-        : "memory");
-}
-
 __host__ __device__ inline uint32_t level_w(uint32_t w, int i) { return w / (1u << i); }
 __host__ __device__ inline uint32_t level_h(uint32_t h, int i) { return h / (1u << i); }
 __host__ __device__ inline size_t level_offset(uint32_t w, uint32_t h, int level) {
