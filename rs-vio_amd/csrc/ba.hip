@@ -4278,6 +4278,7 @@ struct BundleAdjuster {
     // (profiles/r06g_setprob.txt), the step no slower (profiles/r06h_early_copy_ab.txt)
     bool early_env = false;
     bool stage_kernel = true;   // RSVIO_BA_STAGE=sdma: the staging image by hipMemcpyAsync (A/B)
+    bool stage_split = true;    // RSVIO_BA_STAGE_SPLIT=0: one stage-in launch at the end (A/B)
     const void* h_arena_dev = nullptr;  // the staging image's device address
     // the optimised state of the last solve, written by its final decision kernel (K7) before the
     // ticket: [pose7 n_kf x 7 | p_W n_lm x 3]; state_export = it holds the handle's current state
@@ -4361,6 +4362,8 @@ struct BundleAdjuster {
         const char* stv = std::getenv("RSVIO_BA_STAGE");
         stage_kernel = !(stv && std::strcmp(stv, "sdma") == 0);
         if (stage_kernel) early_env = false;
+        const char* ssv = std::getenv("RSVIO_BA_STAGE_SPLIT");
+        stage_split = stage_kernel && !(ssv && ssv[0] == '0');
         const char* kv = std::getenv("RSVIO_K5");  // A/B switch: "gj1" one-wave Gauss-Jordan
         if (kv && std::strcmp(kv, "gj1") == 0) k5_variant = 1;
         if (kv && std::strcmp(kv, "pipe4") == 0) k5_variant = 0;
@@ -4594,6 +4597,18 @@ struct BundleAdjuster {
             d_arena.alloc(2 * L.upload);
         }
         settled = false;  // (the upload, grow_buffers' memset and ba_build_layout go on the stream)
+        // the staging image's [off0, off1) into the arena by ba_stage_in (both 256-B aligned)
+        auto stage = [&](size_t off0, size_t off1) {
+            const int nw = (int)((off1 - off0) / 16);
+            if (nw <= 0) return;
+            hipLaunchKernelGGL(ba_stage_in, dim3((nw + 511) / 512), dim3(256), 0, stream,
+                               reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(h_arena_dev) + off0),
+                               reinterpret_cast<uint4*>(d_arena.p + off0), nw);
+            RSVIO_HIP(hipGetLastError());
+        };
+        // split: the observation section (masks, keys, (u, v): ~300 KB of the ~390) goes up now,
+        // while the host packs the waves and fills the tables; the rest at the end
+        if (stage_split) stage(L.mask, L.upload);
         if (early_env)
             RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice, stream));
         mark();
@@ -4656,6 +4671,7 @@ struct BundleAdjuster {
         L.total = off;
         if (d_arena.n < L.total) {  // the observation copy above went to the old arena: redo it
             d_arena.alloc(L.total + L.total / 4);
+            if (stage_split) stage(L.mask, L.upload);
             if (early_env)
                 RSVIO_HIP(hipMemcpyAsync(d_arena.p + L.mask, hb + L.mask, L.upload - L.mask, hipMemcpyHostToDevice,
                                          stream));
@@ -4685,10 +4701,7 @@ struct BundleAdjuster {
         std::memcpy(hb + L.desc, &hdesc, sizeof(WinDesc));
         mark();
         if (stage_kernel) {
-            const int nw = (int)(L.upload / 16);  // (L.upload is a multiple of 256)
-            hipLaunchKernelGGL(ba_stage_in, dim3((nw + 511) / 512), dim3(256), 0, stream,
-                               reinterpret_cast<const uint4*>(h_arena_dev), reinterpret_cast<uint4*>(d_arena.p), nw);
-            RSVIO_HIP(hipGetLastError());
+            stage(0, stage_split ? L.mask : L.upload);  // (L.mask and L.upload are multiples of 256)
         } else {
             RSVIO_HIP(hipMemcpyAsync(d_arena.p, hb, early_env ? L.mask : L.upload, hipMemcpyHostToDevice, stream));
         }
