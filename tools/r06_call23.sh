@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 6, call 23: the final tree's headline-only kernel summary and its traced step timeline
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06x_prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-rows --pipeline-frames 0 \
+  > gpurun_out/r06x_prof.json 2> gpurun_out/r06x_prof.err || { tail -20 gpurun_out/r06x_prof.err; exit 1; }
+python tools/kstats.py gpurun_out/r06x_prof > gpurun_out/r06x_headline_kstats.txt; head -18 gpurun_out/r06x_headline_kstats.txt
+rm -f gpurun_out/r06x_prof/run_kernel_trace.csv
+timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/r06x_tl -o run \
+  -- python3 bench.py --steps 20 --warmup 5 --reps 2 --no-cpu --no-rows --pipeline-frames 0 > gpurun_out/r06x_tl.json 2> gpurun_out/r06x_tl.err || { tail -20 gpurun_out/r06x_tl.err; exit 1; }
+python tools/step_timeline.py gpurun_out/r06x_tl > gpurun_out/r06x_timeline.txt 2>&1; head -50 gpurun_out/r06x_timeline.txt
+gzip -f gpurun_out/r06x_tl/*.csv
