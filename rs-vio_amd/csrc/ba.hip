@@ -3715,9 +3715,18 @@ __device__ __forceinline__ void lm_decide_body(const Geometry& G, const Prob& Pr
         const double* pose = Wk.pose[s.cur];
         const double* pw = Wk.pw[s.cur];
         const int np = 7 * G.n_kf, n = np + 3 * G.n_lm;
-        const int per = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+        // even slices, written 16 B per store (half the PCIe write requests of 8-B stores)
+        const int per = (((n + (int)gridDim.x - 1) / (int)gridDim.x) + 1) & ~1;
         const int i0 = (int)blockIdx.x * per, i1 = min(n, i0 + per);
-        for (int i = i0 + (int)threadIdx.x; i < i1; i += kK7Threads) hout[i] = i < np ? pose[i] : pw[i - np];
+        for (int i = i0 + 2 * (int)threadIdx.x; i < i1; i += 2 * kK7Threads) {
+            const double a = i < np ? pose[i] : pw[i - np];
+            if (i + 1 < i1) {
+                const double b = i + 1 < np ? pose[i + 1] : pw[i + 1 - np];
+                *reinterpret_cast<double2*>(hout + i) = make_double2(a, b);
+            } else {
+                hout[i] = a;
+            }
+        }
         __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0)
