@@ -635,6 +635,24 @@ def tame_malloc():
     log(f"[bench] malloc: no trimming, mmap threshold 32 MB ({'ok' if ok else 'mallopt refused'})")
 
 
+def pin_main_thread(mode: str) -> str:
+    """--pin-cpu: keep the calling (main) thread on one CPU -- the one it runs on now ("current"),
+    or the given number -- as a real-time caller pins its control thread; the runtime's own threads,
+    created earlier, keep their affinity."""
+    if mode in ("", "off"):
+        return "off"
+    try:
+        if mode == "current":
+            with open("/proc/thread-self/stat") as f:
+                cpu = int(f.read().rsplit(")", 1)[1].split()[36])
+        else:
+            cpu = int(mode)
+        os.sched_setaffinity(0, {cpu})
+        return f"cpu {cpu}"
+    except (OSError, ValueError, IndexError) as e:
+        return f"failed ({e})"
+
+
 def lock_code() -> str:
     """mlock the executable mappings of the HIP / HSA runtimes and the product library (diagnostic
     of the one-rep stall: if host memory pressure drops their code pages from this process, the
@@ -1376,6 +1394,8 @@ def main():
                     help="who runs the protocol step's calls: native (default) -- lib/librsvio_host.so, the same "
                          "C ABI calls from C++ as the reference's Rust caller makes them; python -- this loop "
                          "(ctypes; ~1-5 us of interpreter per call; --trace-steps uses it)")
+    ap.add_argument("--pin-cpu", default="off",
+                    help="pin the main thread: off (default), current (the CPU it runs on), or a CPU number")
     ap.add_argument("--lock-code", type=int, default=0,
                     help="1: mlock the runtimes' and the library's mapped pages (stall diagnostic)")
     ap.add_argument("--tame-malloc", type=int, default=1,
@@ -1414,6 +1434,8 @@ def main():
     arch = rsvio.require_device(local)
     if args.lock_code:
         log(f"[bench] lock-code: {lock_code()}")
+    pin_state = pin_main_thread(args.pin_cpu)
+    log(f"[bench] main thread: {pin_state}")
     log(f"[bench] rank {rank}/{world} on cuda:{local} ({arch})")
     streams = []
     if args.cu_split > 0:
@@ -1589,10 +1611,14 @@ def main():
         "warmup": args.warmup,
         "reps": args.reps,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-        "value_note": "BASELINE.md protocol, median of reps: per frame 2 x 361 KB image H2D (pinned), "
-                      "pyramids + LK, 3 x 300 feature states + valid flags D2H; a NEW keyframe window "
-                      "uploaded (rsvio_ba_set_problem: sort, tables, pinned staging, H2D; two windows "
-                      "alternate) and solved (graph re-captured), its state (48.6 KB) D2H",
+        "value_note": "BASELINE.md protocol, median of reps: per frame the 2 x 361 KB images up from "
+                      "pinned host memory (--upload kernel: rsvio_upload_async, a kernel reads them over "
+                      "PCIe), pyramids + LK, 3 x 300 feature states + valid flags D2H; a NEW keyframe window "
+                      "uploaded (rsvio_ba_set_problem: validation, masks, waves and tables into pinned "
+                      "staging, ba_stage_in reading it over PCIe, the slot layout built on the device; two "
+                      "windows alternate) and solved (the descriptor-mode graph), its state (48.6 KB) "
+                      "published to pinned host memory by the final decision and read back",
+        "main_thread": pin_state,
         "value_reps": [round(frames / e, 3) for e in el_pro],
         "driver": "native (lib/librsvio_host.so: the step's C ABI calls from C++)" if native is not None
                   else "python (ctypes)",
