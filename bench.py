@@ -653,6 +653,36 @@ def pin_main_thread(mode: str) -> str:
         return f"failed ({e})"
 
 
+def numa_local(device: int) -> str:
+    """--numa-local: every thread of the process onto the CPUs of the GPU's NUMA node (those the
+    process may use), as a deployment places a GPU's host process -- the pinned staging, the
+    caller's arrays and the queue writes then stay on the GPU's side of the socket link."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return "off (no PCI bus id)"
+        bus = buf.value.decode().lower()
+        node = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
+        if node < 0:
+            return "off (no NUMA node)"
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return "off (no allowed CPU on the node)"
+        for t in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(t), cpus)
+            except OSError:
+                pass
+        return f"node {node} ({len(cpus)} CPUs)"
+    except (OSError, ValueError) as e:
+        return f"off ({e})"
+
+
 def lock_code() -> str:
     """mlock the executable mappings of the HIP / HSA runtimes and the product library (diagnostic
     of the one-rep stall: if host memory pressure drops their code pages from this process, the
@@ -1394,6 +1424,8 @@ def main():
                     help="who runs the protocol step's calls: native (default) -- lib/librsvio_host.so, the same "
                          "C ABI calls from C++ as the reference's Rust caller makes them; python -- this loop "
                          "(ctypes; ~1-5 us of interpreter per call; --trace-steps uses it)")
+    ap.add_argument("--numa-local", type=int, default=0,
+                    help="1: every thread onto the CPUs of the GPU's NUMA node (process placement)")
     ap.add_argument("--pin-cpu", default="off",
                     help="pin the main thread: off (default), current (the CPU it runs on), or a CPU number")
     ap.add_argument("--lock-code", type=int, default=0,
@@ -1435,6 +1467,8 @@ def main():
     if args.lock_code:
         log(f"[bench] lock-code: {lock_code()}")
     pin_state = pin_main_thread(args.pin_cpu)
+    if args.numa_local:
+        pin_state += "; process: " + numa_local(local)
     log(f"[bench] main thread: {pin_state}")
     log(f"[bench] rank {rank}/{world} on cuda:{local} ({arch})")
     streams = []
