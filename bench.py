@@ -1424,8 +1424,10 @@ def main():
                     help="who runs the protocol step's calls: native (default) -- lib/librsvio_host.so, the same "
                          "C ABI calls from C++ as the reference's Rust caller makes them; python -- this loop "
                          "(ctypes; ~1-5 us of interpreter per call; --trace-steps uses it)")
-    ap.add_argument("--numa-local", type=int, default=0,
-                    help="1: every thread onto the CPUs of the GPU's NUMA node (process placement)")
+    ap.add_argument("--numa-local", type=int, default=1,
+                    help="1 (default): every thread onto the CPUs of the GPU's NUMA node, as a deployment places "
+                         "a GPU's host process (4,799-4,854 frames/s vs 4,121-4,821 unplaced, 3 alternating pairs, "
+                         "profiles/r06z3_numa_local_ab.txt); 0: wherever the scheduler puts it")
     ap.add_argument("--pin-cpu", default="off",
                     help="pin the main thread: off (default), current (the CPU it runs on), or a CPU number")
     ap.add_argument("--lock-code", type=int, default=0,
