@@ -2454,6 +2454,8 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
     WSTAMP(0, 32 + K);                       // slots 32..51: the same for every step (NF <= 20)
     WSTAMP(1, 64 + K);                       // slots 64..83: wave 1 done with step K - 1's update
     if (wave == 0) {
+        double Dg[6][6], Lg[6][6], inv[6];
+#ifdef RSVIO_BK_DIAG_LDS
         // the diagonal block to every lane: its 6 rows store, every lane reads the lower 21
 #pragma unroll
         for (int h = 0; h < RPL; ++h) {
@@ -2464,11 +2466,18 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        double Dg[6][6], Lg[6][6], inv[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i)
 #pragma unroll
             for (int j = 0; j <= i; ++j) Dg[i][j] = Dsc[6 * i + j];
+#else
+        // the diagonal block to every lane by readlane: row c0 + i is lane (c0 + i) % 64's register
+        // set (c0 + i) / 64, both compile-time -- no LDS store, wave barrier and read on the chain
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) Dg[i][j] = rl64(a[(c0 + i) >> 6][j], (c0 + i) & 63);
+#endif
         // its LDL^T, redundantly on every lane: Dg[i][j] (i > j) ends as U = (D L)[i][j], Lg = L
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
