@@ -2453,6 +2453,7 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
     if constexpr (K < 9) WSTAMP(0, 8 + K);  // slots 8..16: wave 0 at the step's start
     WSTAMP(0, 32 + K);                       // slots 32..51: the same for every step (NF <= 20)
     WSTAMP(1, 64 + K);                       // slots 64..83: wave 1 done with step K - 1's update
+    WSTAMP(7, 160 + K);                      // slots 160..179: wave 7 (the last update wave) the same
     if (wave == 0) {
         double Dg[6][6], Lg[6][6], inv[6];
 #ifdef RSVIO_BK_DIAG_LDS
@@ -2524,6 +2525,7 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
     if constexpr (K == 0) WSTAMP(0, 30);  // wave 0's part A of step 0 done
     if constexpr (K == 4) WSTAMP(0, 31);
     if constexpr (K >= 1 && K <= 4) WSTAMP(1, 25 + K);  // slots 26..29: wave 1 done with step K - 1
+    WSTAMP(0, 128 + K);  // slots 128..147: wave 0 at barrier K (its part A done)
     __syncthreads();  // L and U of block K visible; the update waves finished block K - 1's update
     if constexpr (K < 8) WSTAMP(0, 17 + K);  // slots 17..24: wave 0 released by barrier K
     WSTAMP(0, 96 + K);                          // slots 96..115: the same for every step

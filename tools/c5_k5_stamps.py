@@ -25,17 +25,18 @@ ba.set_problem_from(prob)
 rows = []
 for rep in range(8):
     ba.camera_step(1e-4)
-    buf = (C.c_ulonglong * 128)()
-    lib.rsvio_dbg_ba_stamps(buf, 128)
-    rows.append(np.array(buf[:128], dtype=np.int64))
+    buf = (C.c_ulonglong * 192)()
+    lib.rsvio_dbg_ba_stamps(buf, 192)
+    rows.append(np.array(buf[:192], dtype=np.int64))
 st = np.median(np.stack(rows[3:]), axis=0).astype(np.int64)
 t0 = st[0]
 nf = int((prob.kf_fixed == 0).sum())
 print(f"config 5 K5 (ba_camera_solve_blk<20>, {nf} free keyframes): cycles from entry")
 print(f"combine done {st[1] - t0}, fail check {st[2] - t0}, factorisation done {st[3] - t0}, "
       f"back substitution {st[4] - t0}, end {st[5] - t0}")
-print("step  w0_start  w0_released  w1_prev_update_done  step_len")
+print("step  w0_start  w0_at_barrier  w0_released  w1_prev_update_done  w7_prev_update_done  step_len")
 for k in range(nf):
     a, r, u = st[32 + k] - t0, st[96 + k] - t0, st[64 + k] - t0
+    b, u7 = st[128 + k] - t0, st[160 + k] - t0
     nxt = st[32 + k + 1] - t0 if k + 1 < nf else st[3] - t0
-    print(f"{k:4d} {a:9d} {r:12d} {u:20d} {nxt - a:9d}")
+    print(f"{k:4d} {a:9d} {b:14d} {r:12d} {u:20d} {u7:20d} {nxt - a:9d}")
