@@ -2450,7 +2450,6 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
     constexpr int RPL = D::RPL, LD = D::LD, c0 = 6 * K;
     const int lane = tid & 63, wave = tid >> 6;
     double u[RPL][6];
-    double lk[RPL][6];  // this step's multipliers of the chain wave's rows (the look-ahead's L rows)
     if constexpr (K < 9) WSTAMP(0, 8 + K);  // slots 8..16: wave 0 at the step's start
     WSTAMP(0, 32 + K);                       // slots 32..51: the same for every step (NF <= 20)
     WSTAMP(1, 64 + K);                       // slots 64..83: wave 1 done with step K - 1's update
@@ -2517,14 +2516,10 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
             if (r < D::NPP)
 #pragma unroll
                 for (int j = 0; j < 6; ++j) U[(K & 1) * 6 * LD + j * LD + r] = below ? u[h][j] : 0.0;
-#pragma unroll
-            for (int j = 0; j < 6; ++j) lk[h][j] = l[j];
-#ifdef RSVIO_BK_LSC_LDS
             if constexpr (K + 1 < NF)
                 if (i >= 6 && i < 12)
 #pragma unroll
                     for (int j = 0; j < 6; ++j) Lsc[6 * (i - 6) + j] = l[j];
-#endif
         }
     }
     if constexpr (K == 0) WSTAMP(0, 30);  // wave 0's part A of step 0 done
@@ -2539,20 +2534,10 @@ __device__ __forceinline__ void bk_steps(double* M, double* U, double* Dsc, doub
             // the look-ahead: column block K + 1 (block K - 1's update applied by the update
             // waves) minus this block's contribution, in registers
             double Ls[6][6];
-#ifdef RSVIO_BK_LSC_LDS
 #pragma unroll
             for (int j = 0; j < 6; ++j)
 #pragma unroll
                 for (int m = 0; m < 6; ++m) Ls[j][m] = Lsc[6 * j + m];
-#else
-            // the next block's 6 L rows by readlane from the lanes that formed them (row c0 + 6 + j:
-            // lane (c0 + 6 + j) % 64, register set (c0 + 6 + j) / 64, compile-time) -- no LDS
-            // stores before the barrier, no broadcast reads after it
-#pragma unroll
-            for (int j = 0; j < 6; ++j)
-#pragma unroll
-                for (int m = 0; m < 6; ++m) Ls[j][m] = rl64(lk[(c0 + 6 + j) >> 6][m], (c0 + 6 + j) & 63);
-#endif
 #pragma unroll
             for (int h = 0; h < RPL; ++h) {
                 const int r = lane + 64 * h < D::NPP ? lane + 64 * h : D::NPP - 1;
