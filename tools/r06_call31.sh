@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6, call 23: the final tree's headline-only kernel summary and its traced step timeline
+# round 6, call 31: the final tree's headline-only kernel summary
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
