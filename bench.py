@@ -386,7 +386,7 @@ class _StageTimer:
 
 
 def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_seconds: float = 40.0,
-                         native: bool = True):
+                         native: bool = True, ba_cus=None):
     """BASELINE config 4 on one GPU: the Estimator (estimator.rs:101-262) over the device backend
     on a rendered stereo stream of textured planes (synthetic.euroc_scene_stream_device, frames
     resident in HBM): per frame the tracker (6 levels, grid 50, fused radtan unprojection), PnP +
@@ -410,7 +410,7 @@ def measure_pipeline_row(device: int, cpu: bool, n_frames: int = 500, cpu_second
     cams = [Camera.opencv5(*p) for p in s.intrinsics]
 
     def run(frames):
-        be = _StageTimer(DeviceBackend(W, H, cams, 6, 50, MAX_IT, THRESH, 10, 0.05, 0.05, device))
+        be = _StageTimer(DeviceBackend(W, H, cams, 6, 50, MAX_IT, THRESH, 10, 0.05, 0.05, device, ba_cus=ba_cus))
         if native:  # the host logic in C++ (rsvio.estimator.NativeEstimator): the same calls
             est = NativeEstimator(be.be, s.T_B_Cl, s.T_B_Cr, window=10)
             t0 = time.perf_counter()

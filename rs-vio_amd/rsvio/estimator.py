@@ -47,7 +47,7 @@ class DeviceBackend:
     """StereoPatchTracker (+ fused unprojection), MotionTracker and BundleAdjuster on one device."""
 
     def __init__(self, width, height, cameras, levels, grid_size, max_iterations, thresh, window,
-                 translation_threshold, rotation_threshold, device):
+                 translation_threshold, rotation_threshold, device, ba_cus=None):
         from .motion import MotionTracker
         from .tracker import StereoPatchTracker
         self.tracker = StereoPatchTracker(width, height, levels=levels, grid_size=grid_size,
@@ -61,7 +61,8 @@ class DeviceBackend:
         # process needs one stream fewer beside the tracker's (HIP maps streams onto 4 hardware
         # queues per process; PnP queued on the tracker's queue waited behind frame t + 1)
         from ._lib import CuStream
-        self._ba_stream = CuStream(device)
+        # ba_cus: the CUs (rsvio_stream_create's mask bits) of the BA + PnP stream; None: all
+        self._ba_stream = CuStream(device, ba_cus) if ba_cus else CuStream(device)
         self.solver.set_stream(self._ba_stream.ptr)
         self.motion.set_stream(self._ba_stream.ptr)
 
