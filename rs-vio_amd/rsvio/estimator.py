@@ -61,8 +61,18 @@ class DeviceBackend:
         # process needs one stream fewer beside the tracker's (HIP maps streams onto 4 hardware
         # queues per process; PnP queued on the tracker's queue waited behind frame t + 1)
         from ._lib import CuStream
-        # ba_cus: the CUs (rsvio_stream_create's mask bits) of the BA + PnP stream; None: all
-        self._ba_stream = CuStream(device, ba_cus) if ba_cus else CuStream(device)
+        # ba_cus: the CUs (rsvio_stream_create's mask bits) of the BA + PnP stream; None: all of
+        # them -- still through a CU mask: a CU-masked stream gets a hardware queue of its own,
+        # where a plain stream takes the next of the process's 4 round-robin queues and may land
+        # on the tracker's (PnP then waits behind frame t + 1's tracking: 0.23 ms per frame,
+        # 2.5k instead of 3.6k frames/s, profiles/r06z7_config4_ba_cus_ab.txt)
+        if not ba_cus:
+            import ctypes as C
+            from ._lib import check, load
+            n = C.c_int(0)
+            check(load().rsvio_device_info(device, None, 0, C.byref(n)))
+            ba_cus = list(range(n.value))
+        self._ba_stream = CuStream(device, ba_cus)
         self.solver.set_stream(self._ba_stream.ptr)
         self.motion.set_stream(self._ba_stream.ptr)
 

@@ -1,6 +1,6 @@
 """GPU box: only bench.py's config-4 Estimator row (no CPU leg), printed as JSON.
 usage: python tools/pipeline_row.py [frames] [repeats] [ba_cus]   (ba_cus: the BA + PnP stream on the
-last ba_cus mask bits -- ba_cus / 8 CUs of every XCD; 0 or absent: all CUs)"""
+last ba_cus mask bits -- ba_cus / 8 CUs of every XCD; 0 or absent: all CUs, still CU-masked)"""
 import json
 import sys
 from pathlib import Path
