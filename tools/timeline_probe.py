@@ -3,7 +3,7 @@ tracker and BA streams, all relative to the step's first event (the image upload
 the host phases.  Medians over the steps, in microseconds.
   python tools/timeline_probe.py [steps] [order] [graphs]   (order: split | ba-first | frame-first;
                                                             graphs 0: the tracker enqueued directly)
-Tracker stream: img_up (image H2D done), down (the frame done: pyramids, LK and the feature
+Tracker stream: img_up (the images up: rsvio_upload_async, bench.py's default), down (the frame done: pyramids, LK and the feature
 lists' D2H; the kernels' own times come from a rocprofv3 kernel trace).  BA stream: win_up (the window's upload + ba_build_layout done: an event recorded after
 set_problem), solve_end (an event after the solve's last kernel: recorded after ba.finish, so it
 is the stream's position, not a host wait).  Host: when each call returned."""
@@ -28,6 +28,7 @@ def main(steps=80, order="split", graphs=True):
     streams = [CuStream(0, cu_trk), CuStream(0, cu_ba)]
     trk = bench.TrackerWorkload(0, streams[0].ptr)
     trk.graphs = graphs
+    trk.upload_kernel = True  # bench.py's default (--upload kernel: rsvio_upload_async)
     ba = bench.BAWorkload(0, 1, 0, streams[1].ptr)
     trk.enable_pcie()
     dev = torch.device("cuda", 0)
