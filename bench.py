@@ -1167,6 +1167,7 @@ class BAWorkload:
             self.p2p_us = {f"{n}_doubles": round(reduce_scalar(self.ba.p2p_latency_us(200, n), world, "max"), 2)
                            for n in (4, 1600)}
             log(f"[bench] rank {rank}: P2P exchange latency {self.p2p_us} us")
+        self.stream_ptr = stream_ptr
         if stream_ptr:
             self.ba.set_stream(stream_ptr)
         self.ba.set_problem_from(self.prob)
@@ -1256,7 +1257,8 @@ class NativeProtocol:
                     ("d_out", ctypes.c_void_p), ("h_out", ctypes.c_void_p), ("out_bytes", ctypes.c_size_t),
                     ("d_valid", ctypes.c_void_p), ("h_valid", ctypes.c_void_p), ("valid_bytes", ctypes.c_size_t),
                     ("first_step", ctypes.c_int32), ("lk_events", ctypes.c_void_p), ("n_lk_events", ctypes.c_int32),
-                    ("order", ctypes.c_int32), ("phase_us", ctypes.c_void_p)]
+                    ("order", ctypes.c_int32), ("phase_us", ctypes.c_void_p), ("ba_stream", ctypes.c_void_p),
+                    ("tl_events", ctypes.c_void_p), ("n_tl", ctypes.c_int32)]
 
     def __init__(self, trk: "TrackerWorkload", ba: "BAWorkload", state_out, max_steps: int, order: int = 0):
         from rsvio import _lib
@@ -1306,6 +1308,9 @@ class NativeProtocol:
         self.n_ev = n_ev
         self.order = order
         self.phases = None  # a list: each run appends its steps' 7 host phase times (us)
+        self.timeline = None  # a list: each run appends its steps' (window laid out, solve end) (us)
+        self.ba_stream = ba.stream_ptr
+        self._create = create
 
     def run(self, steps: int):
         """`steps` protocol steps from the workloads' current phase and window; advances them."""
@@ -1321,6 +1326,17 @@ class NativeProtocol:
                            trk.k, ctypes.addressof(self.ev_ptrs), self.n_ev, self.order, None)
         ph = (ctypes.c_double * (7 * steps))() if self.phases is not None else None
         setup.phase_us = ctypes.addressof(ph) if ph is not None else None
+        tl = None
+        if self.timeline is not None and self.ba_stream:
+            from rsvio import _lib
+            tl = (ctypes.c_void_p * (3 * steps))()
+            for i in range(3 * steps):
+                e = ctypes.c_void_p()
+                _lib.check(self._create(ctypes.byref(e), 0))  # timing events
+                tl[i] = e.value
+            setup.ba_stream = self.ba_stream
+            setup.tl_events = ctypes.addressof(tl)
+            setup.n_tl = steps
         iters = (ctypes.c_int32 * steps)()
         sms = (ctypes.c_double * steps)()
         sec, npair = ctypes.c_double(0.0), ctypes.c_int32(0)
@@ -1330,6 +1346,14 @@ class NativeProtocol:
             raise RuntimeError(f"rsvio_protocol_run failed: {rc}")
         if ph is not None:
             self.phases += [list(ph[7 * i:7 * i + 7]) for i in range(steps)]
+        if tl is not None:
+            for i in range(steps):
+                w, e = ctypes.c_float(0.0), ctypes.c_float(0.0)
+                self._elapsed(ctypes.byref(w), tl[3 * i], tl[3 * i + 1])
+                self._elapsed(ctypes.byref(e), tl[3 * i], tl[3 * i + 2])
+                self.timeline.append((1e3 * w.value, 1e3 * e.value))
+            for i in range(3 * steps):
+                self._destroy(tl[i])
         trk.k += steps
         trk.slot ^= steps & 1
         ba.k += steps
@@ -1600,6 +1624,7 @@ def main():
         native.run(max(args.warmup, 2))
         if trace is not None:
             native.phases = []
+            native.timeline = []
     else:
         for _ in range(max(args.warmup, 2)):
             protocol_step(False)
@@ -1626,7 +1651,11 @@ def main():
         names = ["upload", "set_problem", "start", "frame_enqueue", "frame_wait", "solve_wait", "state"]
         ph = np.array(native.phases)
         with open(args.trace_steps, "w") as f:
+            tlv = np.array(native.timeline) if native.timeline else None
             json.dump({"driver": "native", "phases": names, "steps_per_rep": args.steps,
+                       "timeline_median_us": ({"window_laid_out": round(float(np.median(tlv[:, 0])), 1),
+                                               "solve_end": round(float(np.median(tlv[:, 1])), 1)}
+                                              if tlv is not None else None),
                        "median_us": [round(float(x), 2) for x in np.median(ph, axis=0)],
                        "p90_us": [round(float(x), 2) for x in np.percentile(ph, 90, axis=0)],
                        "us": [[round(float(x), 1) for x in r] for r in ph]}, f)

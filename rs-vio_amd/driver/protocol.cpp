@@ -99,6 +99,11 @@ struct rsvio_protocol {
     double* phase_us;          // null, or 7 host phase times per step (us): image upload, set_problem,
                                // run_async, frame enqueue, frame wait, rsvio_ba_wait, get_state (order
                                // 1 counts the image upload after set_problem into its first entry)
+    void* ba_stream;           // hipStream_t of the BA handle (for the timeline events)
+    void** tl_events;          // null, or 3 timing hipEvent_t per step for the first n_tl steps: the
+    int32_t n_tl;              // step's start (tracker stream, before the image upload), the window
+                               // laid out (BA stream, after set_problem), the solve's end (BA stream,
+                               // after run_async: the stream's position past the solve's graph)
 };
 
 // Runs `steps` protocol steps; per step the solve's LM iterations and device solve time into
@@ -121,8 +126,12 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
     auto mark = [&](int i) {
         if (ph) tp[i] = clk::now();
     };
+    const bool tl = P->tl_events && P->ba_stream;
+    const hipStream_t bs = static_cast<hipStream_t>(P->ba_stream);
     for (int32_t k = 0; k < steps; ++k) {
         mark(0);
+        const bool tk = tl && k < P->n_tl;
+        if (tk && hipEventRecord(static_cast<hipEvent_t>(P->tl_events[3 * k]), ts) != hipSuccess) return RSVIO_ERR_HIP;
         const rsvio_protocol_frame& f = P->frames[(P->first_phase + k) % P->n_phases];
         const rsvio_protocol_window& w = P->windows[(P->first_window + k) % P->n_windows];
         auto up = [&]() -> int {
@@ -136,6 +145,8 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
         int rc = A.set_problem(P->ba, w.n_kf, w.pose7, w.kf_fixed, w.n_lm, w.p_W, w.n_obs, w.obs_lm, w.obs_kf,
                                w.obs_cam, w.obs_uv, w.T_C_B2);
         if (rc) return rc;
+        if (tk && hipEventRecord(static_cast<hipEvent_t>(P->tl_events[3 * k + 1]), bs) != hipSuccess)
+            return RSVIO_ERR_HIP;
         mark(2);
         if (P->order == 1) {
             if (up()) return RSVIO_ERR_HIP;
@@ -146,6 +157,8 @@ int rsvio_protocol_run(const rsvio_protocol* P, int32_t steps, int32_t* iters_ou
             }
         }
         if ((rc = A.run_async(P->ba, P->cfg))) return rc;
+        if (tk && hipEventRecord(static_cast<hipEvent_t>(P->tl_events[3 * k + 2]), bs) != hipSuccess)
+            return RSVIO_ERR_HIP;
         mark(3);
         if (P->lk_events && (P->first_step + k) % 4 == 0 && n_lk < P->n_lk_events) {
             // the frame enqueued directly, the LK launch between two timing events
@@ -196,7 +209,8 @@ int rsvio_protocol_layout(int64_t* out, int32_t n) {
                          (int64_t)offsetof(rsvio_protocol_window, T_C_B2), (int64_t)offsetof(rsvio_protocol_frame, batches),
                          (int64_t)offsetof(rsvio_protocol, first_step), (int64_t)offsetof(rsvio_protocol, lk_events),
                          (int64_t)offsetof(rsvio_protocol, n_lk_events), (int64_t)offsetof(rsvio_protocol, thresh),
-                         (int64_t)offsetof(rsvio_protocol, valid_bytes), (int64_t)offsetof(rsvio_protocol, order), (int64_t)offsetof(rsvio_protocol, phase_us)};
+                         (int64_t)offsetof(rsvio_protocol, valid_bytes), (int64_t)offsetof(rsvio_protocol, order), (int64_t)offsetof(rsvio_protocol, phase_us),
+                         (int64_t)offsetof(rsvio_protocol, n_tl)};
     const int32_t m = (int32_t)(sizeof v / sizeof v[0]);
     for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
     return m;

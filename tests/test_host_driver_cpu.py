@@ -20,7 +20,7 @@ def test_driver_loads_and_struct_layout_matches():
     want = [ctypes.sizeof(N.Window), ctypes.sizeof(N.Frame), ctypes.sizeof(N.Api), ctypes.sizeof(N.Setup),
             N.Window.T_C_B2.offset, N.Frame.batches.offset, N.Setup.first_step.offset, N.Setup.lk_events.offset,
             N.Setup.n_lk_events.offset, N.Setup.thresh.offset, N.Setup.valid_bytes.offset,
-            N.Setup.order.offset, N.Setup.phase_us.offset]
+            N.Setup.order.offset, N.Setup.phase_us.offset, N.Setup.n_tl.offset]
     assert n == len(want)
     assert list(out[:n]) == want
 
