@@ -733,10 +733,21 @@ def setup_dist(same_device: bool = False):
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        if same_device:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # the communication libraries' own connection messages (gloo prints "[Gloo] Rank r is
+        # connected to ..." on stdout) go to stderr: rank 0's stdout carries the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if same_device:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()  # (the mesh is connected here at the latest)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
