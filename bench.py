@@ -671,6 +671,16 @@ def pin_main_thread(mode: str) -> str:
         return f"failed ({e})"
 
 
+def parse_cpulist(text: str) -> set:
+    """A Linux CPU list ("0-63,128-191") as a set of CPU numbers."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
 def numa_local(device: int) -> str:
     """--numa-local: every thread of the process onto the CPUs of the GPU's NUMA node (those the
     process may use), as a deployment places a GPU's host process -- the pinned staging, the
@@ -684,11 +694,7 @@ def numa_local(device: int) -> str:
         node = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
         if node < 0:
             return "off (no NUMA node)"
-        cpus = set()
-        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
-            a, _, b = part.partition("-")
-            cpus.update(range(int(a), int(b or a) + 1))
-        cpus &= os.sched_getaffinity(0)
+        cpus = parse_cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()) & os.sched_getaffinity(0)
         if not cpus:
             return "off (no allowed CPU on the node)"
         for t in os.listdir("/proc/self/task"):
