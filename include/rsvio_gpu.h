@@ -53,7 +53,8 @@ int rsvio_stream_destroy(void* stream);
 /* Host-to-device copy of page-locked host memory (hipHostMalloc / hipHostRegister) by a kernel on
  * `stream` instead of a copy engine: the next kernel on the stream starts without the copy-engine ->
  * compute-queue hand-off (how bench.py's protocol step uploads the frame's images).  A pageable or
- * non-16-byte-aligned source or destination takes hipMemcpyAsync.  No reference counterpart. */
+ * non-16-byte-aligned source or destination takes hipMemcpyAsync.  As with hipMemcpyAsync, the source
+ * must stay valid and unchanged until the stream has passed the copy.  No reference counterpart. */
 int rsvio_upload_async(void* d_dst, const void* h_src, size_t bytes, void* stream);
 
 /* =============================== HP-T: patch tracker =============================== */
